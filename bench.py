@@ -1,0 +1,282 @@
+"""Benchmark: MPixels/sec decoded, 4K baseline JPEG 4:2:0, fused dequant + IDCT
++ upsample + YCbCr->RGBA on MI355X (BASELINE.json configs[1]).
+
+A step = one launch of the device plan over the batch (64 synthetic 4096x4096
+q75 4:2:0 frames per GPU, coefficient grids resident in HBM, RGBA written to
+HBM).  Host entropy decoding happens before the timed region (it is reported
+separately as host_entropy_mpix_s).  Multi-GPU: one process per GPU
+(torch.distributed over RCCL), each rank decodes its own 64 frames (weak
+scaling, no data-path collective); `--gather` adds an RCCL gather of every
+rank's RGBA to rank 0, timed separately.
+
+The PNG workload (configs[2]: 64 x 4096^2 tc8, mixed Sub/Up/Avg/Paeth rows)
+is measured in the same run and reported under "png" (disable: --no-png).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MEASURED_COPY_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--images", type=int, default=64, help="frames per GPU")
+    ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic frames per GPU (slots cycle them)")
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--quality", type=int, default=75)
+    ap.add_argument("--no-png", action="store_true")
+    ap.add_argument("--png-only", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
+    ap.add_argument("--gather", action="store_true", help="RCCL-gather all RGBA outputs to rank 0 (timed apart)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/)")
+    return ap.parse_args()
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def timed_steps(torch, dist, launch, steps, warmup, ws):
+    """W untimed steps; K timed steps bracketed by barrier + synchronize; HIP
+    events on the launch stream give the average per-launch kernel time."""
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        launch(stream.cuda_stream)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        launch(stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / steps
+    if ws > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    return wall, kern_ms
+
+
+def cpu_baseline_jpeg(data: bytes, seconds: float):
+    """The oracle (C restatement of the reference algorithm, -O2, scalar) on a
+    bounded sample: full jpeg.decode + Image.rgbaPixels of the same 4K frame,
+    on all host cores (one frame per thread) and on one core."""
+    import numpy as np  # noqa: F401
+    import oracle_py as O
+
+    O.lib()
+    cores = min(16, os.cpu_count() or 1)
+
+    def one():
+        img = O.jpeg_decode(data)
+        img.rgba_pixels()
+        return img.width * img.height
+
+    t0 = time.perf_counter()
+    px1 = one()
+    t1 = time.perf_counter() - t0
+    single = px1 / t1 / 1e6
+    # all cores: threads (ctypes releases the GIL inside the oracle)
+    budget = max(seconds - t1, 1.0)
+    per_thread = max(1, int(budget / t1 / 1.5))
+    done = [0] * cores
+
+    def worker(i):
+        for _ in range(per_thread):
+            done[i] += one()
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(cores)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    tm = time.perf_counter() - t0
+    multi = sum(done) / tm / 1e6
+    return {"value": round(multi, 2), "unit": "MPixels/sec", "cores": cores, "kind": "port",
+            "sample": f"{cores * per_thread + 1} x oracle jpeg.decode+rgbaPixels of one 4096x4096 q75 4:2:0 frame "
+                      f"({tm + t1:.1f}s)", "single_core_mpix_s": round(single, 2)}
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_env()
+    import numpy as np
+    import torch
+
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from tools import synthetic as S
+
+    import zpix_amd
+    from zpix_amd import device, jpeg, png
+
+    ctx = zpix_amd.context.default(dev)
+    W = H = args.size
+    result = {}
+    # ------------------------------------------------------------ JPEG (headline)
+    if not args.png_only:
+        t0 = time.perf_counter()
+        datas = [S.jpeg_420(rank * args.distinct + j, W, H, args.quality) for j in range(args.distinct)]
+        t_gen = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        coeffs = [jpeg.Coefficients(d) for d in datas]
+        t_ent = time.perf_counter() - t0
+        host_entropy = args.distinct * W * H / t_ent / 1e6
+        log(f"[rank {rank}] generated {args.distinct} frames in {t_gen:.1f}s; host entropy "
+            f"{host_entropy:.1f} MPix/s (1 thread)")
+        slots = [i % args.distinct for i in range(args.images)]
+        batch = device.JpegBatch(coeffs, slots=slots, output="rgba", ctx=ctx)
+        # parity gate before timing: slot 0 vs the oracle (rank 0, cheap at 4K)
+        if rank == 0:
+            import oracle_py as O
+
+            batch.launch(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            want = O.jpeg_decode(datas[0]).rgba_pixels()
+            ok = torch.equal(batch.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want))
+            if not ok:
+                raise SystemExit("parity failure: GPU RGBA != oracle for frame 0")
+        wall, kern_ms = timed_steps(torch, dist, batch.launch, args.steps, args.warmup, ws)
+        px_per_step = batch.pixels * ws
+        value = px_per_step * args.steps / wall / 1e6
+        launch_bytes = batch.bytes
+        achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("images") == args.images and tj.get("size") == args.size and tj.get("kernel", "").startswith("jpeg_rgba"):
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        gather = None
+        if args.gather and ws > 1:
+            out = batch.out_arena
+            bufs = [torch.empty_like(out) for _ in range(ws)] if rank == 0 else None
+            torch.cuda.synchronize()
+            dist.barrier()
+            g0 = time.perf_counter()
+            dist.gather(out, gather_list=bufs, dst=0)
+            torch.cuda.synchronize()
+            gt = time.perf_counter() - g0
+            gather = {"bytes": int(out.numel() * (ws - 1)), "seconds": round(gt, 4),
+                      "GB_s": round(out.numel() * (ws - 1) / gt / 1e9, 1)}
+        result = {
+            "metric": "MPixels/sec decoded (4K baseline JPEG 4:2:0) at 1/8 GPU; % HBM roofline",
+            "value": round(value, 1),
+            "unit": "MPixels/sec",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32 (int16 coefficients in, u8 RGBA out)",
+            "data": f"synthetic: {args.images} x {W}x{H} q{args.quality} 4:2:0 baseline JPEG per GPU "
+                    f"({args.distinct} distinct frames, Pillow), host-entropy-decoded before timing, "
+                    "coefficients resident in HBM",
+            "config": {"workload": f"{args.images}x {W}x{H} baseline 4:2:0 JPEG -> RGBA (fused dequant+IDCT+"
+                                   "upsample+YCbCr->RGB), configs[1]",
+                       "images_per_gpu": args.images, "width": W, "height": H, "quality": args.quality,
+                       "parallelism": f"image-sharded x{ws}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "frac_of_measured_copy": round(achieved / MEASURED_COPY_GBS, 4),
+                         "kernel": "jpeg_rgba_kernel", "kernel_ms_per_launch": round(kern_ms, 4),
+                         "algorithmic_bytes_per_launch": launch_bytes},
+            "host_entropy_mpix_s": round(host_entropy, 1),
+        }
+        if gather:
+            result["gather"] = gather
+        del batch
+        torch.cuda.empty_cache()
+    # ------------------------------------------------------------ PNG (configs[2])
+    if not args.no_png:
+        t0 = time.perf_counter()
+        pdatas = [S.png_tc8_mixed(rank * args.distinct + j, W, H) for j in range(args.distinct)]
+        t_gen = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        streams = [png.Stream(d) for d in pdatas]
+        t_inf = time.perf_counter() - t0
+        log(f"[rank {rank}] PNG generated in {t_gen:.1f}s, host inflate {args.distinct * W * H / t_inf / 1e6:.1f} MPix/s")
+        slots = [i % args.distinct for i in range(args.images)]
+        pb = device.PngBatch(streams, slots=slots, ctx=ctx)
+        if rank == 0:
+            raw, _ = S.png_filtered_tc8(0, W, H)
+            pb.launch(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = pb.output_tensor(0).cpu().numpy().reshape(H, W, 4)
+            if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
+                raise SystemExit("parity failure: GPU PNG unfilter != source pixels")
+        wall, kern_ms = timed_steps(torch, dist, pb.launch, max(3, args.steps // 2), 1, ws)
+        steps = max(3, args.steps // 2)
+        pv = pb.pixels * ws * steps / wall / 1e6
+        ach = pb.bytes / (kern_ms * 1e-3) / 1e9
+        pres = {"metric": "MPixels/sec decoded (4K truecolor-8 PNG, mixed Sub/Up/Avg/Paeth)", "value": round(pv, 1),
+                "unit": "MPixels/sec", "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
+                "config": {"workload": f"{args.images}x {W}x{H} tc8 PNG unfilter -> RGBA, configs[2]"},
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "png_unfilter_kernel",
+                             "kernel_ms_per_launch": round(kern_ms, 3), "algorithmic_bytes_per_launch": pb.bytes},
+                "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1)}
+        if result:
+            result["png"] = pres
+        else:
+            result = dict(pres, n_gpus=ws, warmup=1, higher_is_better=True, scaling="weak", vs_baseline=None,
+                          dtype="u8", data="synthetic PNG")
+        del pb
+    # ------------------------------------------------------------ CPU baseline (rank 0, N=1)
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.png_only:
+        result["cpu_baseline"] = cpu_baseline_jpeg(datas[0], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,354 @@
+/*
+ * zpix_amd.h — C-ABI of the MI355X-native decode path for braheezy/zpix.
+ *
+ * The reference is a pure-Zig library; its API is Zig-ABI (allocator + error
+ * union).  This header is the C-ABI shim a Zig host binds with `extern "c"`
+ * (see INTEGRATION.md).  Every entry point cites the reference interface it
+ * replaces.  Conventions that mirror the reference:
+ *   - Ownership: the caller passes an allocator (zpx_allocator, the C shape of
+ *     std.mem.Allocator; NULL = malloc/free).  A returned zpx_image owns
+ *     `pixels` (and `palette` for Paletted) allocated from it; release with
+ *     zpx_image_free (Image.free, src/image/image.zig:68-99).
+ *   - Errors: int return, 0 = ok, otherwise a ZPX_E_* code whose
+ *     zpx_error_name() is the reference's Zig error name (e.g.
+ *     "UnexpectedEof", "BadRSTMarker", "InvalidFilterType").  No exception or
+ *     abort crosses the ABI.
+ *   - Threading: a zpx_ctx (one per GPU) is not shared by host threads
+ *     concurrently; calls on different contexts are independent.
+ *
+ * Layer split: serial entropy decoding (Huffman, zlib
+ * inflate) runs on the host inside this library; dequant + IDCT + level
+ * shift, chroma upsample + YCbCr->RGB, PNG unfilter + pixel store + Adam7
+ * merge, and Image.rgbaPixels run as HIP kernels on gfx950.  There is no CPU
+ * fallback: if the device path cannot run, calls fail with ZPX_E_HIP or
+ * ZPX_E_UNSUPPORTED.
+ */
+#ifndef ZPIX_AMD_H
+#define ZPIX_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZPX_ABI_VERSION 1
+
+typedef struct zpx_ctx zpx_ctx;
+
+/* ---------------------------------------------------------------------- */
+/* errors                                                                  */
+/* ---------------------------------------------------------------------- */
+/* Status codes.  Every name is the reference's Zig error name (the JPEG set
+ * from src/jpeg/decoder.zig, the PNG set from src/png/decoder.zig), plus
+ * Unsupported / Panic / Hip / InvalidArgument for conditions of the device
+ * path itself.  zpx_error_name(code) returns the name. */
+#define ZPX_ERROR_LIST(X) \
+    X(Ok, OK) \
+    X(UnexpectedEof, UNEXPECTED_EOF) \
+    X(InvalidSOIMarker, INVALID_SOI_MARKER) \
+    X(ShortSegmentLength, SHORT_SEGMENT_LENGTH) \
+    X(UnknownMarker, UNKNOWN_MARKER) \
+    X(UnsupportedMarker, UNSUPPORTED_MARKER) \
+    X(MultipleSofMarkers, MULTIPLE_SOF_MARKERS) \
+    X(NumberComponents, NUMBER_COMPONENTS) \
+    X(Precision, PRECISION) \
+    X(SofWrongLength, SOF_WRONG_LENGTH) \
+    X(RepeatedComponentIdentifier, REPEATED_COMPONENT_IDENTIFIER) \
+    X(BadTqValue, BAD_TQ_VALUE) \
+    X(LumaChromaSubSamplingRatio, LUMA_CHROMA_SUB_SAMPLING_RATIO) \
+    X(DriWrongLength, DRI_WRONG_LENGTH) \
+    X(BadPqValue, BAD_PQ_VALUE) \
+    X(DqtWrongLength, DQT_WRONG_LENGTH) \
+    X(MissingFF00, MISSING_FF00) \
+    X(UninitializedHuffmanTable, UNINITIALIZED_HUFFMAN_TABLE) \
+    X(BadHuffmanCode, BAD_HUFFMAN_CODE) \
+    X(DhtWrongLength, DHT_WRONG_LENGTH) \
+    X(BadTcValue, BAD_TC_VALUE) \
+    X(BadThValue, BAD_TH_VALUE) \
+    X(HuffZeroLength, HUFF_ZERO_LENGTH) \
+    X(HuffTooLong, HUFF_TOO_LONG) \
+    X(MissingSosMarker, MISSING_SOS_MARKER) \
+    X(SosWrongLength, SOS_WRONG_LENGTH) \
+    X(UnknownComponentSelector, UNKNOWN_COMPONENT_SELECTOR) \
+    X(BadTdValue, BAD_TD_VALUE) \
+    X(BadTaValue, BAD_TA_VALUE) \
+    X(SamplingFactorsTooLarge, SAMPLING_FACTORS_TOO_LARGE) \
+    X(BadSpectralSelection, BAD_SPECTRAL_SELECTION) \
+    X(ProgressiveACCoefficientsForMoreThanOneComponent, PROGRESSIVE_AC_COEFFICIENTS_FOR_MORE_THAN_ONE_COMPONENT) \
+    X(BadSuccessiveApproximation, BAD_SUCCESSIVE_APPROXIMATION) \
+    X(ExcessiveDCComponent, EXCESSIVE_DC_COMPONENT) \
+    X(UnexpectedHuffmanCode, UNEXPECTED_HUFFMAN_CODE) \
+    X(TooManyCoefficients, TOO_MANY_COEFFICIENTS) \
+    X(BadRSTMarker, BAD_RST_MARKER) \
+    X(UnsupportedComponent, UNSUPPORTED_COMPONENT) \
+    X(UnsupportedColorModel, UNSUPPORTED_COLOR_MODEL) \
+    X(InvalidPngHeader, INVALID_PNG_HEADER) \
+    X(ChunkOrderInHeaderError, CHUNK_ORDER_IN_HEADER_ERROR) \
+    X(ChunkOrderPlteError, CHUNK_ORDER_PLTE_ERROR) \
+    X(ChunkOrderIdatError, CHUNK_ORDER_IDAT_ERROR) \
+    X(ChunkOrderTrns1Error, CHUNK_ORDER_TRNS1_ERROR) \
+    X(ChunkOrderTrns2Error, CHUNK_ORDER_TRNS2_ERROR) \
+    X(ChunkOrderTrns3Error, CHUNK_ORDER_TRNS3_ERROR) \
+    X(ChunkOrderIendError, CHUNK_ORDER_IEND_ERROR) \
+    X(InvalidIHDRLength, INVALID_IHDR_LENGTH) \
+    X(UnsupportedCompressionMethod, UNSUPPORTED_COMPRESSION_METHOD) \
+    X(UnsupportedFilterMethod, UNSUPPORTED_FILTER_METHOD) \
+    X(UnsupportedInterlaceMethod, UNSUPPORTED_INTERLACE_METHOD) \
+    X(InvalidDimension, INVALID_DIMENSION) \
+    X(DimensionOverflow, DIMENSION_OVERFLOW) \
+    X(InvalidColorType, INVALID_COLOR_TYPE) \
+    X(InvalidColorTypeDepthCombo, INVALID_COLOR_TYPE_DEPTH_COMBO) \
+    X(UnsupportedBitDepth, UNSUPPORTED_BIT_DEPTH) \
+    X(EmptyIdatData, EMPTY_IDAT_DATA) \
+    X(BadTrnsLength, BAD_TRNS_LENGTH) \
+    X(TrnsColorTypeMismatch, TRNS_COLOR_TYPE_MISMATCH) \
+    X(BadPlteLength, BAD_PLTE_LENGTH) \
+    X(PlteColorTypeMismatch, PLTE_COLOR_TYPE_MISMATCH) \
+    X(InvalidFilterType, INVALID_FILTER_TYPE) \
+    X(InvalidChecksum, INVALID_CHECKSUM) \
+    X(EndOfStream, END_OF_STREAM) \
+    X(ReadFailed, READ_FAILED) \
+    X(InvalidImageDimensions, INVALID_IMAGE_DIMENSIONS) \
+    X(OutOfMemory, OUT_OF_MEMORY) \
+    X(Unsupported, UNSUPPORTED) \
+    X(Panic, PANIC) \
+    X(Hip, HIP) \
+    X(InvalidArgument, INVALID_ARGUMENT) \
+    X(FileNotFound, FILE_NOT_FOUND) \
+    X(UnknownImageFormat, UNKNOWN_IMAGE_FORMAT)
+
+enum zpx_status {
+#define ZPX_ENUM_(name, up) ZPX_E_##up,
+    ZPX_ERROR_LIST(ZPX_ENUM_)
+#undef ZPX_ENUM_
+    ZPX_E__COUNT
+};
+#define ZPX_OK ZPX_E_OK
+/* Name of any status code ("Ok", "UnexpectedEof", ... as in the reference). */
+const char *zpx_error_name(int code);
+/* Detail message of the last failure on this context (never NULL). */
+const char *zpx_last_error(const zpx_ctx *ctx);
+
+/* ---------------------------------------------------------------------- */
+/* context                                                                 */
+/* ---------------------------------------------------------------------- */
+/* One context per GPU: owns a compute stream, a copy stream, pinned staging
+ * and device scratch.  Replaces nothing in the reference (it has no device). */
+int zpx_ctx_create(int device, zpx_ctx **out);
+void zpx_ctx_destroy(zpx_ctx *ctx);
+/* The context's compute stream (a hipStream_t). */
+void *zpx_ctx_stream(zpx_ctx *ctx);
+int zpx_ctx_device(const zpx_ctx *ctx);
+/* Blocks until all work queued by this context is complete. */
+int zpx_ctx_synchronize(zpx_ctx *ctx);
+
+/* std.mem.Allocator in C form. alloc returns NULL on failure. */
+typedef struct zpx_allocator {
+    void *(*alloc)(void *user, size_t len);
+    void (*free)(void *user, void *ptr, size_t len);
+    void *user;
+} zpx_allocator;
+
+/* ---------------------------------------------------------------------- */
+/* image.Image                                                             */
+/* ---------------------------------------------------------------------- */
+/* Image tags, src/image/image.zig:24-34 */
+enum zpx_kind {
+    ZPX_GRAY = 0,
+    ZPX_GRAY16 = 1,
+    ZPX_YCBCR = 2,
+    ZPX_RGBA = 3,
+    ZPX_RGBA64 = 4,
+    ZPX_NRGBA = 5,
+    ZPX_NRGBA64 = 6,
+    ZPX_CMYK = 7,
+    ZPX_PALETTED = 8,
+};
+/* YCbCrSubsample, src/image/image.zig:465-472 */
+enum zpx_subsample {
+    ZPX_RATIO444 = 0,
+    ZPX_RATIO422 = 1,
+    ZPX_RATIO420 = 2,
+    ZPX_RATIO440 = 3,
+    ZPX_RATIO411 = 4,
+    ZPX_RATIO410 = 5,
+};
+/* A palette Color: the .rgba (model 0) or .nrgba (model 1) arm of
+ * color.Color (src/color/color.zig:13-23). */
+typedef struct zpx_color {
+    uint8_t r, g, b, a;
+    uint8_t model;
+    uint8_t pad[3];
+} zpx_color;
+
+/* image.Image (src/image/image.zig:24-34 + the concrete pixel buffers
+ * :133-890).  Pixel layouts are the reference's: RGBA/NRGBA/CMYK 4 B/px,
+ * RGBA64/NRGBA64 8 B/px big-endian per channel, Gray 1, Gray16 2 (BE),
+ * Paletted 1 (+palette).  YCbCr planes are views into `pixels`. */
+typedef struct zpx_image {
+    int32_t kind;
+    int32_t min_x, min_y, max_x, max_y;
+    uint8_t *pixels;
+    size_t pixels_len;
+    size_t stride;
+    size_t y_off, cb_off, cr_off;  /* YCbCr */
+    size_t y_stride, c_stride;     /* YCbCr */
+    int32_t subsample;             /* YCbCr */
+    zpx_color *palette;            /* Paletted */
+    int32_t palette_len;
+} zpx_image;
+
+/* Image.free, src/image/image.zig:68-99 */
+void zpx_image_free(const zpx_allocator *al, zpx_image *img);
+
+/* Image.rgbaPixels, src/image/image.zig:103-130: 8-bit RGBA, 4*dX*dY bytes,
+ * caller-owned (allocated from al).  Runs the conversion on the GPU. */
+int zpx_image_rgba_pixels(zpx_ctx *ctx, const zpx_allocator *al, const zpx_image *img,
+                          uint8_t **out, size_t *out_len);
+
+/* ---------------------------------------------------------------------- */
+/* codecs (host entropy decode + device pixel loops)                       */
+/* ---------------------------------------------------------------------- */
+/* jpeg.decode / jpeg.loadFromBuffer: src/jpeg/decoder.zig:155-176,
+ * src/jpeg/root.zig:10-15.  Returns .Gray, .YCbCr, .RGBA (Adobe RGB) or .CMYK
+ * exactly as decodeInner's output select (decoder.zig:357-372). */
+int zpx_jpeg_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                    zpx_image *out);
+/* jpeg.load, src/jpeg/root.zig:36-53 */
+int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out);
+/* jpeg.probeBuffer, src/jpeg/root.zig:17-21 */
+int zpx_jpeg_probe_buffer(const uint8_t *buf, size_t len);
+
+/* jpeg.decode followed by Image.rgbaPixels, fused on the device (one kernel:
+ * dequant + IDCT + level shift + upsample + YCbCr->RGB). */
+int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                         uint8_t **rgba, size_t *rgba_len, uint32_t *width, uint32_t *height);
+
+/* png.decode / png.loadFromBuffer: src/png/decoder.zig:143-221,
+ * src/png/root.zig:29-34 */
+int zpx_png_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                   zpx_image *out);
+/* png.load, src/png/root.zig:13-27 */
+int zpx_png_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out);
+/* png.probeBuffer, src/png/root.zig:37-40 */
+int zpx_png_probe_buffer(const uint8_t *buf, size_t len);
+
+/* zpix.fromBuffer / zpix.fromFilePath, src/root.zig:24-40 (PNG and JPEG;
+ * QOI/BMP are out of scope and return ZPX_E_UNSUPPORTED). */
+int zpx_from_buffer(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                    zpx_image *out);
+int zpx_from_file_path(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out);
+
+/* ---------------------------------------------------------------------- */
+/* device-level plans (device pointers, asynchronous, graph-capturable)    */
+/* ---------------------------------------------------------------------- */
+typedef struct zpx_plan zpx_plan;
+
+/* What a JPEG frame's reconstruct writes. */
+enum zpx_jpeg_output {
+    ZPX_JPEG_PLANES = 0, /* reconstructBlock into Y/Cb/Cr/K planes (decoder.zig:1553-1634) */
+    ZPX_JPEG_RGBA = 1,   /* planes + Image.rgbaPixels fused (RGBA8, stride rgba_stride) */
+};
+/* Which blocks of a component are reconstructed. */
+enum zpx_block_rule {
+    ZPX_BLOCKS_ALL = 0,         /* baseline interleaved scan: every MCU block */
+    ZPX_BLOCKS_PROGRESSIVE = 1, /* by*v<H && bx*h<W, decoder.zig:1649-1651 */
+    ZPX_BLOCKS_SCAN = 2,        /* non-interleaved baseline scan: bx*8<W && by*8<H (:1334) */
+    ZPX_BLOCKS_NONE = 3,        /* component never scanned: plane stays zero */
+};
+/* Colour handling of the fused RGBA output. */
+enum zpx_jpeg_color {
+    ZPX_JPEG_COLOR_YCBCR = 0, /* Color.toRGBA .ycbcr (color.zig:90-113) */
+    ZPX_JPEG_COLOR_RGB = 1,   /* Adobe/RGB ids: convertToRGB (decoder.zig:751-783) */
+    ZPX_JPEG_COLOR_GRAY = 2,  /* 1 component: .gray (color.zig:122-126) */
+};
+
+/* One JPEG frame after host entropy decoding: coefficient grids
+ * (processSos accumulate form, decoder.zig:1340-1345) + frame geometry. */
+typedef struct zpx_jpeg_frame {
+    uint32_t width, height;
+    int32_t n_comp;          /* 1, 3 or 4 */
+    int32_t h[4], v[4];      /* sampling factors after processSof (decoder.zig:490-618) */
+    int32_t mxx, myy;        /* MCU grid (decoder.zig:1262-1263) */
+    int32_t rule[4];         /* zpx_block_rule per component */
+    int32_t coeff_bits;      /* 16 or 32 */
+    int32_t narrow;          /* 1 if max|coef*q| <= 16384 for every component */
+    int32_t color;           /* zpx_jpeg_color (fused output only) */
+    const void *coeffs[4];   /* DEVICE: (mxx*h) x (myy*v) blocks, 64 natural-order coefs each */
+    int32_t qt[4][64];       /* per component, NATURAL order (unzig applied) */
+    uint8_t *planes[4];      /* DEVICE, ZPX_JPEG_PLANES: plane base per component */
+    size_t strides[4];
+    uint8_t *rgba;           /* DEVICE, ZPX_JPEG_RGBA */
+    size_t rgba_stride;
+} zpx_jpeg_frame;
+
+/* Uploads the frame descriptors once; zpx_plan_launch then only enqueues
+ * kernels (no host allocation or sync, so it can be captured in a hipGraph). */
+int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, int n_frames, int output,
+                         zpx_plan **out);
+
+/* PNG ColorBitDepth, src/png/decoder.zig:88-118 */
+enum zpx_png_depth {
+    ZPX_PNG_G1 = 1, ZPX_PNG_G2, ZPX_PNG_G4, ZPX_PNG_G8, ZPX_PNG_GA8, ZPX_PNG_TC8,
+    ZPX_PNG_P1, ZPX_PNG_P2, ZPX_PNG_P4, ZPX_PNG_P8, ZPX_PNG_TCA8, ZPX_PNG_G16,
+    ZPX_PNG_GA16, ZPX_PNG_TC16, ZPX_PNG_TCA16,
+};
+/* Readable bytes the device input must have past its last filtered row. */
+#define ZPX_PNG_INPUT_PAD 64
+
+/* One PNG image after host inflate (parseIdat, png/decoder.zig:404-545). */
+typedef struct zpx_png_frame {
+    uint32_t width, height;
+    int32_t depth;           /* zpx_png_depth */
+    int32_t interlace;       /* 0 none, 1 Adam7 */
+    int32_t use_transparent; /* tRNS colour key (png/decoder.zig:547-602) */
+    uint8_t transparent[6];
+    uint8_t pad[2];
+    const uint8_t *filtered; /* DEVICE: inflated stream, filter byte per row, all passes */
+    uint8_t *out;            /* DEVICE: pixels of the image type readImagePass allocates */
+    size_t out_stride;
+    int32_t *max_index;      /* DEVICE, paletted only: receives max palette index (or NULL) */
+} zpx_png_frame;
+
+/* Unfilter (Sub/Up/Avg/Paeth) + per-depth pixel store (+ Adam7 merge) of
+ * readImagePass (png/decoder.zig:649-1149, 1289-1373).  Filter bytes must be
+ * valid (<= 4): the host checks them (InvalidFilterType) before planning. */
+int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames, zpx_plan **out);
+
+/* Enqueue the plan's kernels on `stream` (NULL = the context's stream). */
+int zpx_plan_launch(zpx_plan *plan, void *stream);
+/* Algorithmic bytes (read + written) one launch of the plan moves. */
+uint64_t zpx_plan_bytes(const zpx_plan *plan);
+/* Number of kernel launches one zpx_plan_launch enqueues. */
+int zpx_plan_kernel_count(const zpx_plan *plan);
+void zpx_plan_destroy(zpx_plan *plan);
+
+/* Image.rgbaPixels on device memory: img->pixels / img->palette are DEVICE
+ * pointers; out is a DEVICE buffer of 4*dX*dY bytes. */
+int zpx_dev_rgba_pixels(zpx_ctx *ctx, const zpx_image *img, uint8_t *out, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* host entropy stage exposed for batching / parity                        */
+/* ---------------------------------------------------------------------- */
+typedef struct zpx_jpeg_coeffs zpx_jpeg_coeffs;
+/* Runs the host half of jpeg.decode (markers, DHT/DQT/SOF/SOS, Huffman,
+ * progressive refinement) and keeps the coefficient grids in pinned memory. */
+int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out);
+/* Fills a frame descriptor (host pointers for coeffs) from decoded coefficients. */
+int zpx_jpeg_coeffs_frame(const zpx_jpeg_coeffs *c, zpx_jpeg_frame *frame,
+                          size_t *coeff_bytes_per_comp /* [4] */);
+void zpx_jpeg_coeffs_free(zpx_jpeg_coeffs *c);
+
+typedef struct zpx_png_stream zpx_png_stream;
+/* Host half of png.decode: chunk parse + CRC + inflate into pinned memory. */
+int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out);
+int zpx_png_stream_frame(const zpx_png_stream *s, zpx_png_frame *frame, size_t *filtered_len);
+const uint8_t *zpx_png_stream_data(const zpx_png_stream *s);
+void zpx_png_stream_free(zpx_png_stream *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZPIX_AMD_H */

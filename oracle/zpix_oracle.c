@@ -937,7 +937,9 @@ static int jd_process_sos(zo_jdec *d, int32_t n)
                         if (bx * 8 >= (int32_t)d->width || by * 8 >= (int32_t)d->height) continue;
                     }
                     size_t bidx = (size_t)by * mxx * hi + bx;
-                    if (accumulate) memcpy(b, d->prog[ci] + 64 * bidx, sizeof(b));
+                    /* progressive loads the partial block (:1340-1343); baseline starts
+                     * from an empty block (:1344) even when only accumulating */
+                    if (d->progressive) memcpy(b, d->prog[ci] + 64 * bidx, sizeof(b));
                     else memset(b, 0, sizeof(b));
 
                     if (ah != 0) {

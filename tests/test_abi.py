@@ -1,0 +1,207 @@
+"""CPU-side checks of the drop-in boundary and the host (serial) stages.
+
+- libzpix_amd.so loads and exports every function include/zpix_amd.h declares;
+- error codes map 1:1 onto the reference's error names;
+- the product's host JPEG entropy stage produces the oracle's coefficient
+  grids for every fixture (and the same error names for malformed input);
+- the product's host PNG stage (chunks, CRC, inflate, filter-byte checks)
+  yields the exact filtered stream and the reference's error names.
+No compute kernel runs here (no GPU in this container).
+"""
+import glob
+import os
+import re
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import ROOT, golden, read
+from tools import synthetic as S
+
+zpix_amd = pytest.importorskip("zpix_amd")
+from zpix_amd import _lib  # noqa: E402
+from zpix_amd import jpeg as J  # noqa: E402
+from zpix_amd import png as P  # noqa: E402
+
+HEADER = os.path.join(ROOT, "include", "zpix_amd.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(zpx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declarations_match_exports():
+    assert declared_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+
+
+def test_error_names_match_reference():
+    L = _lib.lib()
+    assert L.zpx_error_name(0) == b"Ok"
+    names = [L.zpx_error_name(i).decode() for i in range(80)]
+    for ref_name in ["UnexpectedEof", "InvalidSOIMarker", "BadRSTMarker", "MissingFF00", "BadHuffmanCode",
+                     "InvalidFilterType", "InvalidChecksum", "EmptyIdatData", "InvalidPngHeader",
+                     "InvalidColorTypeDepthCombo", "UnsupportedMarker"]:
+        assert ref_name in names, ref_name
+    # the oracle uses the same names for the shared prefix of codes
+    for i in range(1, 66):
+        assert names[i] == O.error_name(i)
+
+
+def test_ctx_create_without_gpu_fails_cleanly():
+    import ctypes as C
+
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    assert _lib.lib().zpx_ctx_create(0, C.byref(h)) == list(map(bytes.decode, [_lib.lib().zpx_error_name(i) for i in range(80)])).index("Hip")
+
+
+JPEGS = sorted(glob.glob(golden("testdata", "*.jpeg"))) + [golden("testdata", "iceberg.jpg")]
+
+
+@pytest.mark.parametrize("path", JPEGS, ids=os.path.basename)
+def test_host_entropy_matches_oracle(path):
+    data = open(path, "rb").read()
+    try:
+        oc = O.jpeg_coefficients(data)
+    except O.OracleError as e:
+        with pytest.raises(_lib.ZpixError) as ei:
+            J.Coefficients(data)
+        assert ei.value.name == e.name
+        return
+    pc = J.Coefficients(data)
+    f = pc.frame
+    assert (f.width, f.height, f.n_comp, f.mxx, f.myy) == (oc.width, oc.height, oc.n_comp, oc.mxx, oc.myy)
+    for c in range(oc.n_comp):
+        assert (f.h[c], f.v[c]) == (oc.h[c], oc.v[c])
+        g = pc.grid(c)
+        if oc.grids[c] is None:
+            assert g is None
+        else:
+            assert np.array_equal(oc.grids[c], g.astype(np.int32))
+            # quant table used for reconstruction, natural order
+            unzig = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27,
+                     20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58,
+                     59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
+            nat = np.zeros(64, np.int32)
+            nat[unzig] = oc.quant_zigzag[oc.tq[c]]
+            assert np.array_equal(np.array(f.qt[c][:]), nat)
+
+
+def _jpeg_err_product(data):
+    try:
+        J.Coefficients(data)
+        return "OK"
+    except _lib.ZpixError as e:
+        return e.name
+
+
+def test_host_entropy_error_cases():
+    b = read("testdata", "video-005.gray.q50.jpeg")
+    i = b.index(b"\xff\xda") + 2
+    for k in range(i, min(i + 10, len(b))):
+        assert _jpeg_err_product(b[:k]) == "UnexpectedEof"
+    assert _jpeg_err_product(read("testdata", "large_short.jpeg")) == "UnexpectedEof"
+    assert _jpeg_err_product(read("testdata", "video-001.jpeg")[:24]) == "UnexpectedEof"
+    r = read("testdata", "video-001.restart2.jpeg")
+    for infix, want in [(b"", "OK"), (b"\x61\x62\x63\xff\x00\x64", "OK"), (b"\xff\xff\xff\x00\xff\x00\x00\xff\xff\xff", "OK"),
+                        (b"\xff\x03", "BadRSTMarker"), (b"\xff\xd5", "BadRSTMarker"), (b"\xff\xff\xd5", "BadRSTMarker")]:
+        assert _jpeg_err_product(r[:2816] + infix + r[2816:]) == want
+
+
+def test_host_entropy_fuzz_matches_oracle():
+    """Random byte corruption of fixtures: same coefficients or same error name."""
+    rng = np.random.default_rng(7)
+    srcs = [read("testdata", n) for n in ("video-001.q50.420.jpeg", "video-001.q50.420.progressive.jpeg",
+                                          "video-001.restart2.jpeg", "video-005.gray.q50.jpeg")]
+    for it in range(60):
+        d = bytearray(srcs[it % len(srcs)])
+        for _ in range(rng.integers(1, 4)):
+            d[rng.integers(0, len(d))] = rng.integers(0, 256)
+        data = bytes(d)
+        try:
+            oc = O.jpeg_coefficients(data)
+        except O.OracleError as e:
+            assert _jpeg_err_product(data) == e.name
+            continue
+        pc = J.Coefficients(data)
+        for c in range(oc.n_comp):
+            if oc.grids[c] is not None:
+                assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32))
+
+
+def _idat_stream(png_bytes):
+    pos, z = 8, b""
+    while pos < len(png_bytes):
+        n = struct.unpack(">I", png_bytes[pos:pos + 4])[0]
+        if png_bytes[pos + 4:pos + 8] == b"IDAT":
+            z += png_bytes[pos + 8:pos + 8 + n]
+        pos += 12 + n
+    return zlib.decompress(z)
+
+
+PNGS = sorted(glob.glob(golden("pngsuite", "*.png"))) + sorted(glob.glob(golden("testdata", "*.png")))
+
+
+@pytest.mark.parametrize("path", PNGS, ids=os.path.basename)
+def test_host_inflate_stream(path):
+    data = open(path, "rb").read()
+    st = P.Stream(data)
+    want = _idat_stream(data)
+    got = st.filtered()[:st.filtered_len]
+    assert bytes(got) == want[:st.filtered_len]
+
+
+def _png_err_product(data):
+    try:
+        P.Stream(data)
+        return "OK"
+    except _lib.ZpixError as e:
+        return e.name
+
+
+def _png_err_oracle(data):
+    try:
+        O.png_decode(data)
+        return "OK"
+    except O.OracleError as e:
+        return e.name
+
+
+def test_host_png_errors_match_oracle():
+    base = S.png_generic(3, 37, 21, 8, 2)
+    cases = [base[:20], base[:-5], b"\x89PNX" + base[4:]]
+    # bad CRC of IHDR
+    bad_crc = bytearray(base)
+    bad_crc[29] ^= 0xFF
+    cases.append(bytes(bad_crc))
+    # invalid filter type in row 3
+    raw = np.frombuffer(_idat_stream(base), np.uint8).copy().reshape(21, -1)
+    raw[3, 0] = 7
+    cases.append(S.encode_png(37, 21, 8, 2, raw.tobytes()))
+    # truncated zlib stream
+    cases.append(S.encode_png(37, 21, 8, 2, raw.tobytes()[: raw.size // 2]))
+    # bad colour type / depth combination
+    cases.append(S.encode_png(5, 5, 4, 2, b"\x00" * 100))
+    rng = np.random.default_rng(11)
+    for _ in range(40):
+        d = bytearray(base)
+        d[rng.integers(8, len(d))] ^= 1 << int(rng.integers(0, 8))
+        cases.append(bytes(d))
+    for d in cases:
+        want = _png_err_oracle(d)
+        got = _png_err_product(d)
+        assert got == want, (got, want)

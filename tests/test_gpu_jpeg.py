@@ -1,0 +1,215 @@
+"""GPU parity of the JPEG pixel path (jpeg_planar_kernel, jpeg_rgba_kernel,
+convertToRGB / applyBlack kernels) against the CPU oracle, bit-exact.
+
+Sizes are ones the oracle finishes in seconds; the 4096^2 bench frame is
+checked against the oracle once (both sides are deterministic integer code).
+"""
+import ctypes as C
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import golden, read
+from tools import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import zpix_amd  # noqa: E402
+from zpix_amd import _lib, device  # noqa: E402
+from zpix_amd import jpeg as J  # noqa: E402
+
+JPEGS = sorted(glob.glob(golden("testdata", "*.jpeg"))) + [golden("testdata", "iceberg.jpg")]
+
+
+def _oracle_or_error(data):
+    try:
+        return O.jpeg_decode(data), None
+    except O.OracleError as e:
+        return None, e.name
+
+
+def assert_same_image(got, want):
+    assert got.kind == want.kind
+    assert tuple(got.rect) == tuple(want.rect)
+    if want.kind == "YCbCr":
+        assert (got.y_stride, got.c_stride, got.cb_off, got.cr_off, got.subsample) == (
+            want.y_stride, want.c_stride, want.cb_off, want.cr_off, want.subsample)
+    else:
+        assert got.stride == want.stride
+    assert got.pixels.size == want.pixels.size
+    assert np.array_equal(got.pixels, want.pixels)
+
+
+@pytest.mark.parametrize("path", JPEGS, ids=os.path.basename)
+def test_jpeg_decode_planes_match_oracle(path):
+    data = open(path, "rb").read()
+    want, err = _oracle_or_error(data)
+    if err:
+        with pytest.raises(zpix_amd.ZpixError) as ei:
+            J.decode(data)
+        assert ei.value.name == err
+        return
+    assert_same_image(J.decode(data), want)
+
+
+@pytest.mark.parametrize("path", JPEGS, ids=os.path.basename)
+def test_jpeg_decode_rgba_matches_oracle(path):
+    data = open(path, "rb").read()
+    want, err = _oracle_or_error(data)
+    if err:
+        return
+    got = J.decode_rgba(data)
+    assert np.array_equal(got.reshape(-1), want.rgba_pixels())
+
+
+def test_jpeg_load_and_facade():
+    p = golden("testdata", "video-001.q50.422.jpeg")
+    want = O.jpeg_decode(read("testdata", "video-001.q50.422.jpeg"))
+    assert_same_image(J.load(p), want)
+    assert_same_image(zpix_amd.from_file_path(p), want)
+    assert J.probe_path(p)
+
+
+SYNTH = [
+    ("420", 2, 333, 177), ("444", 0, 129, 65), ("422", 1, 250, 99), ("420", 2, 17, 9),
+    ("420", 2, 1, 1), ("444", 0, 8, 8), ("420", 2, 512, 384),
+]
+
+
+@pytest.mark.parametrize("name,sub,w,h", SYNTH)
+@pytest.mark.parametrize("progressive", [False, True])
+def test_jpeg_synthetic_sizes(name, sub, w, h, progressive):
+    data = S.jpeg_subsampled(w * 7 + h, w, h, sub, quality=80, progressive=progressive)
+    want = O.jpeg_decode(data)
+    assert_same_image(J.decode(data), want)
+    assert np.array_equal(J.decode_rgba(data).reshape(-1), want.rgba_pixels())
+
+
+@pytest.mark.parametrize("progressive", [False, True])
+def test_jpeg_gray_synthetic(progressive):
+    data = S.jpeg_gray(5, 203, 77, progressive=progressive)
+    want = O.jpeg_decode(data)
+    assert_same_image(J.decode(data), want)
+    assert np.array_equal(J.decode_rgba(data).reshape(-1), want.rgba_pixels())
+
+
+def test_jpeg_errors_match_oracle():
+    b = read("testdata", "video-005.gray.q50.jpeg")
+    i = b.index(b"\xff\xda") + 2
+    with pytest.raises(zpix_amd.ZpixError) as ei:
+        J.decode(b[:i + 3])
+    assert ei.value.name == "UnexpectedEof"
+    r = read("testdata", "video-001.restart2.jpeg")
+    with pytest.raises(zpix_amd.ZpixError) as ei:
+        J.decode(r[:2816] + b"\xff\xd5" + r[2816:])
+    assert ei.value.name == "BadRSTMarker"
+    assert_same_image(J.decode(r[:2816] + b"\xff\xff\xff\x00\xff\x00\x00\xff\xff\xff" + r[2816:]),
+                      O.jpeg_decode(r[:2816] + b"\xff\xff\xff\x00\xff\x00\x00\xff\xff\xff" + r[2816:]))
+
+
+# ------------------------------------------------------------ kernel level
+def _run_planar_grids(grids, qts, h, v, mxx, myy, width, height, rule, coeff_bits, narrow):
+    """Launch a one-frame planar plan on raw coefficient grids (device)."""
+    n_comp = len(grids)
+    f = _lib.zpx_jpeg_frame()
+    f.width, f.height, f.n_comp, f.mxx, f.myy = width, height, n_comp, mxx, myy
+    f.coeff_bits, f.narrow, f.color = coeff_bits, narrow, 0
+    keep = []
+    planes = []
+    dt = torch.int16 if coeff_bits == 16 else torch.int32
+    for c in range(n_comp):
+        f.h[c], f.v[c], f.rule[c] = h[c], v[c], rule
+        g = torch.from_numpy(np.ascontiguousarray(grids[c]).astype(np.int16 if coeff_bits == 16 else np.int32)).to("cuda")
+        keep.append(g)
+        f.coeffs[c] = g.data_ptr()
+        for i in range(64):
+            f.qt[c][i] = int(qts[c][i])
+        gw, gh = mxx * h[c], myy * v[c]
+        p = torch.zeros(gw * 8 * gh * 8, dtype=torch.uint8, device="cuda")
+        planes.append(p)
+        f.planes[c] = p.data_ptr()
+        f.strides[c] = gw * 8
+    ctx = zpix_amd.context.default()
+    hp = C.c_void_p()
+    _lib.check(_lib.lib().zpx_jpeg_plan_create(ctx.handle, C.byref(f), 1, 0, C.byref(hp)), ctx.handle)
+    plan = device._Plan(hp, ctx)
+    plan.launch(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    plan.close()
+    return [p.cpu().numpy() for p in planes]
+
+
+UNZIG = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27,
+                  20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58,
+                  59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63])
+
+
+@pytest.mark.parametrize("coeff_bits,scale,narrow,rule", [
+    (16, 64, 1, 0), (16, 2000, 0, 0), (32, 1 << 20, 0, 0), (32, 1 << 27, 0, 1), (16, 300, 1, 2),
+])
+def test_planar_kernel_random_grids(coeff_bits, scale, narrow, rule):
+    """Random (incl. overflowing) coefficient grids: wrap-around i32 IDCT,
+    DC-only shortcut and clamp must match the oracle bit for bit."""
+    rng = np.random.default_rng(coeff_bits + scale)
+    h, v, mxx, myy, width, height = [2, 1, 1], [2, 1, 1], 7, 5, 100, 70
+    grids, qz = [], []
+    for c in range(3):
+        nb = mxx * h[c] * myy * v[c]
+        g = rng.integers(-scale, scale, (nb, 64)) if coeff_bits == 32 else rng.integers(-min(scale, 32767), min(scale, 32767), (nb, 64))
+        sparse = rng.random((nb, 64)) < 0.7
+        g[sparse] = 0
+        g[rng.random(nb) < 0.2, 1:] = 0  # DC-only blocks
+        grids.append(g.astype(np.int32))
+        qz.append(rng.integers(1, 256 if narrow else 65535, 64).astype(np.int32))
+    if narrow:  # keep max|coef*q| <= 16384 as the host would certify
+        for c in range(3):
+            grids[c] = np.clip(grids[c], -(16384 // 255), 16384 // 255)
+    qnat = []
+    for c in range(3):
+        n = np.zeros(64, np.int32)
+        n[UNZIG] = qz[c]
+        qnat.append(n)
+    got = _run_planar_grids(grids, qnat, h, v, mxx, myy, width, height, rule, coeff_bits, narrow)
+    want = [np.zeros_like(p) for p in got]
+    strides = [mxx * h[c] * 8 for c in range(3)]
+    O.reconstruct_grids(3, width, height, h, v, mxx, myy, grids, qz, rule == 1, want, strides)
+    if rule == 2:  # scan rule: blocks with bx*8>=W or by*8>=H stay untouched
+        for c in range(3):
+            gw = mxx * h[c]
+            m = np.zeros((myy * v[c] * 8, gw * 8), bool)
+            for by in range(myy * v[c]):
+                for bx in range(gw):
+                    if bx * 8 < width and by * 8 < height:
+                        m[by * 8:by * 8 + 8, bx * 8:bx * 8 + 8] = True
+            want[c] = np.where(m.reshape(-1), want[c], 0)
+    for c in range(3):
+        assert np.array_equal(got[c], want[c]), c
+
+
+def test_jpeg_batch_4k_fused_matches_oracle():
+    """The bench workload (4096^2 4:2:0, q75) for one frame, slot-replicated."""
+    data = S.jpeg_420(0, 4096, 4096)
+    co = J.Coefficients(data)
+    assert co.frame.narrow == 1 and co.frame.coeff_bits == 16
+    batch = device.JpegBatch([co], slots=[0, 0], output="rgba")
+    batch.launch(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = O.jpeg_decode(data).rgba_pixels().reshape(4096, 4096, 4)
+    for s in range(2):
+        assert torch.equal(batch.output_tensor(s).cpu(), torch.from_numpy(want))
+    assert batch.bytes == 393216 * 128 + 4096 * 4096 * 4 + 3 * 256
+
+
+def test_jpeg_batch_planes_matches_oracle():
+    data = S.jpeg_420(3, 640, 480)
+    co = J.Coefficients(data)
+    batch = device.JpegBatch([co], output="planes")
+    batch.launch()
+    torch.cuda.synchronize()
+    want = O.jpeg_decode(data)
+    got = batch.output_tensor(0).cpu().numpy()
+    assert np.array_equal(got, want.pixels)

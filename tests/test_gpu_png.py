@@ -1,0 +1,155 @@
+"""GPU parity of the PNG pixel path (wavefront unfilter + pixel store + Adam7
+scatter) and of Image.rgbaPixels, against the oracle and the reference goldens.
+
+- PngSuite .sng goldens (src/png/decoder_test.zig) through the GPU decode;
+- BMP parity pairs (src/bmp/decoder_test.zig, pins Avg + rgbaPixels);
+- every colour type x bit depth x interlace x tRNS on random sizes that
+  exercise partial chunks, one-row images, many 64-row bands;
+- at the bench size (4096^2 tc8, mixed Sub/Up/Avg/Paeth): unfilter(filter(x))
+  == x, a size-independent round trip.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+import sng
+from conftest import golden, read
+from test_oracle import BMP_PAIRS, PNGSUITE, bmp_rgba_premultiplied
+from tools import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import zpix_amd  # noqa: E402
+from zpix_amd import device  # noqa: E402
+from zpix_amd import png as P  # noqa: E402
+
+
+def assert_same_png(got, want):
+    assert got.kind == want.kind
+    assert tuple(got.rect) == tuple(want.rect)
+    assert got.stride == want.stride
+    assert np.array_equal(got.pixels, want.pixels)
+    if want.kind == "Paletted":
+        assert [tuple(p) for p in got.palette] == [tuple(p) for p in want.palette]
+
+
+@pytest.mark.parametrize("name", PNGSUITE)
+def test_pngsuite_gpu(name):
+    path = golden("pngsuite", name + ".png")
+    img = P.load(path)
+    assert_same_png(img, O.png_decode(read("pngsuite", name + ".png")))
+    if name == "basn4a16":
+        return
+    with open(golden("pngsuite", name + ".sng")) as f:
+        sng.compare_with_golden(sng.sng(path, img), f.read())
+
+
+@pytest.mark.parametrize("name", BMP_PAIRS)
+def test_bmp_parity_gpu(name):
+    pytest.importorskip("PIL")
+    img = P.load(golden("testdata", name + ".png"))
+    rgba = img.rgba_pixels().reshape(img.height, img.width, 4)
+    assert np.array_equal(rgba, bmp_rgba_premultiplied(golden("testdata", name + ".bmp")))
+
+
+# (depth, color_type) pairs the reference accepts (png/decoder.zig:366-397)
+COMBOS = [(1, 0), (2, 0), (4, 0), (8, 0), (16, 0), (8, 2), (16, 2), (1, 3), (2, 3), (4, 3), (8, 3),
+          (8, 4), (16, 4), (8, 6), (16, 6)]
+SIZES = [(1, 1), (3, 2), (17, 5), (64, 65), (130, 200), (33, 129)]
+
+
+def _palette(n):
+    rng = np.random.default_rng(n)
+    return bytes(rng.integers(0, 256, 3 * n, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("depth,ct", COMBOS)
+@pytest.mark.parametrize("interlace", [0, 1])
+def test_png_all_depths(depth, ct, interlace):
+    for k, (w, h) in enumerate(SIZES):
+        seed = depth * 1000 + ct * 100 + interlace * 10 + k
+        pal = _palette(min(1 << depth, 200)) if ct == 3 else None
+        data = S.png_generic(seed, w, h, depth, ct, interlace=interlace, palette=pal)
+        assert_same_png(P.decode(data), O.png_decode(data))
+
+
+@pytest.mark.parametrize("depth,ct,trns", [
+    (8, 2, b"\x00\x10\x00\x20\x00\x30"), (16, 2, b"\x12\x34\x56\x78\x9a\xbc"), (8, 0, b"\x00\x40"),
+    (16, 0, b"\x40\x41"), (1, 0, b"\x00\x01"), (2, 0, b"\x00\x02"), (4, 0, b"\x00\x07"), (8, 3, None)])
+@pytest.mark.parametrize("interlace", [0, 1])
+def test_png_trns(depth, ct, trns, interlace):
+    for k, (w, h) in enumerate(SIZES[2:]):
+        pal = _palette(50) if ct == 3 else None
+        t = trns if ct != 3 else bytes(np.random.default_rng(k).integers(0, 256, 30, dtype=np.uint8))
+        data = S.png_generic(k + 77, w, h, depth, ct, interlace=interlace, trns=t, palette=pal)
+        want = O.png_decode(data)
+        got = P.decode(data)
+        assert_same_png(got, want)
+        assert np.array_equal(got.rgba_pixels(), want.rgba_pixels())
+
+
+def test_png_out_of_range_palette_index_grows_palette():
+    # indices up to 15 with a 4-entry PLTE: implicit palette growth
+    data = S.png_generic(5, 40, 9, 4, 3, palette=_palette(16)[:12])
+    got, want = P.decode(data), O.png_decode(data)
+    assert_same_png(got, want)
+
+
+@pytest.mark.parametrize("w,h", [(4096, 256), (333, 1000), (1000, 333), (7, 3000)])
+def test_png_tc8_mixed_filters(w, h):
+    data = S.png_tc8_mixed(w + h, w, h)
+    assert_same_png(P.decode(data), O.png_decode(data))
+
+
+def test_png_bench_size_roundtrip():
+    """4096^2 tc8 with per-row Sub/Up/Avg/Paeth: the GPU unfilter must return
+    exactly the generator's raw pixels (unfilter(filter(x)) == x)."""
+    raw, filt = S.png_filtered_tc8(0, 4096, 4096)
+    data = S.encode_png(4096, 4096, 8, 2, filt.tobytes())
+    st = P.Stream(data)
+    batch = device.PngBatch([st], slots=[0, 0])
+    for _ in range(2):  # relaunch: scratch must be re-initialised every call
+        batch.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    want = np.concatenate([raw.reshape(4096, 4096, 3), np.full((4096, 4096, 1), 255, np.uint8)], 2)
+    for s in range(2):
+        got = batch.output_tensor(s).cpu().numpy().reshape(4096, 4096, 4)
+        assert np.array_equal(got, want)
+    assert batch.bytes == 4096 * (1 + 4096 * 3) + 4096 * 4096 * 4
+
+
+def test_png_adam7_rgba16_roundtrip():
+    data = S.png_rgba16_adam7(3, 1024, 768)
+    assert_same_png(P.decode(data), O.png_decode(data))
+
+
+def test_png_errors_gpu():
+    base = S.png_generic(3, 37, 21, 8, 2)
+    with pytest.raises(zpix_amd.ZpixError) as ei:
+        P.decode(base[:-5])
+    want = None
+    try:
+        O.png_decode(base[:-5])
+    except O.OracleError as e:
+        want = e.name
+    assert ei.value.name == want
+
+
+# ---------------------------------------------------------------- rgbaPixels
+ALL_KIND_FILES = [("pngsuite", n + ".png") for n in PNGSUITE] + [
+    ("testdata", n) for n in ("video-001.jpeg", "video-001.q50.410.jpeg", "video-001.q50.411.jpeg",
+                              "video-001.q50.440.jpeg", "video-001.cmyk.jpeg", "video-001.rgb.jpeg",
+                              "video-005.gray.jpeg", "video-001.221212.jpeg")]
+
+
+@pytest.mark.parametrize("where,name", ALL_KIND_FILES)
+def test_rgba_pixels_every_kind(where, name):
+    data = read(where, name)
+    want = O.decode(data)
+    got = zpix_amd.from_buffer(data)
+    assert got.kind == want.kind
+    assert np.array_equal(got.rgba_pixels(), want.rgba_pixels())

@@ -1,0 +1,173 @@
+"""ctypes binding of libzpix_amd.so (the C-ABI in include/zpix_amd.h).
+
+The shared library is built in-tree (zpix_amd/libzpix_amd.so) by
+`__graft_entry__.build()` / `make -C zpix_amd/csrc`.  If it is missing this
+module raises: there is no Python or CPU fallback for the pixel path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzpix_amd.so")
+
+# one HIP runtime per process: if torch is importable, let it load its
+# libamdhip64 first so device pointers from torch tensors and from this
+# library share the runtime (same SONAME, so ours resolves to the loaded one).
+try:  # pragma: no cover - import side effect only
+    import torch  # noqa: F401
+except Exception:  # torch is plumbing, not required for the C-ABI itself
+    torch = None
+
+
+class ZpixError(Exception):
+    """A decode error carrying the reference's Zig error name (e.g. 'UnexpectedEof')."""
+
+    def __init__(self, name: str, detail: str = ""):
+        super().__init__(name if not detail else f"{name}: {detail}")
+        self.name = name
+        self.detail = detail
+
+
+class zpx_color(C.Structure):
+    _fields_ = [("r", C.c_uint8), ("g", C.c_uint8), ("b", C.c_uint8), ("a", C.c_uint8),
+                ("model", C.c_uint8), ("pad", C.c_uint8 * 3)]
+
+
+class zpx_image(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("min_x", C.c_int32),
+        ("min_y", C.c_int32),
+        ("max_x", C.c_int32),
+        ("max_y", C.c_int32),
+        ("pixels", C.POINTER(C.c_uint8)),
+        ("pixels_len", C.c_size_t),
+        ("stride", C.c_size_t),
+        ("y_off", C.c_size_t),
+        ("cb_off", C.c_size_t),
+        ("cr_off", C.c_size_t),
+        ("y_stride", C.c_size_t),
+        ("c_stride", C.c_size_t),
+        ("subsample", C.c_int32),
+        ("palette", C.POINTER(zpx_color)),
+        ("palette_len", C.c_int32),
+    ]
+
+
+class zpx_jpeg_frame(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("n_comp", C.c_int32),
+        ("h", C.c_int32 * 4),
+        ("v", C.c_int32 * 4),
+        ("mxx", C.c_int32),
+        ("myy", C.c_int32),
+        ("rule", C.c_int32 * 4),
+        ("coeff_bits", C.c_int32),
+        ("narrow", C.c_int32),
+        ("color", C.c_int32),
+        ("coeffs", C.c_void_p * 4),
+        ("qt", (C.c_int32 * 64) * 4),
+        ("planes", C.c_void_p * 4),
+        ("strides", C.c_size_t * 4),
+        ("rgba", C.c_void_p),
+        ("rgba_stride", C.c_size_t),
+    ]
+
+
+class zpx_png_frame(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("depth", C.c_int32),
+        ("interlace", C.c_int32),
+        ("use_transparent", C.c_int32),
+        ("transparent", C.c_uint8 * 6),
+        ("pad", C.c_uint8 * 2),
+        ("filtered", C.c_void_p),
+        ("out", C.c_void_p),
+        ("out_stride", C.c_size_t),
+        ("max_index", C.c_void_p),
+    ]
+
+
+# every symbol include/zpix_amd.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "zpx_error_name", "zpx_last_error", "zpx_ctx_create", "zpx_ctx_destroy", "zpx_ctx_stream",
+    "zpx_ctx_device", "zpx_ctx_synchronize", "zpx_image_free", "zpx_image_rgba_pixels",
+    "zpx_jpeg_decode", "zpx_jpeg_load", "zpx_jpeg_probe_buffer", "zpx_jpeg_decode_rgba",
+    "zpx_png_decode", "zpx_png_load", "zpx_png_probe_buffer", "zpx_from_buffer", "zpx_from_file_path",
+    "zpx_jpeg_plan_create", "zpx_png_plan_create", "zpx_plan_launch", "zpx_plan_bytes",
+    "zpx_plan_kernel_count", "zpx_plan_destroy", "zpx_dev_rgba_pixels", "zpx_jpeg_entropy_decode",
+    "zpx_jpeg_coeffs_frame", "zpx_jpeg_coeffs_free", "zpx_png_inflate", "zpx_png_stream_frame",
+    "zpx_png_stream_data", "zpx_png_stream_free",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libzpix_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, sz, u8p = C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_uint8)
+    sig = {
+        "zpx_error_name": (C.c_char_p, [i32]),
+        "zpx_last_error": (C.c_char_p, [vp]),
+        "zpx_ctx_create": (i32, [i32, C.POINTER(vp)]),
+        "zpx_ctx_destroy": (None, [vp]),
+        "zpx_ctx_stream": (vp, [vp]),
+        "zpx_ctx_device": (i32, [vp]),
+        "zpx_ctx_synchronize": (i32, [vp]),
+        "zpx_image_free": (None, [vp, C.POINTER(zpx_image)]),
+        "zpx_image_rgba_pixels": (i32, [vp, vp, C.POINTER(zpx_image), C.POINTER(u8p), C.POINTER(sz)]),
+        "zpx_jpeg_decode": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(zpx_image)]),
+        "zpx_jpeg_load": (i32, [vp, vp, C.c_char_p, C.POINTER(zpx_image)]),
+        "zpx_jpeg_probe_buffer": (i32, [C.c_char_p, sz]),
+        "zpx_jpeg_decode_rgba": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(u8p), C.POINTER(sz),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "zpx_png_decode": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(zpx_image)]),
+        "zpx_png_load": (i32, [vp, vp, C.c_char_p, C.POINTER(zpx_image)]),
+        "zpx_png_probe_buffer": (i32, [C.c_char_p, sz]),
+        "zpx_from_buffer": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(zpx_image)]),
+        "zpx_from_file_path": (i32, [vp, vp, C.c_char_p, C.POINTER(zpx_image)]),
+        "zpx_jpeg_plan_create": (i32, [vp, C.POINTER(zpx_jpeg_frame), i32, i32, C.POINTER(vp)]),
+        "zpx_png_plan_create": (i32, [vp, C.POINTER(zpx_png_frame), i32, C.POINTER(vp)]),
+        "zpx_plan_launch": (i32, [vp, vp]),
+        "zpx_plan_bytes": (C.c_uint64, [vp]),
+        "zpx_plan_kernel_count": (i32, [vp]),
+        "zpx_plan_destroy": (None, [vp]),
+        "zpx_dev_rgba_pixels": (i32, [vp, C.POINTER(zpx_image), vp, vp]),
+        "zpx_jpeg_entropy_decode": (i32, [C.c_char_p, sz, C.POINTER(vp)]),
+        "zpx_jpeg_coeffs_frame": (i32, [vp, C.POINTER(zpx_jpeg_frame), C.POINTER(sz)]),
+        "zpx_jpeg_coeffs_free": (None, [vp]),
+        "zpx_png_inflate": (i32, [C.c_char_p, sz, C.POINTER(vp)]),
+        "zpx_png_stream_frame": (i32, [vp, C.POINTER(zpx_png_frame), C.POINTER(sz)]),
+        "zpx_png_stream_data": (vp, [vp]),
+        "zpx_png_stream_free": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def error_name(code: int) -> str:
+    return lib().zpx_error_name(code).decode()
+
+
+def check(code: int, ctx=None) -> None:
+    if code:
+        detail = ""
+        if ctx is not None:
+            detail = (lib().zpx_last_error(ctx) or b"").decode()
+        raise ZpixError(error_name(code), detail)

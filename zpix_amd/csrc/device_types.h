@@ -1,0 +1,59 @@
+// Descriptors shared by the host planner and the gfx950 kernels.
+#pragma once
+
+#include <cstdint>
+
+namespace zpx {
+
+// One JPEG frame as the kernels see it (uploaded once per plan).
+struct DevJpegFrame {
+    const void *coeffs[4];   // (mxx*h) x (myy*v) blocks x 64 coefficients (int16 or int32)
+    uint8_t *planes[4];      // planar output
+    uint64_t strides[4];
+    uint8_t *rgba;           // fused output
+    uint64_t rgba_stride;
+    int32_t width, height, mxx, myy;
+    int32_t h[4], v[4];
+    int32_t rule[4];
+    int32_t n_comp, color;
+    int32_t qt[4][64];       // natural order
+};
+
+// One PNG unfilter job: a (pass of a) PNG image.  Rows are processed by the
+// skewed wavefront kernel in bands of 64 rows (one row per lane).
+struct DevPngPass {
+    const uint8_t *filtered; // first filter byte of this pass
+    uint8_t *out;            // output image base
+    int32_t *max_index;      // paletted: max index seen (atomicMax), else null
+    uint64_t out_stride;     // bytes between output rows of the full image
+    uint32_t width;          // pixels in a pass row
+    uint32_t rows;           // rows in the pass
+    uint32_t row_bytes;      // filtered bytes per row without the filter byte
+    uint32_t xo, yo, xf, yf; // Adam7 placement (0,0,1,1 when not interlaced)
+    uint32_t nbands;         // ceil(rows / 64)
+    uint32_t band_base;      // index of this pass's first band in the progress table
+    uint8_t trns[6];         // tRNS colour key (raw bytes)
+    uint8_t use_trns;
+    uint8_t pad;
+};
+
+// A scheduled band: which pass and which band in it.  Bands are ordered so
+// that band b of a pass always precedes band b+1 of the same pass.
+struct DevPngBand {
+    uint32_t pass;
+    uint32_t band;
+};
+
+} // namespace zpx
+
+namespace zpx {
+
+// An image.Image on the device (pixels / palette are device pointers).
+struct DevImage {
+    const uint8_t *pixels;
+    const uint8_t *palette; // zpx_color entries
+    uint64_t stride, y_off, cb_off, cr_off, y_stride, c_stride;
+    int32_t kind, subsample, width, height, palette_len, pad;
+};
+
+} // namespace zpx

@@ -1,0 +1,824 @@
+// Host entropy stage of the JPEG path.  Same observable behaviour as the
+// reference decoder (coefficients and error names), organised for the device
+// split: scans always accumulate into coefficient grids and no pixel is
+// produced here.  References are to src/jpeg/decoder.zig unless noted.
+#include "jpeg_host.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+namespace zpx {
+
+// ---------------------------------------------------------------- HostBuf
+HostBuf &HostBuf::operator=(HostBuf &&o) noexcept
+{
+    if (this != &o) {
+        release();
+        ptr = o.ptr;
+        bytes = o.bytes;
+        pinned = o.pinned;
+        o.ptr = nullptr;
+        o.bytes = 0;
+        o.pinned = false;
+    }
+    return *this;
+}
+
+static bool pinned_allowed()
+{
+    static int ok = -1;
+    if (ok < 0) {
+        const char *env = getenv("ZPX_NO_PINNED");
+        int n = 0;
+        ok = (!(env && env[0] == '1') && hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
+    }
+    return ok == 1;
+}
+
+bool HostBuf::alloc(size_t n, bool zero)
+{
+    release();
+    if (n == 0) n = 1;
+    if (pinned_allowed() && hipHostMalloc(&ptr, n, hipHostMallocDefault) == hipSuccess) {
+        pinned = true;
+    } else {
+        ptr = aligned_alloc(64, (n + 63) & ~size_t(63));
+        pinned = false;
+        if (!ptr) return false;
+    }
+    bytes = n;
+    if (zero) memset(ptr, 0, n);
+    return true;
+}
+
+void HostBuf::release()
+{
+    if (ptr) {
+        if (pinned) (void)hipHostFree(ptr);
+        else free(ptr);
+    }
+    ptr = nullptr;
+    bytes = 0;
+    pinned = false;
+}
+
+// ---------------------------------------------------------------- CoeffGrid
+bool CoeffGrid::init(size_t blocks)
+{
+    blocks_ = blocks;
+    wide_ = false;
+    max_abs_ = 0;
+    return buf_.alloc(blocks * 64 * sizeof(int16_t), true);
+}
+
+void CoeffGrid::load(size_t blk, int32_t *b) const
+{
+    if (wide_) {
+        memcpy(b, static_cast<const int32_t *>(buf_.ptr) + blk * 64, 64 * sizeof(int32_t));
+    } else {
+        const int16_t *s = static_cast<const int16_t *>(buf_.ptr) + blk * 64;
+        for (int i = 0; i < 64; i++) b[i] = s[i];
+    }
+}
+
+bool CoeffGrid::widen()
+{
+    HostBuf nb;
+    if (!nb.alloc(blocks_ * 64 * sizeof(int32_t), false)) return false;
+    const int16_t *s = static_cast<const int16_t *>(buf_.ptr);
+    int32_t *d = static_cast<int32_t *>(nb.ptr);
+    for (size_t i = 0; i < blocks_ * 64; i++) d[i] = s[i];
+    buf_ = static_cast<HostBuf &&>(nb);
+    wide_ = true;
+    return true;
+}
+
+bool CoeffGrid::store(size_t blk, const int32_t *b)
+{
+    int32_t m = max_abs_;
+    for (int i = 0; i < 64; i++) {
+        int32_t a = b[i] < 0 ? -b[i] : b[i];
+        if (a > m || a < 0) m = (a < 0) ? INT32_MAX : a;
+    }
+    max_abs_ = m;
+    if (!wide_ && m > 32767 && !widen()) return false;
+    if (wide_) {
+        memcpy(static_cast<int32_t *>(buf_.ptr) + blk * 64, b, 64 * sizeof(int32_t));
+    } else {
+        int16_t *d = static_cast<int16_t *>(buf_.ptr) + blk * 64;
+        for (int i = 0; i < 64; i++) d[i] = static_cast<int16_t>(b[i]);
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- decoder
+namespace {
+
+// zig-zag -> natural index (decoder.zig:73-82)
+constexpr uint8_t kUnzig[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
+};
+
+struct Huff { // HuffTable.zig
+    int32_t num_codes = 0;
+    uint16_t lut[256] = {};
+    uint8_t vals[256] = {};
+    int32_t min_codes[16] = {}, max_codes[16] = {}, vals_indices[16] = {};
+};
+
+#define ZTRY(e)                                                                \
+    do {                                                                       \
+        int e_ = (e);                                                          \
+        if (e_) return e_;                                                     \
+    } while (0)
+
+class Decoder {
+  public:
+    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out) : src_(p), len_(n), o_(out) {}
+    int run();
+
+  private:
+    // --- byte source (the whole input stays addressable, so the
+    //     unread-by-up-to-two-bytes of unreadByteStuffedByte (:479-487)
+    //     is a plain rewind)
+    int byte(uint8_t &x)
+    { // readByte :402-410
+        if (pos_ >= len_) return ZPX_E_UNEXPECTED_EOF;
+        x = src_[pos_++];
+        unread_ = 0;
+        return 0;
+    }
+    void unread_stuffed()
+    {
+        pos_ -= unread_;
+        unread_ = 0;
+        if (bn_ >= 8) {
+            ba_ >>= 8;
+            bn_ -= 8;
+            bm_ >>= 8;
+        }
+    }
+    void settle()
+    { // common prologue of readFull / ignore
+        if (unread_ > 0) {
+            if (bn_ >= 8) unread_stuffed();
+            unread_ = 0;
+        }
+    }
+    int full(uint8_t *p, size_t n)
+    { // readFull :414-443
+        settle();
+        if (len_ - pos_ < n) {
+            pos_ = len_;
+            return ZPX_E_UNEXPECTED_EOF;
+        }
+        memcpy(p, src_ + pos_, n);
+        pos_ += n;
+        return 0;
+    }
+    int skip(int32_t n)
+    { // ignore :376-398
+        settle();
+        if (len_ - pos_ < static_cast<size_t>(n)) {
+            pos_ = len_;
+            return ZPX_E_UNEXPECTED_EOF;
+        }
+        pos_ += static_cast<size_t>(n);
+        return 0;
+    }
+    inline int stuffed(uint8_t &out)
+    { // readByteStuffedByte :712-749
+        if (pos_ + 2 <= len_) {
+            uint8_t x = src_[pos_++];
+            unread_ = 1;
+            if (x != 0xff) {
+                out = x;
+                return 0;
+            }
+            if (src_[pos_] != 0x00) return ZPX_E_MISSING_FF00;
+            pos_++;
+            unread_ = 2;
+            out = 0xff;
+            return 0;
+        }
+        unread_ = 0;
+        uint8_t x;
+        ZTRY(byte(x));
+        unread_ = 1;
+        if (x != 0xff) {
+            out = x;
+            return 0;
+        }
+        ZTRY(byte(x));
+        unread_ = 2;
+        if (x != 0x00) return ZPX_E_MISSING_FF00;
+        out = 0xff;
+        return 0;
+    }
+    inline int ensure(int32_t n)
+    { // ensureNBits :975-991
+        do {
+            uint8_t c;
+            ZTRY(stuffed(c));
+            ba_ = (ba_ << 8) | c;
+            bn_ += 8;
+            bm_ = bm_ == 0 ? 0x80u : bm_ << 8;
+        } while (bn_ < n);
+        return 0;
+    }
+    inline int huffman(const Huff &h, uint8_t &out)
+    { // decodeHuffman :909-970
+        if (h.num_codes == 0) return ZPX_E_UNINITIALIZED_HUFFMAN_TABLE;
+        bool slow = false;
+        if (bn_ < 8) {
+            int e = ensure(8);
+            if (e) {
+                if (e != ZPX_E_MISSING_FF00) return e;
+                if (unread_ != 0) unread_stuffed();
+                slow = true;
+            }
+        }
+        if (!slow) {
+            uint16_t lv = h.lut[(ba_ >> (bn_ - 8)) & 0xff];
+            if (lv != 0) {
+                int32_t nb = static_cast<int32_t>(lv & 0xff) - 1;
+                bn_ -= nb;
+                bm_ >>= nb;
+                out = static_cast<uint8_t>(lv >> 8);
+                return 0;
+            }
+        }
+        int32_t code = 0;
+        for (int i = 0; i < 16; i++) {
+            if (bn_ == 0) ZTRY(ensure(1));
+            if (ba_ & bm_) code |= 1;
+            bn_--;
+            bm_ >>= 1;
+            if (code <= h.max_codes[i]) {
+                int32_t idx = h.vals_indices[i] + code - h.min_codes[i];
+                if (idx < 0 || idx > 255) return ZPX_E_PANIC;
+                out = h.vals[idx];
+                return 0;
+            }
+            code <<= 1;
+        }
+        return ZPX_E_BAD_HUFFMAN_CODE;
+    }
+    int bit(bool &b)
+    { // decodeBit :994-1006
+        if (bn_ == 0) ZTRY(ensure(1));
+        b = (ba_ & bm_) != 0;
+        bn_--;
+        bm_ >>= 1;
+        return 0;
+    }
+    int bits(int32_t n, uint32_t &out)
+    { // decodeBits :1009-1022
+        if (bn_ < n) ZTRY(ensure(n));
+        uint32_t r = ba_ >> (bn_ - n);
+        r &= n >= 32 ? 0xffffffffu : ((1u << n) - 1);
+        bn_ -= n;
+        bm_ >>= n;
+        out = r;
+        return 0;
+    }
+    inline int receive_extend(uint8_t t, int32_t &out)
+    { // receiveExtend :1115-1134
+        if (bn_ < static_cast<int32_t>(t)) ZTRY(ensure(t));
+        bn_ -= t;
+        bm_ >>= t;
+        int32_t thr = int32_t(1) << t;
+        int32_t v = static_cast<int32_t>((ba_ >> bn_) & static_cast<uint32_t>(thr - 1));
+        if (v < (thr >> 1)) v += static_cast<int32_t>(0xffffffffu << t) + 1;
+        out = v;
+        return 0;
+    }
+
+    int sof(int32_t n);
+    int dqt(int32_t n);
+    int dht(int32_t n);
+    int sos(int32_t n);
+    int refine(int32_t *b, const Huff &h, int32_t zs, int32_t ze, int32_t delta);
+    int refine_nonzero(int32_t *b, int32_t zig, int32_t ze, int32_t nz, int32_t delta,
+                       int32_t &zout);
+    int find_rst(uint8_t expected);
+    void snapshot_quant(int c);
+
+    const uint8_t *src_;
+    size_t len_, pos_ = 0, unread_ = 0;
+    uint32_t ba_ = 0, bm_ = 0;
+    int32_t bn_ = 0;
+    JpegCoeffs &o_;
+    uint16_t restart_interval_ = 0;
+    uint16_t eob_run_ = 0;
+    Huff huff_[2][4];
+    int32_t quant_[4][64] = {}; // zig-zag order, as the reference keeps it
+    uint8_t tmp_[128] = {};
+    bool seen_sos_ = false;
+    bool interleaved_[4] = {}, noninterleaved_[4] = {};
+};
+
+int Decoder::sof(int32_t n)
+{ // processSof :490-618
+    if (o_.n_comp != 0) return ZPX_E_MULTIPLE_SOF_MARKERS;
+    if (n == 9) o_.n_comp = 1;
+    else if (n == 15) o_.n_comp = 3;
+    else if (n == 18) o_.n_comp = 4;
+    else return ZPX_E_NUMBER_COMPONENTS;
+    ZTRY(full(tmp_, static_cast<size_t>(n)));
+    if (tmp_[0] != 8) return ZPX_E_PRECISION;
+    o_.height = (uint32_t(tmp_[1]) << 8) + tmp_[2];
+    o_.width = (uint32_t(tmp_[3]) << 8) + tmp_[4];
+    if (tmp_[5] != o_.n_comp) return ZPX_E_SOF_WRONG_LENGTH;
+    JpegComponent *c = o_.comp;
+    for (int i = 0; i < o_.n_comp; i++) {
+        c[i].id = tmp_[6 + 3 * i];
+        for (int j = 0; j < i; j++)
+            if (c[i].id == c[j].id) return ZPX_E_REPEATED_COMPONENT_IDENTIFIER;
+        c[i].tq = tmp_[8 + 3 * i];
+        if (c[i].tq > 3) return ZPX_E_BAD_TQ_VALUE;
+        const uint8_t hv = tmp_[7 + 3 * i];
+        int32_t h = hv >> 4, v = hv & 0x0f;
+        if (h < 1 || h > 4 || v < 1 || v > 4 || h == 3 || v == 3)
+            return ZPX_E_LUMA_CHROMA_SUB_SAMPLING_RATIO;
+        if (o_.n_comp == 1) {
+            h = v = 1; // non-interleaved by definition (A.2)
+        } else if (o_.n_comp == 3) {
+            bool bad = (i == 0 && v == 4) || (i == 1 && (c[0].h % h != 0 || c[0].v % v != 0)) ||
+                       (i == 2 && (c[1].h != h || c[1].v != v));
+            if (bad) return ZPX_E_LUMA_CHROMA_SUB_SAMPLING_RATIO;
+        } else {
+            bool bad = (i == 0 && hv != 0x11 && hv != 0x22) || ((i == 1 || i == 2) && hv != 0x11) ||
+                       (i == 3 && (c[0].h != h || c[0].v != v));
+            if (bad) return ZPX_E_LUMA_CHROMA_SUB_SAMPLING_RATIO;
+        }
+        c[i].h = h;
+        c[i].v = v;
+    }
+    return 0;
+}
+
+int Decoder::dqt(int32_t n)
+{ // processDqt :629-666
+    while (n > 0) {
+        n--;
+        uint8_t qi;
+        ZTRY(byte(qi));
+        const uint8_t tq = qi & 0x0f;
+        if (tq > 3) return ZPX_E_BAD_TQ_VALUE;
+        const int pq = qi >> 4;
+        if (pq > 1) return ZPX_E_BAD_PQ_VALUE;
+        const int32_t need = pq == 0 ? 64 : 128;
+        if (n < need) break;
+        n -= need;
+        ZTRY(full(tmp_, static_cast<size_t>(need)));
+        for (int i = 0; i < 64; i++)
+            quant_[tq][i] = pq == 0 ? tmp_[i] : ((int32_t(tmp_[2 * i]) << 8) | tmp_[2 * i + 1]);
+    }
+    return n != 0 ? ZPX_E_DQT_WRONG_LENGTH : 0;
+}
+
+int Decoder::dht(int32_t n)
+{ // processDht :1026-1111
+    while (n > 0) {
+        if (n < 17) return ZPX_E_DHT_WRONG_LENGTH;
+        ZTRY(full(tmp_, 17));
+        const uint8_t tc = tmp_[0] >> 4, th = tmp_[0] & 0x0f;
+        if (tc > 1) return ZPX_E_BAD_TC_VALUE;
+        if (th > 3 || (o_.baseline && th > 1)) return ZPX_E_BAD_TH_VALUE;
+        Huff &h = huff_[tc][th];
+        int32_t count[16];
+        h.num_codes = 0;
+        for (int i = 0; i < 16; i++) h.num_codes += (count[i] = tmp_[1 + i]);
+        if (h.num_codes == 0) return ZPX_E_HUFF_ZERO_LENGTH;
+        if (h.num_codes > 256) return ZPX_E_HUFF_TOO_LONG;
+        n -= h.num_codes + 17;
+        if (n < 0) return ZPX_E_DHT_WRONG_LENGTH;
+        ZTRY(full(h.vals, static_cast<size_t>(h.num_codes)));
+        memset(h.lut, 0, sizeof(h.lut));
+        uint32_t code = 0;
+        int vi = 0;
+        for (int len = 1; len <= 8; len++) {
+            code <<= 1;
+            for (int j = 0; j < count[len - 1]; j++, code++, vi++) {
+                const uint32_t base = code << (8 - len);
+                const uint16_t lv = static_cast<uint16_t>((h.vals[vi] << 8) | (len + 1));
+                for (uint32_t k = 0; k < (1u << (8 - len)); k++) {
+                    if ((base | k) > 255) return ZPX_E_PANIC; // over-full code set
+                    h.lut[base | k] = lv;
+                }
+            }
+        }
+        int32_t cb = 0, idx = 0;
+        for (int i = 0; i < 16; i++) {
+            if (count[i] == 0) {
+                h.min_codes[i] = h.max_codes[i] = h.vals_indices[i] = -1;
+            } else {
+                h.min_codes[i] = cb;
+                h.max_codes[i] = cb + count[i] - 1;
+                h.vals_indices[i] = idx;
+                cb += count[i];
+                idx += count[i];
+            }
+            cb <<= 1;
+        }
+    }
+    return 0;
+}
+
+int Decoder::refine_nonzero(int32_t *b, int32_t zig, int32_t ze, int32_t nz, int32_t delta,
+                            int32_t &zout)
+{ // refineNonZeroes :1522-1549
+    for (; zig <= ze; zig++) {
+        const int idx = kUnzig[zig];
+        if (b[idx] == 0) {
+            if (nz == 0) break;
+            nz--;
+            continue;
+        }
+        bool set;
+        ZTRY(bit(set));
+        if (!set) continue;
+        b[idx] += b[idx] >= 0 ? delta : -delta;
+    }
+    zout = zig;
+    return 0;
+}
+
+int Decoder::refine(int32_t *b, const Huff &h, int32_t zs, int32_t ze, int32_t delta)
+{ // refine :1459-1518
+    if (zs == 0) {
+        if (ze != 0) return ZPX_E_PANIC;
+        bool set;
+        ZTRY(bit(set));
+        if (set) b[0] |= delta;
+        return 0;
+    }
+    int32_t zig = zs;
+    if (eob_run_ == 0) {
+        for (; zig <= ze; zig++) {
+            int32_t z = 0;
+            uint8_t value;
+            ZTRY(huffman(h, value));
+            const uint8_t v0 = value >> 4, v1 = value & 0x0f;
+            if (v1 == 0) {
+                if (v0 != 0x0f) {
+                    eob_run_ = static_cast<uint16_t>(1u << v0);
+                    if (v0 != 0) {
+                        uint32_t x;
+                        ZTRY(bits(v0, x));
+                        eob_run_ |= static_cast<uint16_t>(x);
+                    }
+                    break;
+                }
+            } else if (v1 == 1) {
+                bool positive;
+                ZTRY(bit(positive));
+                z = positive ? delta : -delta;
+            } else {
+                return ZPX_E_UNEXPECTED_HUFFMAN_CODE;
+            }
+            ZTRY(refine_nonzero(b, zig, ze, v0, delta, zig));
+            if (zig > ze) return ZPX_E_TOO_MANY_COEFFICIENTS;
+            if (z != 0) b[kUnzig[zig]] = z;
+        }
+    }
+    if (eob_run_ > 0) {
+        eob_run_--;
+        int32_t ignored;
+        ZTRY(refine_nonzero(b, zig, ze, -1, delta, ignored));
+    }
+    return 0;
+}
+
+int Decoder::find_rst(uint8_t expected)
+{ // findRst :1671-1705
+    for (;;) {
+        size_t i = 0;
+        if (tmp_[0] == 0xff) {
+            if (tmp_[1] == expected) return 0;
+            if (tmp_[1] == 0xff) i = 1;
+            else if (tmp_[1] != 0x00) return ZPX_E_BAD_RST_MARKER;
+        } else if (tmp_[1] == 0xff) {
+            tmp_[0] = 0xff;
+            i = 1;
+        }
+        ZTRY(full(tmp_ + i, 2 - i));
+    }
+}
+
+void Decoder::snapshot_quant(int c)
+{
+    const int32_t *q = quant_[o_.comp[c].tq];
+    int32_t m = 0;
+    for (int z = 0; z < 64; z++) {
+        o_.qt_natural[c][kUnzig[z]] = q[z];
+        int32_t a = q[z] < 0 ? -q[z] : q[z];
+        m = a > m ? a : m;
+    }
+    o_.max_q[c] = m;
+}
+
+int Decoder::sos(int32_t n)
+{ // processSos :1148-1455
+    if (o_.n_comp == 0) return ZPX_E_MISSING_SOS_MARKER;
+    if (n < 6 || 4 + 2 * o_.n_comp < n || n % 2 != 0) return ZPX_E_SOS_WRONG_LENGTH;
+    ZTRY(full(tmp_, static_cast<size_t>(n)));
+    const int ns = tmp_[0];
+    if (n != 4 + 2 * ns) return ZPX_E_SOS_WRONG_LENGTH;
+    struct {
+        uint8_t id = 0, td = 0, ta = 0;
+    } scan[4];
+    int32_t total_hv = 0;
+    for (int i = 0; i < ns; i++) {
+        const uint8_t sel = tmp_[1 + 2 * i];
+        int ci = -1;
+        for (int j = 0; j < o_.n_comp; j++)
+            if (o_.comp[j].id == sel) {
+                ci = j;
+                break;
+            }
+        if (ci < 0) return ZPX_E_UNKNOWN_COMPONENT_SELECTOR;
+        scan[i].id = static_cast<uint8_t>(ci);
+        for (int j = 0; j < i; j++)
+            if (scan[j].id == scan[i].id) return ZPX_E_REPEATED_COMPONENT_IDENTIFIER;
+        total_hv += o_.comp[ci].h * o_.comp[ci].v;
+        scan[i].td = tmp_[2 + 2 * i] >> 4;
+        if (scan[i].td > 3 || (o_.baseline && scan[i].td > 1)) return ZPX_E_BAD_TD_VALUE;
+        scan[i].ta = tmp_[2 + 2 * i] & 0x0f;
+        if (scan[i].ta > 3 || (o_.baseline && scan[i].ta > 1)) return ZPX_E_BAD_TA_VALUE;
+    }
+    if (o_.n_comp > 1 && total_hv > 10) return ZPX_E_SAMPLING_FACTORS_TOO_LARGE;
+
+    int32_t zs = 0, ze = 63;
+    uint32_t ah = 0, al = 0;
+    if (o_.progressive) {
+        zs = tmp_[1 + 2 * ns];
+        ze = tmp_[2 + 2 * ns];
+        ah = tmp_[3 + 2 * ns] >> 4;
+        al = tmp_[3 + 2 * ns] & 0x0f;
+        if ((zs == 0 && ze != 0) || zs > ze || ze >= 64) return ZPX_E_BAD_SPECTRAL_SELECTION;
+        if (zs != 0 && ns != 1) return ZPX_E_PROGRESSIVE_AC_COEFFICIENTS_FOR_MORE_THAN_ONE_COMPONENT;
+        if (ah != 0 && ah != al + 1) return ZPX_E_BAD_SUCCESSIVE_APPROXIMATION;
+    }
+
+    const int32_t h0 = o_.comp[0].h, v0 = o_.comp[0].v;
+    const int32_t mxx = (static_cast<int32_t>(o_.width) + 8 * h0 - 1) / (8 * h0);
+    const int32_t myy = (static_cast<int32_t>(o_.height) + 8 * v0 - 1) / (8 * v0);
+    o_.mxx = mxx;
+    o_.myy = myy;
+    seen_sos_ = true;
+    // Grids: like progressive_coefficients, allocated for scan[i].id over
+    // i < n_comp (:1269-1282; slots past ns read component 0).
+    for (int i = 0; i < o_.n_comp; i++) {
+        const int ci = scan[i].id;
+        if (!o_.has_grid[ci]) {
+            const size_t nb = size_t(mxx) * size_t(myy) * size_t(o_.comp[ci].h * o_.comp[ci].v);
+            if (!o_.grid[ci].init(nb)) return ZPX_E_OUT_OF_MEMORY;
+            o_.has_grid[ci] = true;
+        }
+    }
+    for (int k = 0; k < ns; k++) (ns != 1 ? interleaved_ : noninterleaved_)[scan[k].id] = true;
+
+    ba_ = bm_ = 0;
+    bn_ = 0;
+    int32_t mcu = 0, block_count = 0;
+    uint8_t expected_rst = 0xd0;
+    int32_t dc[4] = {0, 0, 0, 0};
+    int32_t b[64];
+    const bool prog = o_.progressive;
+    for (int32_t my = 0; my < myy; my++) {
+        for (int32_t mx = 0; mx < mxx; mx++) {
+            for (int k = 0; k < ns; k++) {
+                const int ci = scan[k].id;
+                const int32_t hi = o_.comp[ci].h, vi = o_.comp[ci].v;
+                CoeffGrid &g = o_.grid[ci];
+                const Huff &hdc = huff_[0][scan[k].td];
+                const Huff &hac = huff_[1][scan[k].ta];
+                for (int32_t j = 0; j < hi * vi; j++) {
+                    int32_t bx, by;
+                    if (ns != 1) {
+                        bx = hi * mx + j % hi;
+                        by = vi * my + j / hi;
+                    } else {
+                        bx = block_count % (mxx * hi);
+                        by = block_count / (mxx * hi);
+                        block_count++;
+                        if (bx * 8 >= static_cast<int32_t>(o_.width) ||
+                            by * 8 >= static_cast<int32_t>(o_.height))
+                            continue;
+                    }
+                    const size_t blk = size_t(by) * size_t(mxx * hi) + size_t(bx);
+                    if (prog) g.load(blk, b);
+                    else memset(b, 0, sizeof(b));
+                    if (ah != 0) {
+                        ZTRY(refine(b, hac, zs, ze, int32_t(1) << al));
+                    } else {
+                        int32_t zig = zs;
+                        if (zig == 0) {
+                            zig++;
+                            uint8_t t;
+                            ZTRY(huffman(hdc, t));
+                            if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+                            int32_t delta;
+                            ZTRY(receive_extend(t, delta));
+                            dc[ci] += delta;
+                            b[0] = dc[ci] << al;
+                        }
+                        if (zig <= ze && eob_run_ > 0) {
+                            eob_run_--;
+                        } else {
+                            for (; zig <= ze; zig++) {
+                                uint8_t value;
+                                ZTRY(huffman(hac, value));
+                                const uint8_t v0r = value >> 4, v1 = value & 0x0f;
+                                if (v1 != 0) {
+                                    zig += v0r;
+                                    if (zig > ze) break;
+                                    int32_t ac;
+                                    ZTRY(receive_extend(v1, ac));
+                                    b[kUnzig[zig]] = ac << al;
+                                } else {
+                                    if (v0r != 0x0f) {
+                                        eob_run_ = static_cast<uint16_t>(1u << v0r);
+                                        if (v0r != 0) {
+                                            uint32_t x;
+                                            ZTRY(bits(v0r, x));
+                                            eob_run_ |= static_cast<uint16_t>(x);
+                                        }
+                                        eob_run_--;
+                                        break;
+                                    }
+                                    zig += 0x0f;
+                                }
+                            }
+                        }
+                    }
+                    if (!g.store(blk, b)) return ZPX_E_OUT_OF_MEMORY;
+                }
+            }
+            mcu++;
+            if (restart_interval_ > 0 && mcu % restart_interval_ == 0 && mcu < mxx * myy) {
+                ZTRY(full(tmp_, 2));
+                if (tmp_[0] != 0xff || tmp_[1] != expected_rst) ZTRY(find_rst(expected_rst));
+                expected_rst = expected_rst == 0xd7 ? 0xd0 : static_cast<uint8_t>(expected_rst + 1);
+                ba_ = bm_ = 0;
+                bn_ = 0;
+                dc[0] = dc[1] = dc[2] = dc[3] = 0;
+                eob_run_ = 0;
+            }
+        }
+    }
+    // baseline reconstructs during the scan with the table current now
+    if (!prog)
+        for (int k = 0; k < ns; k++) snapshot_quant(scan[k].id);
+    return 0;
+}
+
+int Decoder::run()
+{ // decodeInner :220-373
+    ZTRY(full(tmp_, 2));
+    if (tmp_[0] != 0xff || tmp_[1] != 0xd8) return ZPX_E_INVALID_SOI_MARKER;
+    for (;;) {
+        ZTRY(full(tmp_, 2));
+        while (tmp_[0] != 0xff) { // extraneous data (:246-269)
+            tmp_[0] = tmp_[1];
+            ZTRY(byte(tmp_[1]));
+        }
+        uint8_t marker = tmp_[1];
+        if (marker == 0) continue;
+        while (marker == 0xff) ZTRY(byte(marker));
+        if (marker == 0xd9) break;                    // EOI
+        if (marker >= 0xd0 && marker <= 0xd7) continue; // stray RST
+        ZTRY(full(tmp_, 2));
+        const int32_t n = (int32_t(tmp_[0]) << 8) + tmp_[1] - 2;
+        if (n < 0) return ZPX_E_SHORT_SEGMENT_LENGTH;
+        switch (marker) {
+        case 0xc0:
+        case 0xc1:
+        case 0xc2:
+            o_.baseline = marker == 0xc0;
+            o_.progressive = marker == 0xc2;
+            ZTRY(sof(n));
+            break;
+        case 0xdb: ZTRY(dqt(n)); break;
+        case 0xdd: // processDri :621-627
+            if (n != 2) return ZPX_E_DRI_WRONG_LENGTH;
+            ZTRY(full(tmp_, 2));
+            restart_interval_ = static_cast<uint16_t>((tmp_[0] << 8) + tmp_[1]);
+            break;
+        case 0xc4: ZTRY(dht(n)); break;
+        case 0xda: ZTRY(sos(n)); break;
+        case 0xe0: // processApp0Marker :668-680
+            if (n < 5) {
+                ZTRY(skip(n));
+                break;
+            }
+            ZTRY(full(tmp_, 5));
+            o_.jfif = memcmp(tmp_, "JFIF\0", 5) == 0;
+            ZTRY(skip(n - 5));
+            break;
+        case 0xee: // processApp14Marker :682-697
+            if (n < 12) {
+                ZTRY(skip(n));
+                break;
+            }
+            ZTRY(full(tmp_, 12));
+            if (memcmp(tmp_, "Adobe", 5) == 0) {
+                o_.adobe_valid = true;
+                o_.adobe_transform = tmp_[11];
+            }
+            ZTRY(skip(n - 12));
+            break;
+        default:
+            if ((marker >= 0xe0 && marker <= 0xef) || marker == 0xfe) ZTRY(skip(n));
+            else if (marker < 0xc0) return ZPX_E_UNKNOWN_MARKER;
+            else return ZPX_E_UNSUPPORTED_MARKER;
+        }
+    }
+    if (!seen_sos_) return ZPX_E_MISSING_SOS_MARKER; // :372
+    for (int c = 0; c < o_.n_comp; c++) {
+        if (o_.progressive) {
+            if (o_.has_grid[c]) snapshot_quant(c); // reconstructProgressiveImage uses final tables
+            o_.rule[c] = o_.has_grid[c] ? ZPX_BLOCKS_PROGRESSIVE : ZPX_BLOCKS_NONE;
+        } else if (interleaved_[c]) {
+            o_.rule[c] = ZPX_BLOCKS_ALL;
+        } else if (noninterleaved_[c]) {
+            o_.rule[c] = ZPX_BLOCKS_SCAN;
+        } else {
+            o_.rule[c] = ZPX_BLOCKS_NONE;
+        }
+    }
+    return 0;
+}
+
+} // namespace
+
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out)
+{
+    Decoder d(buf, len, out);
+    return d.run();
+}
+
+JpegOut jpeg_output_kind(const JpegCoeffs &c)
+{
+    if (c.n_comp == 1) return JpegOut::Gray;
+    if (c.n_comp == 4) return (c.adobe_valid && c.adobe_transform == 0) ? JpegOut::CMYK : JpegOut::YCCK;
+    // isRgb :699-709
+    if (!c.jfif && ((c.adobe_valid && c.adobe_transform == 0) ||
+                    (c.comp[0].id == 'R' && c.comp[1].id == 'G' && c.comp[2].id == 'B')))
+        return JpegOut::RGB;
+    return JpegOut::YCbCr;
+}
+
+int jpeg_layout(const JpegCoeffs &c, JpegLayout &l)
+{
+    l = JpegLayout{};
+    if (c.n_comp == 1) { // GrayImage.init on the MCU rect (:1717-1722)
+        l.y_stride = size_t(8 * c.mxx);
+        l.y_rows = size_t(8 * c.myy);
+        l.total = l.y_stride * l.y_rows;
+        return 0;
+    }
+    const int32_t h0 = c.comp[0].h, v0 = c.comp[0].v;
+    const int32_t hr = h0 / c.comp[1].h, vr = v0 / c.comp[1].v;
+    switch ((hr << 4) | vr) { // :1745-1753
+    case 0x11: l.subsample = ZPX_RATIO444; break;
+    case 0x12: l.subsample = ZPX_RATIO440; break;
+    case 0x21: l.subsample = ZPX_RATIO422; break;
+    case 0x22: l.subsample = ZPX_RATIO420; break;
+    case 0x41: l.subsample = ZPX_RATIO411; break;
+    case 0x42: l.subsample = ZPX_RATIO410; break;
+    default: return ZPX_E_PANIC;
+    }
+    const int32_t w = 8 * h0 * c.mxx, h = 8 * v0 * c.myy; // padded rect
+    int32_t cw = w, ch = h;                               // yCbCrSize (image.zig:521-555)
+    switch (l.subsample) {
+    case ZPX_RATIO422: cw = (w + 1) / 2; break;
+    case ZPX_RATIO420: cw = (w + 1) / 2; ch = (h + 1) / 2; break;
+    case ZPX_RATIO440: ch = (h + 1) / 2; break;
+    case ZPX_RATIO411: cw = (w + 3) / 4; break;
+    case ZPX_RATIO410: cw = (w + 3) / 4; ch = (h + 1) / 2; break;
+    default: break;
+    }
+    l.y_stride = size_t(w);
+    l.y_rows = size_t(h);
+    l.c_stride = size_t(cw);
+    l.c_rows = size_t(ch);
+    l.cb_off = size_t(w) * size_t(h);
+    l.cr_off = l.cb_off + size_t(cw) * size_t(ch);
+    l.total = l.cr_off + size_t(cw) * size_t(ch);
+    if (c.n_comp == 4) {
+        l.k_stride = size_t(8 * c.comp[3].h * c.mxx);
+        l.k_rows = size_t(8 * c.comp[3].v * c.myy);
+        l.k_total = l.k_stride * l.k_rows;
+    }
+    return 0;
+}
+
+} // namespace zpx

@@ -1,0 +1,91 @@
+// Host (serial) half of jpeg.decode: marker parsing, DHT/DQT/SOF/SOS and the
+// Huffman / progressive-refinement entropy decoder.  It never reconstructs
+// pixels: every scan writes into coefficient grids (the accumulate form of
+// processSos, src/jpeg/decoder.zig:1340-1345) that the GPU consumes.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "zpix_amd.h"
+
+namespace zpx {
+
+// Host buffer that prefers pinned (page-locked) memory so H2D copies are
+// DMA-direct; falls back to ordinary memory when no HIP device is usable.
+struct HostBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    bool pinned = false;
+    HostBuf() = default;
+    HostBuf(const HostBuf &) = delete;
+    HostBuf &operator=(const HostBuf &) = delete;
+    HostBuf(HostBuf &&o) noexcept { *this = static_cast<HostBuf &&>(o); }
+    HostBuf &operator=(HostBuf &&o) noexcept;
+    ~HostBuf() { release(); }
+    bool alloc(size_t n, bool zero);
+    void release();
+};
+
+// Block rule per component (see zpx_block_rule).
+struct JpegComponent {
+    int32_t h = 0, v = 0;
+    uint8_t id = 0, tq = 0;
+};
+
+class CoeffGrid {
+  public:
+    // Blocks of 64 natural-order coefficients, stored as int16 while every
+    // value fits, widened to int32 the first time one does not.
+    bool init(size_t blocks);
+    bool wide() const { return wide_; }
+    size_t blocks() const { return blocks_; }
+    const void *data() const { return buf_.ptr; }
+    size_t bytes() const { return buf_.bytes; }
+    void load(size_t blk, int32_t *b) const;
+    bool store(size_t blk, const int32_t *b); // false only on allocation failure
+    int32_t max_abs() const { return max_abs_; }
+
+  private:
+    bool widen();
+    HostBuf buf_;
+    size_t blocks_ = 0;
+    bool wide_ = false;
+    int32_t max_abs_ = 0;
+};
+
+struct JpegCoeffs {
+    uint32_t width = 0, height = 0;
+    int n_comp = 0;
+    JpegComponent comp[4];
+    int32_t mxx = 0, myy = 0;
+    bool progressive = false, baseline = false;
+    bool jfif = false, adobe_valid = false;
+    int adobe_transform = 0;
+    int rule[4] = {ZPX_BLOCKS_NONE, ZPX_BLOCKS_NONE, ZPX_BLOCKS_NONE, ZPX_BLOCKS_NONE};
+    CoeffGrid grid[4];
+    bool has_grid[4] = {false, false, false, false};
+    // quant table each component is reconstructed with, natural order
+    int32_t qt_natural[4][64] = {};
+    int32_t max_q[4] = {0, 0, 0, 0};
+};
+
+// Decode `buf` into coefficient grids.  Returns ZPX_E_* (ZPX_E_OK on success),
+// with the reference's error for malformed input.
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out);
+
+// Output kind decodeInner would return (decoder.zig:361-372).
+enum class JpegOut { Gray, YCbCr, RGB, CMYK, YCCK };
+JpegOut jpeg_output_kind(const JpegCoeffs &c);
+
+// makeImg layout (decoder.zig:1708-1783, image.zig:484-555).
+struct JpegLayout {
+    int subsample = ZPX_RATIO444;
+    size_t y_stride = 0, c_stride = 0, k_stride = 0;
+    size_t y_rows = 0, c_rows = 0, k_rows = 0;
+    size_t cb_off = 0, cr_off = 0, total = 0, k_total = 0;
+};
+int jpeg_layout(const JpegCoeffs &c, JpegLayout &l);
+
+} // namespace zpx

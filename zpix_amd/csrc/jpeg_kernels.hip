@@ -1,0 +1,444 @@
+// gfx950 kernels of the JPEG pixel path:
+//   - jpeg_planar_kernel: dequant + 8x8 integer IDCT + level shift/clamp into
+//     the Y/Cb/Cr/K planes (reconstructBlock, src/jpeg/decoder.zig:1553-1634);
+//   - jpeg_rgba_kernel: the same fused with nearest chroma upsample and
+//     YCbCr->RGB (Image.rgbaPixels over a YCbCrImage: image.zig:103-130,
+//     YCbCrAt :614-630, Color.toRGBA .ycbcr color.zig:90-113), one MCU strip
+//     per workgroup, staged through LDS; the planes never reach HBM.
+// Integer arithmetic is wrap-around i32 (built with -fwrapv), bit-identical to
+// the reference's IDCT (src/jpeg/idct.zig:77-201).  MFMA is not used: no
+// stage is a dense contraction.  The kernels are HBM-bound streaming passes.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_types.h"
+#include "kernels.h"
+
+namespace zpx {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBlkStride = 72; // dwords per 8x8 block in LDS (64 + 8 pad: conflict-free column reads)
+
+// idct.zig:50-65
+constexpr int32_t W1 = 2841, W2 = 2676, W3 = 2408, W5 = 1609, W6 = 1108, W7 = 565;
+constexpr int32_t R2 = 181;
+
+// Left shift with two's-complement wrap (no UB for negative operands).
+__device__ __forceinline__ int32_t shl(int32_t x, int n) { return static_cast<int32_t>(static_cast<uint32_t>(x) << n); }
+
+// Multiply by an IDCT constant.  NARROW: the host proved every operand of the
+// stage-1/2 products fits in 24 signed bits (max |coef*q| <= 16384, see
+// DESIGN.md), so v_mul_i32_i24 gives the same low 32 bits as a 32-bit product.
+template <bool NARROW>
+__device__ __forceinline__ int32_t mulc(int32_t c, int32_t x)
+{
+    if constexpr (NARROW) return __mul24(c, x);
+    else return c * x;
+}
+
+// Horizontal 1-D IDCT of one row (idct.zig:79-145).  s[] holds dequantized
+// coefficients of the row in natural order.
+template <bool NARROW>
+__device__ __forceinline__ void idct_row(int32_t s[8])
+{
+    const int32_t dc = s[0];
+    const bool ac_zero = (s[1] | s[2] | s[3] | s[4] | s[5] | s[6] | s[7]) == 0;
+    int32_t x0 = shl(s[0], 11) + 128, x1 = shl(s[4], 11), x2 = s[6], x3 = s[2];
+    int32_t x4 = s[1], x5 = s[7], x6 = s[5], x7 = s[3], x8;
+    x8 = mulc<NARROW>(W7, x4 + x5);
+    x4 = x8 + mulc<NARROW>(W1 - W7, x4);
+    x5 = x8 - mulc<NARROW>(W1 + W7, x5);
+    x8 = mulc<NARROW>(W3, x6 + x7);
+    x6 = x8 - mulc<NARROW>(W3 - W5, x6);
+    x7 = x8 - mulc<NARROW>(W3 + W5, x7);
+    x8 = x0 + x1;
+    x0 -= x1;
+    x1 = mulc<NARROW>(W6, x3 + x2);
+    x2 = x1 - mulc<NARROW>(W2 + W6, x2);
+    x3 = x1 + mulc<NARROW>(W2 - W6, x3);
+    x1 = x4 + x6;
+    x4 -= x6;
+    x6 = x5 + x7;
+    x5 -= x7;
+    x7 = x8 + x3;
+    x8 -= x3;
+    x3 = x0 + x2;
+    x0 -= x2;
+    x2 = (R2 * (x4 + x5) + 128) >> 8;
+    x4 = (R2 * (x4 - x5) + 128) >> 8;
+    s[0] = (x7 + x1) >> 8;
+    s[1] = (x3 + x2) >> 8;
+    s[2] = (x0 + x4) >> 8;
+    s[3] = (x8 + x6) >> 8;
+    s[4] = (x8 - x6) >> 8;
+    s[5] = (x0 - x4) >> 8;
+    s[6] = (x3 - x2) >> 8;
+    s[7] = (x7 - x1) >> 8;
+    if constexpr (!NARROW) {
+        // DC-only shortcut (idct.zig:84-97).  Identical to the full path
+        // unless dc<<11 overflows, which only the wide variant can see.
+        if (ac_zero) {
+            const int32_t d = shl(dc, 3);
+#pragma unroll
+            for (int i = 0; i < 8; i++) s[i] = d;
+        }
+    } else {
+        (void)dc;
+        (void)ac_zero;
+    }
+}
+
+// Vertical 1-D IDCT of one column (idct.zig:148-200) + level shift and clamp
+// (decoder.zig:1622-1628): c<-128 -> 0, c>127 -> 255, else c+128.
+template <bool NARROW>
+__device__ __forceinline__ void idct_col_clamp(int32_t s[8])
+{
+    int32_t y0 = shl(s[0], 8) + 8192, y1 = shl(s[4], 8), y2 = s[6], y3 = s[2];
+    int32_t y4 = s[1], y5 = s[7], y6 = s[5], y7 = s[3], y8;
+    y8 = mulc<NARROW>(W7, y4 + y5) + 4;
+    y4 = (y8 + mulc<NARROW>(W1 - W7, y4)) >> 3;
+    y5 = (y8 - mulc<NARROW>(W1 + W7, y5)) >> 3;
+    y8 = mulc<NARROW>(W3, y6 + y7) + 4;
+    y6 = (y8 - mulc<NARROW>(W3 - W5, y6)) >> 3;
+    y7 = (y8 - mulc<NARROW>(W3 + W5, y7)) >> 3;
+    y8 = y0 + y1;
+    y0 -= y1;
+    y1 = mulc<NARROW>(W6, y3 + y2) + 4;
+    y2 = (y1 - mulc<NARROW>(W2 + W6, y2)) >> 3;
+    y3 = (y1 + mulc<NARROW>(W2 - W6, y3)) >> 3;
+    y1 = y4 + y6;
+    y4 -= y6;
+    y6 = y5 + y7;
+    y5 -= y7;
+    y7 = y8 + y3;
+    y8 -= y3;
+    y3 = y0 + y2;
+    y0 -= y2;
+    y2 = (R2 * (y4 + y5) + 128) >> 8;
+    y4 = (R2 * (y4 - y5) + 128) >> 8;
+    s[0] = (y7 + y1) >> 14;
+    s[1] = (y3 + y2) >> 14;
+    s[2] = (y0 + y4) >> 14;
+    s[3] = (y8 + y6) >> 14;
+    s[4] = (y8 - y6) >> 14;
+    s[5] = (y0 - y4) >> 14;
+    s[6] = (y3 - y2) >> 14;
+    s[7] = (y7 - y1) >> 14;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = min(max(s[i], -128), 127) + 128;
+}
+
+// Load one 8-coefficient row of a block (natural order) and dequantize it.
+template <typename CoefT>
+__device__ __forceinline__ void load_row(const CoefT *__restrict__ p, const int32_t *__restrict__ q,
+                                         int32_t s[8])
+{
+    if constexpr (sizeof(CoefT) == 2) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(p);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            s[2 * i] = static_cast<int32_t>(static_cast<int16_t>(w[i] & 0xffff));
+            s[2 * i + 1] = static_cast<int32_t>(w[i]) >> 16;
+        }
+    } else {
+        const int4 a = *reinterpret_cast<const int4 *>(p);
+        const int4 b = *reinterpret_cast<const int4 *>(p + 4);
+        s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+        s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+    }
+    // coefficients fit in 16 bits for the int16 transport and q in 17 bits,
+    // so the 24-bit multiply is exact there
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        s[i] = (sizeof(CoefT) == 2) ? __mul24(s[i], q[i]) : s[i] * q[i];
+}
+
+__device__ __forceinline__ bool block_in_rule(int rule, int bx, int by, int hh, int vv, int W, int H)
+{
+    switch (rule) {
+    case ZPX_BLOCKS_ALL: return true;
+    case ZPX_BLOCKS_PROGRESSIVE: return bx * hh < W && by * vv < H; // decoder.zig:1649-1651
+    case ZPX_BLOCKS_SCAN: return bx * 8 < W && by * 8 < H;          // decoder.zig:1334
+    default: return false;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Planar reconstruct: each wave owns 8 horizontally adjacent blocks of one
+// block row; lane = (block, row) for the row pass, (block, column) for the
+// column pass, exchanging through LDS.  Grid: x = 32-block segments of a row,
+// y = block row, z = frame*4 + component.
+// ---------------------------------------------------------------------------
+template <typename CoefT, bool NARROW>
+__global__ __launch_bounds__(kThreads) void jpeg_planar_kernel(const DevJpegFrame *__restrict__ frames)
+{
+    __shared__ int32_t qs[64];
+    __shared__ int32_t buf[4 * 8 * kBlkStride];
+    const int f = blockIdx.z >> 2, comp = blockIdx.z & 3;
+    const DevJpegFrame &fr = frames[f];
+    if (comp >= fr.n_comp) return;
+    const CoefT *grid = static_cast<const CoefT *>(fr.coeffs[comp]);
+    const int rule = fr.rule[comp];
+    if (grid == nullptr || rule == ZPX_BLOCKS_NONE) return;
+    const int gw = fr.mxx * fr.h[comp], gh = fr.myy * fr.v[comp];
+    const int by = blockIdx.y;
+    if (by >= gh) return;
+    const int bx0 = blockIdx.x * 32;
+    if (bx0 >= gw) return;
+    const int hh = 8 * (fr.h[0] / fr.h[comp]), vv = 8 * (fr.v[0] / fr.v[comp]);
+
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (tid < 64) qs[tid] = fr.qt[comp][tid];
+    __syncthreads();
+
+    const int blk = lane >> 3, r = lane & 7; // row pass: block, row
+    const int bx = bx0 + wave * 8 + blk;
+    const bool live = bx < gw && block_in_rule(rule, bx, by, hh, vv, fr.width, fr.height);
+    int32_t *wb = buf + wave * 8 * kBlkStride;
+    int32_t s[8];
+    if (live) {
+        load_row<CoefT>(grid + (static_cast<size_t>(by) * gw + bx) * 64 + r * 8, qs + r * 8, s);
+        idct_row<NARROW>(s);
+#pragma unroll
+        for (int i = 0; i < 8; i++) wb[blk * kBlkStride + r * 8 + i] = s[i];
+    }
+    __syncthreads();
+    const int c = lane & 7; // column pass: block, column
+    if (live) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = wb[blk * kBlkStride + i * 8 + c];
+        idct_col_clamp<NARROW>(s);
+        uint8_t *dst = fr.planes[comp] + 8 * (static_cast<size_t>(by) * fr.strides[comp] + bx) + c;
+#pragma unroll
+        for (int i = 0; i < 8; i++) dst[i * fr.strides[comp]] = static_cast<uint8_t>(s[i]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused reconstruct + Image.rgbaPixels.  A workgroup owns a horizontal strip
+// of T MCUs of one MCU row:
+//   phase 1: lane = (block, row): load, dequant, row IDCT -> LDS (all blocks);
+//   phase 2: chroma columns -> clamped samples in an LDS chroma tile;
+//   phase 3: luma columns -> clamped Y, nearest chroma from LDS, YCbCr->RGB,
+//            one 4-byte RGBA store per pixel (a wave writes 64 adjacent
+//            pixels = 256 contiguous bytes per store instruction).
+// ---------------------------------------------------------------------------
+constexpr int strip_mcus(int blocks_per_mcu) { return blocks_per_mcu >= 96 ? 1 : 96 / blocks_per_mcu; }
+
+template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
+__global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames)
+{
+    constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
+    constexpr int kYB = H0 * V0;                      // luma blocks per MCU
+    constexpr int kCB = kGray ? 0 : HC * VC;          // blocks per chroma component per MCU
+    constexpr int T = strip_mcus(kYB + 2 * kCB);      // MCUs per workgroup
+    constexpr int NY = T * kYB, NC = T * kCB, NB = NY + 2 * NC;
+    constexpr int YW = T * H0;                        // luma blocks across the strip
+    constexpr int CW = T * HC;                        // chroma blocks across the strip
+    constexpr int CPX = kGray ? 1 : CW * 8;           // chroma tile width (samples)
+    constexpr int CROWS = kGray ? 1 : VC * 8;
+    constexpr int RX = kGray ? 1 : H0 / HC, RY = kGray ? 1 : V0 / VC; // upsample ratios
+
+    __shared__ int32_t qs[3][64];
+    __shared__ int32_t buf[NB * kBlkStride];
+    __shared__ int32_t ctile[2][CROWS * CPX];
+
+    const DevJpegFrame &fr = frames[blockIdx.y];
+    const int my = blockIdx.z;
+    if (my >= fr.myy) return;
+    const int mx0 = blockIdx.x * T;
+    if (mx0 >= fr.mxx) return;
+    const int tid = threadIdx.x;
+    const int ncomp = kGray ? 1 : 3;
+    for (int i = tid; i < ncomp * 64; i += kThreads) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
+    __syncthreads();
+
+    // ---- phase 1: rows
+    for (int task = tid; task < NB * 8; task += kThreads) {
+        const int blk = task >> 3, r = task & 7;
+        int comp, bx, by, gw;
+        if (blk < NY) {
+            comp = 0;
+            bx = mx0 * H0 + blk % YW;
+            by = my * V0 + blk / YW;
+            gw = fr.mxx * H0;
+        } else {
+            const int k = (blk - NY) % (NC > 0 ? NC : 1);
+            comp = blk < NY + NC ? 1 : 2;
+            bx = mx0 * HC + k % CW;
+            by = my * VC + k / CW;
+            gw = fr.mxx * HC;
+        }
+        const CoefT *grid = static_cast<const CoefT *>(fr.coeffs[comp]);
+        int32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (grid != nullptr && bx < gw) {
+            load_row<CoefT>(grid + (static_cast<size_t>(by) * gw + bx) * 64 + r * 8, qs[comp] + r * 8, s);
+            idct_row<NARROW>(s);
+        }
+        int32_t *d = buf + blk * kBlkStride + r * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) d[i] = s[i];
+    }
+    __syncthreads();
+
+    // ---- phase 2: chroma columns -> LDS tile
+    if constexpr (!kGray) {
+        for (int task = tid; task < 2 * NC * 8; task += kThreads) {
+            const int k = task >> 3, c = task & 7;
+            const int comp = k < NC ? 1 : 2;
+            const int kk = k % NC;
+            const int blk = NY + k;
+            int32_t s[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) s[i] = buf[blk * kBlkStride + i * 8 + c];
+            idct_col_clamp<NARROW>(s);
+            const bool present = fr.coeffs[comp] != nullptr; // component never scanned: samples 0
+            int32_t *t = ctile[comp - 1] + ((kk / CW) * 8) * CPX + (kk % CW) * 8 + c;
+#pragma unroll
+            for (int i = 0; i < 8; i++) t[i * CPX] = present ? s[i] : 0;
+        }
+        __syncthreads();
+    }
+
+    // ---- phase 3: luma columns + colour + store
+    const int W = fr.width, H = fr.height;
+    uint8_t *const out = fr.rgba;
+    const size_t ostride = fr.rgba_stride;
+    for (int task = tid; task < NY * 8; task += kThreads) {
+        const int blk = task >> 3, c = task & 7;
+        const int yrow = blk / YW, ycol = blk % YW;
+        int32_t s[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = buf[blk * kBlkStride + i * 8 + c];
+        idct_col_clamp<NARROW>(s);
+        const int px = ycol * 8 + c;             // x within the strip
+        const int X = mx0 * H0 * 8 + px;
+        const int Y0 = (my * V0 + yrow) * 8;
+        if (X >= W) continue;
+        uint8_t *o = out + static_cast<size_t>(Y0) * ostride + static_cast<size_t>(X) * 4;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if (Y0 + i >= H) break;
+            const int32_t Yv = s[i];
+            uint32_t pix;
+            if constexpr (kGray) {
+                pix = static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
+            } else {
+                const int cx = px / RX, cy = (yrow * 8 + i) / RY;
+                const int32_t cb = ctile[0][cy * CPX + cx], cr = ctile[1][cy * CPX + cx];
+                if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
+                    pix = static_cast<uint32_t>(Yv) | static_cast<uint32_t>(cb) << 8 |
+                          static_cast<uint32_t>(cr) << 16 | 0xff000000u;
+                } else {
+                    // color.zig:95-106; 8-bit result of (v>>8 or clamp)>>8 == clamp(v>>16, 0, 255)
+                    const int32_t yy1 = __mul24(Yv, 0x10101);
+                    const int32_t cb1 = cb - 128, cr1 = cr - 128;
+                    const int32_t r = yy1 + __mul24(91881, cr1);
+                    const int32_t g = yy1 - __mul24(22554, cb1) - __mul24(46802, cr1);
+                    const int32_t b = yy1 + __mul24(116130, cb1);
+                    const uint32_t R = static_cast<uint32_t>(min(max(r >> 16, 0), 255));
+                    const uint32_t G = static_cast<uint32_t>(min(max(g >> 16, 0), 255));
+                    const uint32_t B = static_cast<uint32_t>(min(max(b >> 16, 0), 255));
+                    pix = R | G << 8 | B << 16 | 0xff000000u;
+                }
+            }
+            *reinterpret_cast<uint32_t *>(o + i * ostride) = pix;
+        }
+    }
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh,
+                       bool wide_coeffs, bool narrow, hipStream_t stream)
+{
+    dim3 grid((max_gw + 31) / 32, max_gh, n_frames * 4);
+    if (wide_coeffs) {
+        if (narrow) hipLaunchKernelGGL((jpeg_planar_kernel<int32_t, true>), grid, dim3(kThreads), 0, stream, d_frames);
+        else hipLaunchKernelGGL((jpeg_planar_kernel<int32_t, false>), grid, dim3(kThreads), 0, stream, d_frames);
+    } else {
+        if (narrow) hipLaunchKernelGGL((jpeg_planar_kernel<int16_t, true>), grid, dim3(kThreads), 0, stream, d_frames);
+        else hipLaunchKernelGGL((jpeg_planar_kernel<int16_t, false>), grid, dim3(kThreads), 0, stream, d_frames);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+namespace {
+template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
+void launch_rgba_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int max_myy, hipStream_t stream)
+{
+    constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
+    constexpr int T = strip_mcus(H0 * V0 + 2 * (kGray ? 0 : HC * VC));
+    dim3 grid((max_mxx + T - 1) / T, n_frames, max_myy);
+    hipLaunchKernelGGL((jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>), grid, dim3(kThreads), 0,
+                       stream, d_frames);
+}
+
+template <typename CoefT, bool NARROW, int COLOR>
+int dispatch_geom(int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStream_t s)
+{
+    switch (key) {
+    case 0x1111: launch_rgba_t<CoefT, NARROW, 1, 1, 1, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x1211: launch_rgba_t<CoefT, NARROW, 1, 2, 1, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x2111: launch_rgba_t<CoefT, NARROW, 2, 1, 1, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x2211: launch_rgba_t<CoefT, NARROW, 2, 2, 1, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x4111: launch_rgba_t<CoefT, NARROW, 4, 1, 1, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x4211: launch_rgba_t<CoefT, NARROW, 4, 2, 1, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x2212: launch_rgba_t<CoefT, NARROW, 2, 2, 1, 2, COLOR>(d, n, mxx, myy, s); break;
+    case 0x2221: launch_rgba_t<CoefT, NARROW, 2, 2, 2, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x2121: launch_rgba_t<CoefT, NARROW, 2, 1, 2, 1, COLOR>(d, n, mxx, myy, s); break;
+    case 0x1212: launch_rgba_t<CoefT, NARROW, 1, 2, 1, 2, COLOR>(d, n, mxx, myy, s); break;
+    case 0x2222: launch_rgba_t<CoefT, NARROW, 2, 2, 2, 2, COLOR>(d, n, mxx, myy, s); break;
+    default: return -2; // geometry without a fused kernel: caller uses planes + rgba pass
+    }
+    return 0;
+}
+
+template <typename CoefT, bool NARROW>
+int dispatch_color(int color, int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStream_t s)
+{
+    switch (color) {
+    case ZPX_JPEG_COLOR_YCBCR: return dispatch_geom<CoefT, NARROW, ZPX_JPEG_COLOR_YCBCR>(key, d, n, mxx, myy, s);
+    case ZPX_JPEG_COLOR_RGB: return dispatch_geom<CoefT, NARROW, ZPX_JPEG_COLOR_RGB>(key, d, n, mxx, myy, s);
+    case ZPX_JPEG_COLOR_GRAY:
+        launch_rgba_t<CoefT, NARROW, 1, 1, 1, 1, ZPX_JPEG_COLOR_GRAY>(d, n, mxx, myy, s);
+        return 0;
+    }
+    return -2;
+}
+} // namespace
+
+bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc)
+{
+    if (color == ZPX_JPEG_COLOR_GRAY) return true;
+    const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
+    switch (key) {
+    case 0x1111: case 0x1211: case 0x2111: case 0x2211: case 0x4111: case 0x4211:
+    case 0x2212: case 0x2221: case 0x2121: case 0x1212: case 0x2222:
+        return true;
+    }
+    return false;
+}
+
+int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc,
+                     int vc, int max_mxx, int max_myy, bool wide_coeffs, bool narrow, hipStream_t stream)
+{
+    const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
+    int rc;
+    if (wide_coeffs)
+        rc = narrow ? dispatch_color<int32_t, true>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
+                    : dispatch_color<int32_t, false>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
+    else
+        rc = narrow ? dispatch_color<int16_t, true>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
+                    : dispatch_color<int16_t, false>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
+    if (rc) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace zpx

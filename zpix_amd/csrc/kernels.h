@@ -1,0 +1,32 @@
+// Launchers of the gfx950 kernels (implemented in the .hip translation units).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_types.h"
+#include "zpix_amd.h"
+
+namespace zpx {
+
+// jpeg_kernels.hip
+int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh, bool wide_coeffs,
+                       bool narrow, hipStream_t stream);
+bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc);
+int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
+                     int max_mxx, int max_myy, bool wide_coeffs, bool narrow, hipStream_t stream);
+
+// png_kernels.hip
+int png_chunk_bytes(int depth);
+int launch_png_unfilter(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
+                        uint32_t *ticket, uint32_t *progress, uint8_t *boundary, uint32_t band_bytes,
+                        uint32_t *status, hipStream_t s);
+
+// color_kernels.hip
+int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);
+int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s);
+int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,
+                     uint8_t *out, hipStream_t s);
+
+} // namespace zpx

@@ -1,0 +1,44 @@
+// Host (serial) half of png.decode: signature, chunk walk with CRC checks,
+// IHDR/PLTE/tRNS/IDAT handling and zlib inflate into pinned memory.  Filter
+// reconstruction and pixel store run on the GPU (png_kernels.hip).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "jpeg_host.h" // HostBuf
+#include "zpix_amd.h"
+
+namespace zpx {
+
+struct PngPassInfo {
+    uint32_t width = 0, rows = 0;   // pass pixel dims (0 = empty pass)
+    uint32_t row_bytes = 0;         // without the filter byte
+    uint32_t xo = 0, yo = 0, xf = 1, yf = 1;
+    size_t offset = 0;              // of the pass's first filter byte in the stream
+};
+
+struct PngStream {
+    uint32_t width = 0, height = 0;
+    int depth = 0;                  // zpx_png_depth
+    int interlace = 0;
+    bool use_transparent = false;
+    uint8_t transparent[6] = {};
+    zpx_color palette[256] = {};
+    int palette_len = 0;
+    bool has_palette = false;
+    int kind = ZPX_GRAY;            // image type readImagePass allocates
+    int out_bpp = 1;                // bytes per output pixel
+    int npasses = 0;
+    PngPassInfo pass[7];
+    HostBuf data;                   // inflated stream (+ZPX_PNG_INPUT_PAD)
+    size_t data_len = 0;            // bytes the passes consume
+};
+
+// Parse + inflate.  On success every row's data is present and every filter
+// byte is valid; otherwise returns the reference's error for the first row
+// that would fail (EndOfStream / ReadFailed / InvalidFilterType) or the
+// chunk-level error.
+int png_parse(const uint8_t *buf, size_t len, PngStream &out);
+
+} // namespace zpx

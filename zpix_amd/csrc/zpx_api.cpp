@@ -1,0 +1,916 @@
+// C-ABI of the MI355X decode path (include/zpix_amd.h): contexts, device
+// plans, and the drop-in jpeg/png/image entry points.  Host entropy stages
+// live in jpeg_host.cpp / png_host.cpp; pixel loops in the .hip kernels.
+// There is no CPU pixel path: every reconstruct / unfilter / colour step is a
+// kernel launch, and a HIP failure is reported as ZPX_E_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "device_types.h"
+#include "jpeg_host.h"
+#include "kernels.h"
+#include "png_host.h"
+#include "zpix_amd.h"
+
+using namespace zpx;
+
+// ------------------------------------------------------------------ errors
+static const char *const kErrorNames[] = {
+#define ZPX_NAME_(name, up) #name,
+    ZPX_ERROR_LIST(ZPX_NAME_)
+#undef ZPX_NAME_
+};
+
+extern "C" const char *zpx_error_name(int code)
+{
+    if (code < 0 || code >= ZPX_E__COUNT) return "Unknown";
+    return kErrorNames[code];
+}
+
+struct zpx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+};
+
+extern "C" const char *zpx_last_error(const zpx_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+namespace {
+
+int hip_fail(zpx_ctx *ctx, hipError_t e, const char *what)
+{
+    if (ctx) {
+        char buf[256];
+        snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+        ctx->last_error = buf;
+    }
+    return ZPX_E_HIP;
+}
+
+#define HIPCHK(ctx, call)                                                      \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);               \
+    } while (0)
+
+// Device buffer (RAII).
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    hipError_t alloc(size_t n)
+    {
+        release();
+        bytes = n ? n : 1;
+        return hipMalloc(&ptr, bytes);
+    }
+    template <typename T> T *as() const { return static_cast<T *>(ptr); }
+};
+
+void *al_alloc(const zpx_allocator *al, size_t n)
+{
+    if (al && al->alloc) return al->alloc(al->user, n ? n : 1);
+    return malloc(n ? n : 1);
+}
+void al_free(const zpx_allocator *al, void *p, size_t n)
+{
+    if (!p) return;
+    if (al && al->free) al->free(al->user, p, n);
+    else free(p);
+}
+
+struct CtxScope { // make ctx->device current for this call
+    explicit CtxScope(zpx_ctx *c) { (void)hipSetDevice(c->device); }
+};
+
+int read_file(const char *path, std::vector<uint8_t> &out)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) return ZPX_E_FILE_NOT_FOUND;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    if (n < 0) {
+        fclose(f);
+        return ZPX_E_READ_FAILED;
+    }
+    out.resize(static_cast<size_t>(n));
+    size_t got = n ? fread(out.data(), 1, static_cast<size_t>(n), f) : 0;
+    fclose(f);
+    return got == static_cast<size_t>(n) ? 0 : ZPX_E_READ_FAILED;
+}
+
+} // namespace
+
+// ------------------------------------------------------------------ context
+extern "C" int zpx_ctx_create(int device, zpx_ctx **out)
+{
+    if (!out) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0 || device < 0 || device >= n) return ZPX_E_HIP;
+    std::unique_ptr<zpx_ctx> c(new zpx_ctx);
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) return ZPX_E_HIP;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return ZPX_E_HIP;
+    *out = c.release();
+    return ZPX_OK;
+}
+
+extern "C" void zpx_ctx_destroy(zpx_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" void *zpx_ctx_stream(zpx_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
+extern "C" int zpx_ctx_device(const zpx_ctx *ctx) { return ctx ? ctx->device : -1; }
+extern "C" int zpx_ctx_synchronize(zpx_ctx *ctx)
+{
+    if (!ctx) return ZPX_E_INVALID_ARGUMENT;
+    CtxScope s(ctx);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return ZPX_OK;
+}
+
+// ------------------------------------------------------------------ image
+extern "C" void zpx_image_free(const zpx_allocator *al, zpx_image *img)
+{
+    if (!img) return;
+    al_free(al, img->pixels, img->pixels_len);
+    if (img->palette) al_free(al, img->palette, 256 * sizeof(zpx_color));
+    img->pixels = nullptr;
+    img->palette = nullptr;
+    img->pixels_len = 0;
+}
+
+static DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette)
+{
+    DevImage m{};
+    m.pixels = static_cast<const uint8_t *>(d_pixels);
+    m.palette = static_cast<const uint8_t *>(d_palette);
+    m.stride = img->stride;
+    m.y_off = img->y_off;
+    m.cb_off = img->cb_off;
+    m.cr_off = img->cr_off;
+    m.y_stride = img->y_stride;
+    m.c_stride = img->c_stride;
+    m.kind = img->kind;
+    m.subsample = img->subsample;
+    m.width = img->max_x - img->min_x;
+    m.height = img->max_y - img->min_y;
+    m.palette_len = img->palette_len;
+    return m;
+}
+
+extern "C" int zpx_dev_rgba_pixels(zpx_ctx *ctx, const zpx_image *img, uint8_t *out, void *stream)
+{
+    if (!ctx || !img || !out) return ZPX_E_INVALID_ARGUMENT;
+    if (img->min_x != 0 || img->min_y != 0) return ZPX_E_UNSUPPORTED; // decoders always return min = (0,0)
+    CtxScope s(ctx);
+    const DevImage m = dev_image_of(img, img->pixels, img->palette);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (launch_rgba_pixels(m, out, st)) return hip_fail(ctx, hipGetLastError(), "rgba_pixels_kernel");
+    return ZPX_OK;
+}
+
+extern "C" int zpx_image_rgba_pixels(zpx_ctx *ctx, const zpx_allocator *al, const zpx_image *img, uint8_t **out,
+                                     size_t *out_len)
+{
+    if (!ctx || !img || !out || !out_len) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    *out_len = 0;
+    if (img->min_x != 0 || img->min_y != 0) return ZPX_E_UNSUPPORTED;
+    CtxScope s(ctx);
+    const size_t w = size_t(img->max_x - img->min_x), h = size_t(img->max_y - img->min_y);
+    const size_t n = w * h * 4;
+    DevBuf dpix, dpal, dout;
+    HIPCHK(ctx, dpix.alloc(img->pixels_len));
+    HIPCHK(ctx, hipMemcpyAsync(dpix.ptr, img->pixels, img->pixels_len, hipMemcpyHostToDevice, ctx->stream));
+    if (img->kind == ZPX_PALETTED && img->palette) {
+        HIPCHK(ctx, dpal.alloc(256 * sizeof(zpx_color)));
+        HIPCHK(ctx, hipMemcpyAsync(dpal.ptr, img->palette, 256 * sizeof(zpx_color), hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIPCHK(ctx, dout.alloc(n));
+    const DevImage m = dev_image_of(img, dpix.ptr, dpal.ptr);
+    if (n && launch_rgba_pixels(m, dout.as<uint8_t>(), ctx->stream))
+        return hip_fail(ctx, hipGetLastError(), "rgba_pixels_kernel");
+    uint8_t *host = static_cast<uint8_t *>(al_alloc(al, n));
+    if (!host) return ZPX_E_OUT_OF_MEMORY;
+    hipError_t e = hipMemcpyAsync(host, dout.ptr, n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        al_free(al, host, n);
+        return hip_fail(ctx, e, "rgba_pixels copy-back");
+    }
+    *out = host;
+    *out_len = n;
+    return ZPX_OK;
+}
+
+// ------------------------------------------------------------------ plans
+struct JpegGroup {
+    DevBuf frames;
+    int n = 0;
+    bool wide = false, narrow = true;
+    int color = 0, h0 = 1, v0 = 1, hc = 1, vc = 1;
+    int max_gw = 0, max_gh = 0, max_mxx = 0, max_myy = 0;
+};
+struct PngGroup {
+    int depth = 0;
+    DevBuf passes, sched, scratch, boundary;
+    uint32_t nsched = 0, band_bytes = 0, nbands = 0;
+    size_t scratch_zero_bytes = 0;
+};
+
+struct zpx_plan {
+    zpx_ctx *ctx = nullptr;
+    int kind = 0; // 0 jpeg planes, 1 jpeg rgba, 2 png
+    std::vector<std::unique_ptr<JpegGroup>> jpeg;
+    std::vector<std::unique_ptr<PngGroup>> png;
+    uint64_t bytes = 0;
+};
+
+extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, int n_frames, int output,
+                                    zpx_plan **out)
+{
+    if (!ctx || !frames || n_frames <= 0 || !out) return ZPX_E_INVALID_ARGUMENT;
+    if (output != ZPX_JPEG_PLANES && output != ZPX_JPEG_RGBA) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    CtxScope s(ctx);
+    std::unique_ptr<zpx_plan> plan(new zpx_plan);
+    plan->ctx = ctx;
+    plan->kind = output == ZPX_JPEG_PLANES ? 0 : 1;
+    // group frames by kernel variant
+    std::map<std::tuple<int, int, int, int, int, int, int>, std::vector<int>> groups;
+    for (int i = 0; i < n_frames; i++) {
+        const zpx_jpeg_frame &f = frames[i];
+        if (f.n_comp != 1 && f.n_comp != 3 && f.n_comp != 4) return ZPX_E_INVALID_ARGUMENT;
+        if (f.coeff_bits != 16 && f.coeff_bits != 32) return ZPX_E_INVALID_ARGUMENT;
+        int color = 0, hc = 1, vc = 1;
+        if (output == ZPX_JPEG_RGBA) {
+            color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
+            if (f.n_comp == 4) return ZPX_E_UNSUPPORTED;
+            if (f.n_comp == 3) {
+                hc = f.h[1];
+                vc = f.v[1];
+            }
+            const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
+            if (!jpeg_rgba_supported(color, h0, v0, hc, vc)) return ZPX_E_UNSUPPORTED;
+            groups[{f.coeff_bits, f.narrow, color, h0, v0, hc, vc}].push_back(i);
+        } else {
+            groups[{f.coeff_bits, f.narrow, 0, 0, 0, 0, 0}].push_back(i);
+        }
+    }
+    uint64_t bytes = 0;
+    for (auto &kv : groups) {
+        std::unique_ptr<JpegGroup> g(new JpegGroup);
+        g->wide = std::get<0>(kv.first) == 32;
+        g->narrow = std::get<1>(kv.first) != 0;
+        g->color = std::get<2>(kv.first);
+        g->h0 = std::get<3>(kv.first);
+        g->v0 = std::get<4>(kv.first);
+        g->hc = std::get<5>(kv.first);
+        g->vc = std::get<6>(kv.first);
+        std::vector<DevJpegFrame> df;
+        for (int idx : kv.second) {
+            const zpx_jpeg_frame &f = frames[idx];
+            DevJpegFrame d{};
+            const size_t esz = f.coeff_bits / 8;
+            for (int c = 0; c < 4; c++) {
+                d.coeffs[c] = c < f.n_comp ? f.coeffs[c] : nullptr;
+                d.planes[c] = f.planes[c];
+                d.strides[c] = f.strides[c];
+                d.h[c] = f.h[c];
+                d.v[c] = f.v[c];
+                d.rule[c] = c < f.n_comp ? f.rule[c] : ZPX_BLOCKS_NONE;
+                memcpy(d.qt[c], f.qt[c], sizeof(d.qt[c]));
+            }
+            if (f.n_comp == 1) d.h[0] = d.v[0] = 1;
+            d.rgba = f.rgba;
+            d.rgba_stride = f.rgba_stride;
+            d.width = static_cast<int32_t>(f.width);
+            d.height = static_cast<int32_t>(f.height);
+            d.mxx = f.mxx;
+            d.myy = f.myy;
+            d.n_comp = f.n_comp;
+            d.color = f.color;
+            df.push_back(d);
+            for (int c = 0; c < f.n_comp; c++) {
+                const int gw = f.mxx * d.h[c], gh = f.myy * d.v[c];
+                g->max_gw = std::max(g->max_gw, gw);
+                g->max_gh = std::max(g->max_gh, gh);
+                if (f.coeffs[c]) bytes += uint64_t(gw) * gh * 64 * esz;
+                if (output == ZPX_JPEG_PLANES) bytes += uint64_t(gw) * gh * 64;
+            }
+            bytes += uint64_t(f.n_comp) * 64 * 4; // quant tables
+            if (output == ZPX_JPEG_RGBA) bytes += uint64_t(f.width) * f.height * 4;
+            g->max_mxx = std::max(g->max_mxx, f.mxx);
+            g->max_myy = std::max(g->max_myy, f.myy);
+        }
+        g->n = static_cast<int>(df.size());
+        HIPCHK(ctx, g->frames.alloc(df.size() * sizeof(DevJpegFrame)));
+        HIPCHK(ctx, hipMemcpy(g->frames.ptr, df.data(), df.size() * sizeof(DevJpegFrame), hipMemcpyHostToDevice));
+        plan->jpeg.push_back(std::move(g));
+    }
+    plan->bytes = bytes;
+    *out = plan.release();
+    return ZPX_OK;
+}
+
+static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPass> &passes_in,
+                           const std::vector<uint32_t> &pass_rowbytes)
+{
+    std::vector<DevPngPass> passes = passes_in;
+    const uint32_t cb = static_cast<uint32_t>(png_chunk_bytes(g.depth));
+    uint32_t base = 0, max_bands = 0, band_bytes = 256;
+    for (size_t i = 0; i < passes.size(); i++) {
+        DevPngPass &p = passes[i];
+        p.nbands = (p.rows + 63) / 64;
+        p.band_base = base;
+        base += p.nbands;
+        max_bands = std::max(max_bands, p.nbands);
+        const uint32_t nchunks = (pass_rowbytes[i] + cb - 1) / cb;
+        band_bytes = std::max(band_bytes, ((nchunks + 15) / 16) * 256u);
+    }
+    std::vector<DevPngBand> sched;
+    for (uint32_t b = 0; b < max_bands; b++)
+        for (size_t i = 0; i < passes.size(); i++)
+            if (b < passes[i].nbands) sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
+    g.nsched = static_cast<uint32_t>(sched.size());
+    g.nbands = base;
+    g.band_bytes = band_bytes;
+    HIPCHK(ctx, g.passes.alloc(passes.size() * sizeof(DevPngPass)));
+    HIPCHK(ctx, hipMemcpy(g.passes.ptr, passes.data(), passes.size() * sizeof(DevPngPass), hipMemcpyHostToDevice));
+    HIPCHK(ctx, g.sched.alloc(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand)));
+    if (!sched.empty())
+        HIPCHK(ctx, hipMemcpy(g.sched.ptr, sched.data(), sched.size() * sizeof(DevPngBand), hipMemcpyHostToDevice));
+    // scratch: [ticket, status, 2 pad][progress x nbands], zeroed before every launch
+    g.scratch_zero_bytes = ((4 + size_t(base)) * sizeof(uint32_t) + 15) & ~size_t(15);
+    HIPCHK(ctx, g.scratch.alloc(g.scratch_zero_bytes));
+    HIPCHK(ctx, hipMemset(g.scratch.ptr, 0, g.scratch_zero_bytes));
+    HIPCHK(ctx, g.boundary.alloc(size_t(base) * band_bytes));
+    return 0;
+}
+
+static void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
+                             uint64_t &bytes)
+{
+    static const uint32_t kA7[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                                       {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+    int bits = 0;
+    switch (f.depth) {
+    case ZPX_PNG_G1: case ZPX_PNG_P1: bits = 1; break;
+    case ZPX_PNG_G2: case ZPX_PNG_P2: bits = 2; break;
+    case ZPX_PNG_G4: case ZPX_PNG_P4: bits = 4; break;
+    case ZPX_PNG_G8: case ZPX_PNG_P8: bits = 8; break;
+    case ZPX_PNG_GA8: case ZPX_PNG_G16: bits = 16; break;
+    case ZPX_PNG_TC8: bits = 24; break;
+    case ZPX_PNG_TCA8: case ZPX_PNG_GA16: bits = 32; break;
+    case ZPX_PNG_TC16: bits = 48; break;
+    default: bits = 64; break;
+    }
+    size_t off = 0;
+    const int np = f.interlace ? 7 : 1;
+    for (int p = 0; p < np; p++) {
+        DevPngPass d{};
+        uint32_t w = f.width, h = f.height, xo = 0, yo = 0, xf = 1, yf = 1;
+        if (f.interlace) {
+            xo = kA7[p][0];
+            yo = kA7[p][1];
+            xf = kA7[p][2];
+            yf = kA7[p][3];
+            w = ((f.width > xo ? f.width - xo : 0) + xf - 1) / xf;
+            h = ((f.height > yo ? f.height - yo : 0) + yf - 1) / yf;
+            if (w == 0 || h == 0) continue;
+        }
+        const uint32_t rb = static_cast<uint32_t>((uint64_t(bits) * w + 7) / 8);
+        d.filtered = f.filtered + off;
+        d.out = f.out;
+        d.max_index = f.max_index;
+        d.out_stride = f.out_stride;
+        d.width = w;
+        d.rows = h;
+        d.row_bytes = rb;
+        d.xo = xo;
+        d.yo = yo;
+        d.xf = xf;
+        d.yf = yf;
+        memcpy(d.trns, f.transparent, 6);
+        d.use_trns = f.use_transparent ? 1 : 0;
+        passes.push_back(d);
+        rowbytes.push_back(rb);
+        off += size_t(h) * (size_t(rb) + 1);
+    }
+    bytes += off;
+}
+
+static int png_out_bpp(int depth, bool trns)
+{
+    switch (depth) {
+    case ZPX_PNG_G1: case ZPX_PNG_G2: case ZPX_PNG_G4: case ZPX_PNG_G8: return trns ? 4 : 1;
+    case ZPX_PNG_GA8: case ZPX_PNG_TC8: case ZPX_PNG_TCA8: return 4;
+    case ZPX_PNG_G16: return trns ? 8 : 2;
+    case ZPX_PNG_GA16: case ZPX_PNG_TC16: case ZPX_PNG_TCA16: return 8;
+    default: return 1;
+    }
+}
+
+extern "C" int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames, zpx_plan **out)
+{
+    if (!ctx || !frames || n_frames <= 0 || !out) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    CtxScope s(ctx);
+    std::unique_ptr<zpx_plan> plan(new zpx_plan);
+    plan->ctx = ctx;
+    plan->kind = 2;
+    std::map<int, std::vector<int>> by_depth;
+    for (int i = 0; i < n_frames; i++) {
+        if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
+        by_depth[frames[i].depth].push_back(i);
+    }
+    uint64_t bytes = 0;
+    for (auto &kv : by_depth) {
+        std::unique_ptr<PngGroup> g(new PngGroup);
+        g->depth = kv.first;
+        std::vector<DevPngPass> passes;
+        std::vector<uint32_t> rowbytes;
+        for (int idx : kv.second) {
+            png_frame_passes(frames[idx], passes, rowbytes, bytes);
+            bytes += uint64_t(frames[idx].width) * frames[idx].height *
+                     png_out_bpp(frames[idx].depth, frames[idx].use_transparent != 0);
+        }
+        if (int e = png_build_group(ctx, *g, passes, rowbytes)) return e;
+        plan->png.push_back(std::move(g));
+    }
+    plan->bytes = bytes;
+    *out = plan.release();
+    return ZPX_OK;
+}
+
+extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
+{
+    if (!plan) return ZPX_E_INVALID_ARGUMENT;
+    zpx_ctx *ctx = plan->ctx;
+    CtxScope s(ctx);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    for (auto &g : plan->jpeg) {
+        int rc;
+        if (plan->kind == 0)
+            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->max_gw, g->max_gh, g->wide, g->narrow, st);
+        else
+            rc = launch_jpeg_rgba(g->frames.as<DevJpegFrame>(), g->n, g->color, g->h0, g->v0, g->hc, g->vc,
+                                  g->max_mxx, g->max_myy, g->wide, g->narrow, st);
+        if (rc == -2) return ZPX_E_UNSUPPORTED;
+        if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
+    }
+    for (auto &g : plan->png) {
+        HIPCHK(ctx, hipMemsetAsync(g->scratch.ptr, 0, g->scratch_zero_bytes, st));
+        uint32_t *sc = g->scratch.as<uint32_t>();
+        const int rc = launch_png_unfilter(g->depth, g->passes.as<DevPngPass>(), g->sched.as<DevPngBand>(), g->nsched,
+                                           sc + 0, sc + 4, g->boundary.as<uint8_t>(), g->band_bytes, sc + 1, st);
+        if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
+    }
+    return ZPX_OK;
+}
+
+// Reads the status word of a finished PNG plan (wavefront spin timeout).
+static int png_plan_status(zpx_plan *plan)
+{
+    for (auto &g : plan->png) {
+        uint32_t st = 0;
+        HIPCHK(plan->ctx, hipMemcpy(&st, g->scratch.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost));
+        if (st) {
+            plan->ctx->last_error = "png wavefront hand-off timed out";
+            return ZPX_E_HIP;
+        }
+    }
+    return ZPX_OK;
+}
+
+extern "C" uint64_t zpx_plan_bytes(const zpx_plan *plan) { return plan ? plan->bytes : 0; }
+extern "C" int zpx_plan_kernel_count(const zpx_plan *plan)
+{
+    return plan ? static_cast<int>(plan->jpeg.size() + plan->png.size()) : 0;
+}
+extern "C" void zpx_plan_destroy(zpx_plan *plan)
+{
+    if (!plan) return;
+    (void)hipSetDevice(plan->ctx->device);
+    delete plan;
+}
+
+// ------------------------------------------------------------------ host stages exposed
+struct zpx_jpeg_coeffs {
+    JpegCoeffs c;
+};
+struct zpx_png_stream {
+    PngStream s;
+};
+
+extern "C" int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
+{
+    if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    std::unique_ptr<zpx_jpeg_coeffs> c(new zpx_jpeg_coeffs);
+    if (int e = jpeg_entropy_decode(buf, len, c->c)) return e;
+    *out = c.release();
+    return ZPX_OK;
+}
+
+static void fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes)
+{
+    memset(f, 0, sizeof(*f));
+    f->width = c.width;
+    f->height = c.height;
+    f->n_comp = c.n_comp;
+    f->mxx = c.mxx;
+    f->myy = c.myy;
+    bool wide = false;
+    int64_t m = 0;
+    for (int i = 0; i < c.n_comp; i++) {
+        f->h[i] = c.comp[i].h;
+        f->v[i] = c.comp[i].v;
+        f->rule[i] = c.rule[i];
+        memcpy(f->qt[i], c.qt_natural[i], sizeof(f->qt[i]));
+        if (c.has_grid[i]) {
+            wide |= c.grid[i].wide();
+            m = std::max<int64_t>(m, int64_t(c.grid[i].max_abs()) * c.max_q[i]);
+        }
+    }
+    f->coeff_bits = wide ? 32 : 16;
+    f->narrow = m <= 16384 ? 1 : 0;
+    switch (jpeg_output_kind(c)) {
+    case JpegOut::Gray: f->color = ZPX_JPEG_COLOR_GRAY; break;
+    case JpegOut::RGB: f->color = ZPX_JPEG_COLOR_RGB; break;
+    default: f->color = ZPX_JPEG_COLOR_YCBCR; break;
+    }
+    for (int i = 0; i < 4; i++) {
+        const bool g = i < c.n_comp && c.has_grid[i];
+        f->coeffs[i] = g ? c.grid[i].data() : nullptr;
+        if (coeff_bytes) coeff_bytes[i] = g ? c.grid[i].blocks() * 64 * (wide ? 4 : 2) : 0;
+    }
+}
+
+extern "C" int zpx_jpeg_coeffs_frame(const zpx_jpeg_coeffs *cc, zpx_jpeg_frame *f, size_t *coeff_bytes)
+{
+    if (!cc || !f) return ZPX_E_INVALID_ARGUMENT;
+    fill_frame(cc->c, f, coeff_bytes);
+    return ZPX_OK;
+}
+
+extern "C" void zpx_jpeg_coeffs_free(zpx_jpeg_coeffs *c) { delete c; }
+
+extern "C" int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out)
+{
+    if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    std::unique_ptr<zpx_png_stream> s(new zpx_png_stream);
+    if (int e = png_parse(buf, len, s->s)) return e;
+    *out = s.release();
+    return ZPX_OK;
+}
+
+extern "C" int zpx_png_stream_frame(const zpx_png_stream *ss, zpx_png_frame *f, size_t *filtered_len)
+{
+    if (!ss || !f) return ZPX_E_INVALID_ARGUMENT;
+    const PngStream &s = ss->s;
+    memset(f, 0, sizeof(*f));
+    f->width = s.width;
+    f->height = s.height;
+    f->depth = s.depth;
+    f->interlace = s.interlace;
+    f->use_transparent = s.use_transparent ? 1 : 0;
+    memcpy(f->transparent, s.transparent, 6);
+    f->filtered = static_cast<const uint8_t *>(s.data.ptr);
+    f->out_stride = size_t(s.width) * s.out_bpp;
+    if (filtered_len) *filtered_len = s.data_len;
+    return ZPX_OK;
+}
+
+extern "C" const uint8_t *zpx_png_stream_data(const zpx_png_stream *s)
+{
+    return s ? static_cast<const uint8_t *>(s->s.data.ptr) : nullptr;
+}
+extern "C" void zpx_png_stream_free(zpx_png_stream *s) { delete s; }
+
+// ------------------------------------------------------------------ jpeg.decode
+namespace {
+
+struct JpegDeviceFrame {
+    DevBuf coeffs[4];
+    zpx_jpeg_frame f{};
+};
+
+int upload_jpeg(zpx_ctx *ctx, const JpegCoeffs &c, JpegDeviceFrame &d)
+{
+    size_t cbytes[4];
+    fill_frame(c, &d.f, cbytes);
+    for (int i = 0; i < c.n_comp; i++) {
+        if (!d.f.coeffs[i]) continue;
+        HIPCHK(ctx, d.coeffs[i].alloc(cbytes[i]));
+        HIPCHK(ctx, hipMemcpyAsync(d.coeffs[i].ptr, d.f.coeffs[i], cbytes[i], hipMemcpyHostToDevice, ctx->stream));
+        d.f.coeffs[i] = d.coeffs[i].ptr;
+    }
+    return ZPX_OK;
+}
+
+int run_plan_once(zpx_ctx *ctx, const zpx_jpeg_frame &f, int output)
+{
+    zpx_plan *plan = nullptr;
+    if (int e = zpx_jpeg_plan_create(ctx, &f, 1, output, &plan)) return e;
+    int e = zpx_plan_launch(plan, ctx->stream);
+    if (!e) {
+        hipError_t he = hipStreamSynchronize(ctx->stream);
+        if (he != hipSuccess) e = hip_fail(ctx, he, "jpeg kernel");
+    }
+    zpx_plan_destroy(plan);
+    return e;
+}
+
+} // namespace
+
+extern "C" int zpx_jpeg_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+{
+    if (!ctx || !out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    memset(out, 0, sizeof(*out));
+    CtxScope s(ctx);
+    JpegCoeffs c;
+    if (int e = jpeg_entropy_decode(buf, len, c)) return e;
+    const JpegOut kind = jpeg_output_kind(c);
+    if (c.n_comp == 4 && !c.adobe_valid) return ZPX_E_UNSUPPORTED_COLOR_MODEL; // applyBlack :793-795
+    if (kind == JpegOut::YCCK) {
+        ctx->last_error = "YCbCrK (Adobe transform 2) goes through image/util.zig drawYCbCr: out of scope";
+        return ZPX_E_UNSUPPORTED;
+    }
+    JpegLayout L;
+    if (int e = jpeg_layout(c, L)) return e;
+    JpegDeviceFrame d;
+    if (int e = upload_jpeg(ctx, c, d)) return e;
+    DevBuf planes, kplane;
+    HIPCHK(ctx, planes.alloc(L.total));
+    HIPCHK(ctx, hipMemsetAsync(planes.ptr, 0, L.total, ctx->stream)); // makeImg zeroes (image.zig:505-507)
+    uint8_t *pb = planes.as<uint8_t>();
+    d.f.planes[0] = pb;
+    d.f.strides[0] = L.y_stride;
+    if (c.n_comp >= 3) {
+        d.f.planes[1] = pb + L.cb_off;
+        d.f.planes[2] = pb + L.cr_off;
+        d.f.strides[1] = d.f.strides[2] = L.c_stride;
+    }
+    if (c.n_comp == 4) {
+        HIPCHK(ctx, kplane.alloc(L.k_total));
+        HIPCHK(ctx, hipMemsetAsync(kplane.ptr, 0, L.k_total, ctx->stream));
+        d.f.planes[3] = kplane.as<uint8_t>();
+        d.f.strides[3] = L.k_stride;
+    }
+    if (int e = run_plan_once(ctx, d.f, ZPX_JPEG_PLANES)) return e;
+
+    const int W = static_cast<int>(c.width), H = static_cast<int>(c.height);
+    zpx_image img{};
+    img.max_x = W;
+    img.max_y = H;
+    if (kind == JpegOut::Gray || kind == JpegOut::YCbCr) {
+        img.kind = kind == JpegOut::Gray ? ZPX_GRAY : ZPX_YCBCR;
+        img.pixels_len = L.total;
+        img.stride = L.y_stride;
+        img.y_stride = L.y_stride;
+        img.c_stride = L.c_stride;
+        img.cb_off = L.cb_off;
+        img.cr_off = L.cr_off;
+        img.subsample = L.subsample;
+        img.pixels = static_cast<uint8_t *>(al_alloc(al, L.total));
+        if (!img.pixels) return ZPX_E_OUT_OF_MEMORY;
+        hipError_t e = hipMemcpy(img.pixels, planes.ptr, L.total, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            al_free(al, img.pixels, L.total);
+            return hip_fail(ctx, e, "planes copy-back");
+        }
+        if (kind == JpegOut::Gray) img.y_stride = img.c_stride = img.cb_off = img.cr_off = 0;
+        *out = img;
+        return ZPX_OK;
+    }
+    // RGB (convertToRGB) or CMYK (applyBlack): one more device pass
+    zpx_image planar{};
+    planar.kind = ZPX_YCBCR;
+    planar.max_x = W;
+    planar.max_y = H;
+    planar.y_stride = L.y_stride;
+    planar.c_stride = L.c_stride;
+    planar.cb_off = L.cb_off;
+    planar.cr_off = L.cr_off;
+    planar.subsample = L.subsample;
+    const DevImage m = dev_image_of(&planar, planes.ptr, nullptr);
+    const size_t n = size_t(W) * H * 4;
+    DevBuf dout;
+    HIPCHK(ctx, dout.alloc(n));
+    int rc;
+    if (kind == JpegOut::RGB) {
+        rc = launch_jpeg_rgb(m, c.comp[0].h / c.comp[1].h, dout.as<uint8_t>(), ctx->stream);
+        img.kind = ZPX_RGBA;
+    } else {
+        uint32_t sub = 0;
+        for (int t = 0; t < 4; t++)
+            if (c.comp[t].h != c.comp[0].h || c.comp[t].v != c.comp[0].v) sub |= 1u << t;
+        rc = launch_jpeg_cmyk(m, kplane.as<uint8_t>(), L.k_stride, sub, dout.as<uint8_t>(), ctx->stream);
+        img.kind = ZPX_CMYK;
+    }
+    if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg colour kernel");
+    img.pixels_len = n;
+    img.stride = size_t(W) * 4;
+    img.pixels = static_cast<uint8_t *>(al_alloc(al, n));
+    if (!img.pixels) return ZPX_E_OUT_OF_MEMORY;
+    hipError_t e = hipMemcpyAsync(img.pixels, dout.ptr, n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        al_free(al, img.pixels, n);
+        return hip_fail(ctx, e, "rgba copy-back");
+    }
+    *out = img;
+    return ZPX_OK;
+}
+
+extern "C" int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                                    uint8_t **rgba, size_t *rgba_len, uint32_t *width, uint32_t *height)
+{
+    if (!ctx || !rgba || !rgba_len || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    *rgba = nullptr;
+    *rgba_len = 0;
+    CtxScope s(ctx);
+    JpegCoeffs c;
+    if (int e = jpeg_entropy_decode(buf, len, c)) return e;
+    const JpegOut kind = jpeg_output_kind(c);
+    const size_t n = size_t(c.width) * c.height * 4;
+    bool fused = kind != JpegOut::CMYK && kind != JpegOut::YCCK;
+    if (fused && c.n_comp == 3)
+        fused = jpeg_rgba_supported(kind == JpegOut::RGB ? ZPX_JPEG_COLOR_RGB : ZPX_JPEG_COLOR_YCBCR, c.comp[0].h,
+                                    c.comp[0].v, c.comp[1].h, c.comp[1].v);
+    if (!fused) { // planes + rgbaPixels
+        zpx_image img;
+        if (int e = zpx_jpeg_decode(ctx, nullptr, buf, len, &img)) return e;
+        uint8_t *p = nullptr;
+        size_t pl = 0;
+        int e = zpx_image_rgba_pixels(ctx, al, &img, &p, &pl);
+        zpx_image_free(nullptr, &img);
+        if (e) return e;
+        *rgba = p;
+        *rgba_len = pl;
+        if (width) *width = c.width;
+        if (height) *height = c.height;
+        return ZPX_OK;
+    }
+    JpegDeviceFrame d;
+    if (int e = upload_jpeg(ctx, c, d)) return e;
+    DevBuf dout;
+    HIPCHK(ctx, dout.alloc(n));
+    d.f.rgba = dout.as<uint8_t>();
+    d.f.rgba_stride = size_t(c.width) * 4;
+    if (int e = run_plan_once(ctx, d.f, ZPX_JPEG_RGBA)) return e;
+    uint8_t *host = static_cast<uint8_t *>(al_alloc(al, n));
+    if (!host) return ZPX_E_OUT_OF_MEMORY;
+    hipError_t e = hipMemcpy(host, dout.ptr, n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        al_free(al, host, n);
+        return hip_fail(ctx, e, "rgba copy-back");
+    }
+    *rgba = host;
+    *rgba_len = n;
+    if (width) *width = c.width;
+    if (height) *height = c.height;
+    return ZPX_OK;
+}
+
+// ------------------------------------------------------------------ png.decode
+extern "C" int zpx_png_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+{
+    if (!ctx || !out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    memset(out, 0, sizeof(*out));
+    CtxScope s(ctx);
+    PngStream ps;
+    if (int e = png_parse(buf, len, ps)) return e;
+    const size_t out_len = size_t(ps.width) * ps.height * ps.out_bpp;
+    DevBuf din, dout, dmax;
+    HIPCHK(ctx, din.alloc(ps.data_len + ZPX_PNG_INPUT_PAD));
+    HIPCHK(ctx, hipMemcpyAsync(din.ptr, ps.data.ptr, ps.data_len + ZPX_PNG_INPUT_PAD, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, dout.alloc(out_len));
+    HIPCHK(ctx, dmax.alloc(16));
+    HIPCHK(ctx, hipMemsetAsync(dmax.ptr, 0, 16, ctx->stream));
+    zpx_png_frame f;
+    memset(&f, 0, sizeof(f));
+    f.width = ps.width;
+    f.height = ps.height;
+    f.depth = ps.depth;
+    f.interlace = ps.interlace;
+    f.use_transparent = ps.use_transparent;
+    memcpy(f.transparent, ps.transparent, 6);
+    f.filtered = din.as<uint8_t>();
+    f.out = dout.as<uint8_t>();
+    f.out_stride = size_t(ps.width) * ps.out_bpp;
+    f.max_index = ps.kind == ZPX_PALETTED ? dmax.as<int32_t>() : nullptr;
+    zpx_plan *plan = nullptr;
+    if (int e = zpx_png_plan_create(ctx, &f, 1, &plan)) return e;
+    int e = zpx_plan_launch(plan, ctx->stream);
+    if (!e) {
+        hipError_t he = hipStreamSynchronize(ctx->stream);
+        if (he != hipSuccess) e = hip_fail(ctx, he, "png kernel");
+    }
+    if (!e) e = png_plan_status(plan);
+    zpx_plan_destroy(plan);
+    if (e) return e;
+    zpx_image img{};
+    img.kind = ps.kind;
+    img.max_x = static_cast<int32_t>(ps.width);
+    img.max_y = static_cast<int32_t>(ps.height);
+    img.stride = f.out_stride;
+    img.pixels_len = out_len;
+    img.pixels = static_cast<uint8_t *>(al_alloc(al, out_len));
+    if (!img.pixels) return ZPX_E_OUT_OF_MEMORY;
+    hipError_t he = hipMemcpy(img.pixels, dout.ptr, out_len, hipMemcpyDeviceToHost);
+    if (he != hipSuccess) {
+        al_free(al, img.pixels, out_len);
+        return hip_fail(ctx, he, "png copy-back");
+    }
+    if (ps.kind == ZPX_PALETTED) {
+        int32_t maxidx = 0;
+        he = hipMemcpy(&maxidx, dmax.ptr, 4, hipMemcpyDeviceToHost);
+        if (he != hipSuccess) {
+            zpx_image_free(al, &img);
+            return hip_fail(ctx, he, "palette index copy-back");
+        }
+        img.palette = static_cast<zpx_color *>(al_alloc(al, 256 * sizeof(zpx_color)));
+        if (!img.palette) {
+            zpx_image_free(al, &img);
+            return ZPX_E_OUT_OF_MEMORY;
+        }
+        memcpy(img.palette, ps.palette, sizeof(ps.palette));
+        // implicit palette growth (readImagePass :1079-1134)
+        img.palette_len = std::max(ps.palette_len, maxidx + 1);
+    }
+    *out = img;
+    return ZPX_OK;
+}
+
+// ------------------------------------------------------------------ probes / facade
+extern "C" int zpx_jpeg_probe_buffer(const uint8_t *buf, size_t len)
+{
+    return buf && len >= 2 && buf[0] == 0xff && buf[1] == 0xd8;
+}
+extern "C" int zpx_png_probe_buffer(const uint8_t *buf, size_t len)
+{
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    return buf && len >= 8 && memcmp(buf, sig, 8) == 0;
+}
+
+extern "C" int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+{
+    std::vector<uint8_t> data;
+    if (!path) return ZPX_E_INVALID_ARGUMENT;
+    if (int e = read_file(path, data)) return e;
+    return zpx_jpeg_decode(ctx, al, data.data(), data.size(), out);
+}
+
+extern "C" int zpx_png_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+{
+    std::vector<uint8_t> data;
+    if (!path) return ZPX_E_INVALID_ARGUMENT;
+    if (int e = read_file(path, data)) return e;
+    return zpx_png_decode(ctx, al, data.data(), data.size(), out);
+}
+
+extern "C" int zpx_from_buffer(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+{
+    if (zpx_png_probe_buffer(buf, len)) return zpx_png_decode(ctx, al, buf, len, out);
+    if (zpx_jpeg_probe_buffer(buf, len)) return zpx_jpeg_decode(ctx, al, buf, len, out);
+    if (buf && len >= 4 && memcmp(buf, "qoif", 4) == 0) return ZPX_E_UNSUPPORTED; // QOI: out of scope
+    if (buf && len >= 2 && buf[0] == 'B' && buf[1] == 'M') return ZPX_E_UNSUPPORTED; // BMP: out of scope
+    return ZPX_E_UNKNOWN_IMAGE_FORMAT;
+}
+
+extern "C" int zpx_from_file_path(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+{
+    std::vector<uint8_t> data;
+    if (!path) return ZPX_E_INVALID_ARGUMENT;
+    if (int e = read_file(path, data)) return e;
+    return zpx_from_buffer(ctx, al, data.data(), data.size(), out);
+}

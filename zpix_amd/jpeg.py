@@ -1,0 +1,93 @@
+"""jpeg module mirror (src/jpeg/root.zig): load / load_from_buffer / decode /
+probe_*; plus decode_rgba (decode + Image.rgbaPixels fused on the GPU) and
+the host entropy stage for batching."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib, context
+from .image import Image
+
+
+def decode(data: bytes, ctx: context.Context | None = None) -> Image:
+    """jpeg.decode (src/jpeg/decoder.zig:155-176) over an in-memory buffer."""
+    c = ctx or context.default()
+    raw = _lib.zpx_image()
+    _lib.check(_lib.lib().zpx_jpeg_decode(c.handle, None, bytes(data), len(data), C.byref(raw)), c.handle)
+    return Image._from_c(raw)
+
+
+def load_from_buffer(data: bytes, ctx: context.Context | None = None) -> Image:
+    """jpeg.loadFromBuffer (src/jpeg/root.zig:10-15)."""
+    return decode(data, ctx)
+
+
+def load(path: str, ctx: context.Context | None = None) -> Image:
+    """jpeg.load (src/jpeg/root.zig:36-53)."""
+    c = ctx or context.default()
+    raw = _lib.zpx_image()
+    _lib.check(_lib.lib().zpx_jpeg_load(c.handle, None, path.encode(), C.byref(raw)), c.handle)
+    return Image._from_c(raw)
+
+
+def probe_buffer(data: bytes) -> bool:
+    """jpeg.probeBuffer (src/jpeg/root.zig:17-21)."""
+    return bool(_lib.lib().zpx_jpeg_probe_buffer(bytes(data[:2]), min(len(data), 2)))
+
+
+def probe_path(path: str) -> bool:
+    """jpeg.probePath (src/jpeg/root.zig:23-33)."""
+    with open(path, "rb") as f:
+        return probe_buffer(f.read(2))
+
+
+def decode_rgba(data: bytes, ctx: context.Context | None = None):
+    """decode + Image.rgbaPixels in one fused kernel: returns (rgba uint8 HxWx4)."""
+    c = ctx or context.default()
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_size_t(0)
+    w = C.c_uint32(0)
+    h = C.c_uint32(0)
+    _lib.check(_lib.lib().zpx_jpeg_decode_rgba(c.handle, None, bytes(data), len(data), C.byref(out), C.byref(n),
+                                               C.byref(w), C.byref(h)), c.handle)
+    try:
+        return np.ctypeslib.as_array(out, shape=(n.value,)).copy().reshape(h.value, w.value, 4)
+    finally:
+        C.CDLL(None).free(out)
+
+
+class Coefficients:
+    """Host entropy stage output (pinned coefficient grids + frame descriptor)."""
+
+    def __init__(self, data: bytes):
+        h = C.c_void_p()
+        self._data = bytes(data)
+        _lib.check(_lib.lib().zpx_jpeg_entropy_decode(self._data, len(self._data), C.byref(h)))
+        self.handle = h
+        self.frame = _lib.zpx_jpeg_frame()
+        sizes = (C.c_size_t * 4)()
+        _lib.check(_lib.lib().zpx_jpeg_coeffs_frame(h, C.byref(self.frame), sizes))
+        self.coeff_bytes = [int(s) for s in sizes]
+
+    def grid(self, comp: int) -> np.ndarray:
+        """Coefficient grid of a component as (blocks, 64) int16/int32 (host view)."""
+        ptr = self.frame.coeffs[comp]
+        if not ptr:
+            return None
+        dt = np.int16 if self.frame.coeff_bits == 16 else np.int32
+        n = self.coeff_bytes[comp] // np.dtype(dt).itemsize
+        return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int16 if dt == np.int16 else C.c_int32)),
+                                     shape=(n,)).reshape(-1, 64)
+
+    def close(self):
+        if self.handle:
+            _lib.lib().zpx_jpeg_coeffs_free(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
