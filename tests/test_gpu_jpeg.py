@@ -201,7 +201,7 @@ def test_jpeg_batch_4k_fused_matches_oracle():
     want = O.jpeg_decode(data).rgba_pixels().reshape(4096, 4096, 4)
     for s in range(2):
         assert torch.equal(batch.output_tensor(s).cpu(), torch.from_numpy(want))
-    assert batch.bytes == 393216 * 128 + 4096 * 4096 * 4 + 3 * 256
+    assert batch.bytes == 2 * (393216 * 128 + 4096 * 4096 * 4 + 3 * 256)
 
 
 def test_jpeg_batch_planes_matches_oracle():

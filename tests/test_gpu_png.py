@@ -119,7 +119,7 @@ def test_png_bench_size_roundtrip():
     for s in range(2):
         got = batch.output_tensor(s).cpu().numpy().reshape(4096, 4096, 4)
         assert np.array_equal(got, want)
-    assert batch.bytes == 4096 * (1 + 4096 * 3) + 4096 * 4096 * 4
+    assert batch.bytes == 2 * (4096 * (1 + 4096 * 3) + 4096 * 4096 * 4)
 
 
 def test_png_adam7_rgba16_roundtrip():

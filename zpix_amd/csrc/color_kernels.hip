@@ -27,7 +27,11 @@ __device__ __forceinline__ uint32_t ycc_rgba8(int32_t Y, int32_t Cb, int32_t Cr)
     const int32_t r = yy1 + __mul24(91881, cr1);
     const int32_t g = yy1 - __mul24(22554, cb1) - __mul24(46802, cr1);
     const int32_t b = yy1 + __mul24(116130, cb1);
-    return pack4(min(max(r >> 16, 0), 255), min(max(g >> 16, 0), 255), min(max(b >> 16, 0), 255), 255);
+    // clamp before the shift: (v>>16 clamped to 0..255) == clamp(v, 0, 2^24-1) >> 16.  Written
+    // this way hipcc (ROCm 7.2) does not select v_ashr_pk_u8_i32, which produced a wrong blue
+    // byte on gfx950.
+    return pack4(static_cast<uint32_t>(min(max(r, 0), 0xffffff)) >> 16, static_cast<uint32_t>(min(max(g, 0), 0xffffff)) >> 16,
+                 static_cast<uint32_t>(min(max(b, 0), 0xffffff)) >> 16, 255);
 }
 
 // .nrgba premultiply (color.zig:52-72): ((c*0x101)*a/0xff) >> 8

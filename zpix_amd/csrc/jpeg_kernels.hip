@@ -333,15 +333,16 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
                     pix = static_cast<uint32_t>(Yv) | static_cast<uint32_t>(cb) << 8 |
                           static_cast<uint32_t>(cr) << 16 | 0xff000000u;
                 } else {
-                    // color.zig:95-106; 8-bit result of (v>>8 or clamp)>>8 == clamp(v>>16, 0, 255)
+                    // color.zig:95-106; 8-bit result of (v>>8 or clamp)>>8 == clamp(v, 0, 2^24-1)>>16
+                    // (clamp before the shift: see ycc_rgba8 in color_kernels.hip)
                     const int32_t yy1 = __mul24(Yv, 0x10101);
                     const int32_t cb1 = cb - 128, cr1 = cr - 128;
                     const int32_t r = yy1 + __mul24(91881, cr1);
                     const int32_t g = yy1 - __mul24(22554, cb1) - __mul24(46802, cr1);
                     const int32_t b = yy1 + __mul24(116130, cb1);
-                    const uint32_t R = static_cast<uint32_t>(min(max(r >> 16, 0), 255));
-                    const uint32_t G = static_cast<uint32_t>(min(max(g >> 16, 0), 255));
-                    const uint32_t B = static_cast<uint32_t>(min(max(b >> 16, 0), 255));
+                    const uint32_t R = static_cast<uint32_t>(min(max(r, 0), 0xffffff)) >> 16;
+                    const uint32_t G = static_cast<uint32_t>(min(max(g, 0), 0xffffff)) >> 16;
+                    const uint32_t B = static_cast<uint32_t>(min(max(b, 0), 0xffffff)) >> 16;
                     pix = R | G << 8 | B << 16 | 0xff000000u;
                 }
             }
