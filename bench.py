@@ -63,7 +63,10 @@ def dist_env():
 def timed_steps(torch, dist, launch, steps, warmup, ws):
     """W untimed steps; K timed steps bracketed by barrier + synchronize; HIP
     events on the launch stream give the average per-launch kernel time."""
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-null) stream: the plan launches on it and the HIP events
+    # are recorded on it, so the event time is the kernels' time
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     for _ in range(warmup):
         launch(stream.cuda_stream)
     torch.cuda.synchronize()
