@@ -219,46 +219,100 @@ __global__ __launch_bounds__(kThreads) void jpeg_planar_kernel(const DevJpegFram
 
 // ---------------------------------------------------------------------------
 // Fused reconstruct + Image.rgbaPixels.  A workgroup owns a horizontal strip
-// of T MCUs of one MCU row:
-//   phase 1: lane = (block, row): load, dequant, row IDCT -> LDS (all blocks);
-//   phase 2: chroma columns -> clamped samples in an LDS chroma tile;
-//   phase 3: luma columns -> clamped Y, nearest chroma from LDS, YCbCr->RGB,
-//            one 4-byte RGBA store per pixel (a wave writes 64 adjacent
-//            pixels = 256 contiguous bytes per store instruction).
+// of T MCUs of one MCU row and walks strips persistently (grid-stride), with
+// the next strip's coefficient rows prefetched into registers while the
+// current one is in its LDS phases:
+//   P1: lane = (block, row): dequant + row IDCT -> LDS row buffer;
+//   P2: chroma columns -> clamped samples in an LDS chroma tile;
+//   P3a: luma columns -> clamped Y kept in registers;
+//   P3b: nearest chroma + YCbCr->RGB -> RGBA dwords in an LDS tile that
+//        reuses the row buffer;
+//   P3c: 16-byte stores, a wave writes 1 KiB of one output row per instruction.
 // ---------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+#define ZPX_GLOBAL __attribute__((address_space(1)))
+
 constexpr int strip_mcus(int blocks_per_mcu) { return blocks_per_mcu >= 96 ? 1 : 96 / blocks_per_mcu; }
 
+template <typename CoefT>
+struct RowRegs { // one coefficient row, raw (not yet dequantized)
+    u32x4 a;
+    u32x4 b; // int32 coefficients only
+};
+
+template <typename CoefT>
+__device__ __forceinline__ void load_row_raw(const CoefT *p, RowRegs<CoefT> &r)
+{
+    const ZPX_GLOBAL u32x4 *g = (const ZPX_GLOBAL u32x4 *)p;
+    r.a = g[0];
+    if constexpr (sizeof(CoefT) == 4) r.b = g[1];
+}
+
+template <typename CoefT>
+__device__ __forceinline__ void unpack_dequant(const RowRegs<CoefT> &r, const int32_t *__restrict__ q, int32_t s[8])
+{
+    if constexpr (sizeof(CoefT) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t w = r.a[i];
+            s[2 * i] = static_cast<int32_t>(static_cast<int16_t>(w & 0xffff));
+            s[2 * i + 1] = static_cast<int32_t>(w) >> 16;
+        }
+        // |coef| < 2^15 and q < 2^17: the 24-bit multiply is exact
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = __mul24(s[i], q[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            s[i] = static_cast<int32_t>(r.a[i]);
+            s[4 + i] = static_cast<int32_t>(r.b[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = s[i] * q[i];
+    }
+}
+
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
-__global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames)
+__global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames, int strips_x,
+                                                             int strips_per_frame, int total_strips)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
     constexpr int kYB = H0 * V0;                      // luma blocks per MCU
     constexpr int kCB = kGray ? 0 : HC * VC;          // blocks per chroma component per MCU
-    constexpr int T = strip_mcus(kYB + 2 * kCB);      // MCUs per workgroup
+    constexpr int T = strip_mcus(kYB + 2 * kCB);      // MCUs per strip
     constexpr int NY = T * kYB, NC = T * kCB, NB = NY + 2 * NC;
     constexpr int YW = T * H0;                        // luma blocks across the strip
     constexpr int CW = T * HC;                        // chroma blocks across the strip
     constexpr int CPX = kGray ? 1 : CW * 8;           // chroma tile width (samples)
     constexpr int CROWS = kGray ? 1 : VC * 8;
     constexpr int RX = kGray ? 1 : H0 / HC, RY = kGray ? 1 : V0 / VC; // upsample ratios
+    constexpr int PXW = YW * 8;                       // strip width in pixels
+    constexpr int PXH = V0 * 8;                       // strip height in pixels
+    constexpr int ROW_IT = (NB * 8 + kThreads - 1) / kThreads;
+    constexpr int YCOL_IT = (NY * 8 + kThreads - 1) / kThreads;
+    constexpr int CCOL_IT = (2 * NC * 8 + kThreads - 1) / kThreads;
+    constexpr int CHUNKS = PXH * PXW / 4;             // 16-byte output chunks per strip
+    constexpr int OUT_IT = (CHUNKS + kThreads - 1) / kThreads;
+    static_assert(PXH * PXW <= NB * kBlkStride, "RGBA tile must fit in the row buffer");
 
     __shared__ int32_t qs[3][64];
-    __shared__ int32_t buf[NB * kBlkStride];
-    __shared__ int32_t ctile[2][CROWS * CPX];
+    __shared__ __attribute__((aligned(16))) int32_t buf[NB * kBlkStride]; // row pass, then RGBA tile
+    __shared__ int32_t ctile[kGray ? 1 : 2][CROWS * CPX];
 
-    const DevJpegFrame &fr = frames[blockIdx.y];
-    const int my = blockIdx.z;
-    if (my >= fr.myy) return;
-    const int mx0 = blockIdx.x * T;
-    if (mx0 >= fr.mxx) return;
     const int tid = threadIdx.x;
-    const int ncomp = kGray ? 1 : 3;
-    for (int i = tid; i < ncomp * 64; i += kThreads) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
-    __syncthreads();
+    constexpr int ncomp = kGray ? 1 : 3;
 
-    // ---- phase 1: rows
-    for (int task = tid; task < NB * 8; task += kThreads) {
-        const int blk = task >> 3, r = task & 7;
+    // strip -> (frame, MCU row, first MCU column)
+    auto strip_of = [&](int st, int &f, int &my, int &mx0) {
+        f = st / strips_per_frame;
+        const int r = st - f * strips_per_frame;
+        my = r / strips_x;
+        mx0 = (r - my * strips_x) * T;
+    };
+    // coefficient row address of row-task k of a strip (nullptr: nothing to load)
+    auto row_ptr = [&](const DevJpegFrame &fr, int my, int mx0, int k) -> const CoefT * {
+        const int blk = k >> 3, r = k & 7;
         int comp, bx, by, gw;
         if (blk < NY) {
             comp = 0;
@@ -266,88 +320,179 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
             by = my * V0 + blk / YW;
             gw = fr.mxx * H0;
         } else {
-            const int k = (blk - NY) % (NC > 0 ? NC : 1);
-            comp = blk < NY + NC ? 1 : 2;
-            bx = mx0 * HC + k % CW;
-            by = my * VC + k / CW;
+            const int c = blk - NY;
+            const int kk = NC > 0 ? c % NC : 0;
+            comp = c < NC ? 1 : 2;
+            bx = mx0 * HC + kk % CW;
+            by = my * VC + kk / CW;
             gw = fr.mxx * HC;
         }
         const CoefT *grid = static_cast<const CoefT *>(fr.coeffs[comp]);
-        int32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (grid != nullptr && bx < gw) {
-            load_row<CoefT>(grid + (static_cast<size_t>(by) * gw + bx) * 64 + r * 8, qs[comp] + r * 8, s);
-            idct_row<NARROW>(s);
-        }
-        int32_t *d = buf + blk * kBlkStride + r * 8;
-#pragma unroll
-        for (int i = 0; i < 8; i++) d[i] = s[i];
-    }
-    __syncthreads();
+        if (grid == nullptr || bx >= gw || blk >= NB || my >= fr.myy) return nullptr; // ragged batch: skip
+        return grid + (static_cast<size_t>(by) * gw + bx) * 64 + r * 8;
+    };
 
-    // ---- phase 2: chroma columns -> LDS tile
-    if constexpr (!kGray) {
-        for (int task = tid; task < 2 * NC * 8; task += kThreads) {
-            const int k = task >> 3, c = task & 7;
-            const int comp = k < NC ? 1 : 2;
-            const int kk = k % NC;
-            const int blk = NY + k;
-            int32_t s[8];
+    RowRegs<CoefT> pre[ROW_IT];
+    int st = blockIdx.x;
+    int f = 0, my = 0, mx0 = 0;
+    if (st < total_strips) {
+        strip_of(st, f, my, mx0);
 #pragma unroll
-            for (int i = 0; i < 8; i++) s[i] = buf[blk * kBlkStride + i * 8 + c];
-            idct_col_clamp<NARROW>(s);
-            const bool present = fr.coeffs[comp] != nullptr; // component never scanned: samples 0
-            int32_t *t = ctile[comp - 1] + ((kk / CW) * 8) * CPX + (kk % CW) * 8 + c;
+        for (int it = 0; it < ROW_IT; it++) {
+            const CoefT *p = row_ptr(frames[f], my, mx0, it * kThreads + tid);
+            if (p) load_row_raw<CoefT>(p, pre[it]);
+        }
+    }
+    int qframe = -1;
+    for (; st < total_strips; st += gridDim.x) {
+        const DevJpegFrame &fr = frames[f];
+        if (f != qframe) { // quant tables of this frame (natural order)
+            for (int i = tid; i < ncomp * 64; i += kThreads) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
+            qframe = f;
+            __syncthreads();
+        }
+        // ---- P1: dequant + row IDCT of the prefetched rows
 #pragma unroll
-            for (int i = 0; i < 8; i++) t[i * CPX] = present ? s[i] : 0;
+        for (int it = 0; it < ROW_IT; it++) {
+            const int k = it * kThreads + tid;
+            if (k >= NB * 8) break;
+            const int blk = k >> 3, r = k & 7;
+            const int comp = blk < NY ? 0 : (blk < NY + NC ? 1 : 2);
+            int32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (row_ptr(fr, my, mx0, k) != nullptr) {
+                unpack_dequant<CoefT>(pre[it], qs[comp] + r * 8, s);
+                idct_row<NARROW>(s);
+            }
+            // two 16-byte LDS writes; rows 4..7 write their halves in swapped
+            // order so the 8 lanes of a write group hit distinct banks
+            int32_t *d = buf + blk * kBlkStride + r * 8;
+            const bool sw = (r & 4) != 0;
+            i32x4 lo = {s[0], s[1], s[2], s[3]}, hi = {s[4], s[5], s[6], s[7]};
+            *reinterpret_cast<i32x4 *>(d + (sw ? 4 : 0)) = sw ? hi : lo;
+            *reinterpret_cast<i32x4 *>(d + (sw ? 0 : 4)) = sw ? lo : hi;
+        }
+        // ---- prefetch the next strip's rows (consumed next iteration)
+        const int st_next = st + gridDim.x;
+        int fn = f, myn = my, mxn = mx0;
+        if (st_next < total_strips) {
+            strip_of(st_next, fn, myn, mxn);
+#pragma unroll
+            for (int it = 0; it < ROW_IT; it++) {
+                const CoefT *p = row_ptr(frames[fn], myn, mxn, it * kThreads + tid);
+                if (p) load_row_raw<CoefT>(p, pre[it]);
+            }
         }
         __syncthreads();
-    }
 
-    // ---- phase 3: luma columns + colour + store
-    const int W = fr.width, H = fr.height;
-    uint8_t *const out = fr.rgba;
-    const size_t ostride = fr.rgba_stride;
-    for (int task = tid; task < NY * 8; task += kThreads) {
-        const int blk = task >> 3, c = task & 7;
-        const int yrow = blk / YW, ycol = blk % YW;
-        int32_t s[8];
+        // ---- P2: chroma columns -> LDS tile
+        if constexpr (!kGray) {
+            const bool cb_present = fr.coeffs[1] != nullptr, cr_present = fr.coeffs[2] != nullptr;
 #pragma unroll
-        for (int i = 0; i < 8; i++) s[i] = buf[blk * kBlkStride + i * 8 + c];
-        idct_col_clamp<NARROW>(s);
-        const int px = ycol * 8 + c;             // x within the strip
-        const int X = mx0 * H0 * 8 + px;
-        const int Y0 = (my * V0 + yrow) * 8;
-        if (X >= W) continue;
-        uint8_t *o = out + static_cast<size_t>(Y0) * ostride + static_cast<size_t>(X) * 4;
+            for (int it = 0; it < CCOL_IT; it++) {
+                const int task = it * kThreads + tid;
+                if (task >= 2 * NC * 8) break;
+                const int k = task >> 3, c = task & 7;
+                const int comp = k < NC ? 1 : 2;
+                const int kk = k < NC ? k : k - NC;
+                const int blk = NY + k;
+                int32_t s[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            if (Y0 + i >= H) break;
-            const int32_t Yv = s[i];
-            uint32_t pix;
-            if constexpr (kGray) {
-                pix = static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
-            } else {
-                const int cx = px / RX, cy = (yrow * 8 + i) / RY;
-                const int32_t cb = ctile[0][cy * CPX + cx], cr = ctile[1][cy * CPX + cx];
-                if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
-                    pix = static_cast<uint32_t>(Yv) | static_cast<uint32_t>(cb) << 8 |
-                          static_cast<uint32_t>(cr) << 16 | 0xff000000u;
-                } else {
-                    // color.zig:95-106; 8-bit result of (v>>8 or clamp)>>8 == clamp(v, 0, 2^24-1)>>16
-                    // (clamp before the shift: see ycc_rgba8 in color_kernels.hip)
-                    const int32_t yy1 = __mul24(Yv, 0x10101);
-                    const int32_t cb1 = cb - 128, cr1 = cr - 128;
-                    const int32_t r = yy1 + __mul24(91881, cr1);
-                    const int32_t g = yy1 - __mul24(22554, cb1) - __mul24(46802, cr1);
-                    const int32_t b = yy1 + __mul24(116130, cb1);
-                    const uint32_t R = static_cast<uint32_t>(min(max(r, 0), 0xffffff)) >> 16;
-                    const uint32_t G = static_cast<uint32_t>(min(max(g, 0), 0xffffff)) >> 16;
-                    const uint32_t B = static_cast<uint32_t>(min(max(b, 0), 0xffffff)) >> 16;
-                    pix = R | G << 8 | B << 16 | 0xff000000u;
+                for (int i = 0; i < 8; i++) s[i] = buf[blk * kBlkStride + i * 8 + c];
+                idct_col_clamp<NARROW>(s);
+                const bool present = comp == 1 ? cb_present : cr_present; // never scanned: samples 0
+                int32_t *t = ctile[comp - 1] + ((kk / CW) * 8) * CPX + (kk % CW) * 8 + c;
+#pragma unroll
+                for (int i = 0; i < 8; i++) t[i * CPX] = present ? s[i] : 0;
+            }
+            __syncthreads();
+        }
+
+        // ---- P3a: luma columns
+        int32_t yv[YCOL_IT][8];
+#pragma unroll
+        for (int it = 0; it < YCOL_IT; it++) {
+            const int task = it * kThreads + tid;
+            if (task < NY * 8) {
+                const int blk = task >> 3, c = task & 7;
+#pragma unroll
+                for (int i = 0; i < 8; i++) yv[it][i] = buf[blk * kBlkStride + i * 8 + c];
+                idct_col_clamp<NARROW>(yv[it]);
+            }
+        }
+        __syncthreads(); // row buffer is free: reuse it as the RGBA tile
+
+        // ---- P3b: colour -> RGBA tile [PXH][PXW]
+        uint32_t *otile = reinterpret_cast<uint32_t *>(buf);
+#pragma unroll
+        for (int it = 0; it < YCOL_IT; it++) {
+            const int task = it * kThreads + tid;
+            if (task >= NY * 8) break;
+            const int blk = task >> 3, c = task & 7;
+            const int yrow = blk / YW, ycol = blk % YW;
+            const int px = ycol * 8 + c;
+            uint32_t *o = otile + (yrow * 8) * PXW + px;
+#pragma unroll
+            for (int i0 = 0; i0 < 8; i0 += RY) {
+                int32_t cb = 0, cr = 0;
+                if constexpr (!kGray) {
+                    const int ci = ((yrow * 8 + i0) / RY) * CPX + px / RX;
+                    cb = ctile[0][ci];
+                    cr = ctile[1][ci];
+                }
+#pragma unroll
+                for (int j = 0; j < RY; j++) {
+                    const int i = i0 + j;
+                    const int32_t Yv = yv[it][i];
+                    uint32_t pix;
+                    if constexpr (kGray) {
+                        pix = static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
+                    } else if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
+                        pix = static_cast<uint32_t>(Yv) | static_cast<uint32_t>(cb) << 8 |
+                              static_cast<uint32_t>(cr) << 16 | 0xff000000u;
+                    } else {
+                        // color.zig:95-106; 8-bit result of (v>>8 or clamp)>>8 == clamp(v, 0, 2^24-1)>>16
+                        // (clamp before the shift: see ycc_rgba8 in color_kernels.hip)
+                        const int32_t yy1 = __mul24(Yv, 0x10101);
+                        const int32_t cb1 = cb - 128, cr1 = cr - 128;
+                        const int32_t r = yy1 + __mul24(91881, cr1);
+                        const int32_t g = yy1 - __mul24(22554, cb1) - __mul24(46802, cr1);
+                        const int32_t b = yy1 + __mul24(116130, cb1);
+                        const uint32_t R = static_cast<uint32_t>(min(max(r, 0), 0xffffff)) >> 16;
+                        const uint32_t G = static_cast<uint32_t>(min(max(g, 0), 0xffffff)) >> 16;
+                        const uint32_t B = static_cast<uint32_t>(min(max(b, 0), 0xffffff)) >> 16;
+                        pix = R | G << 8 | B << 16 | 0xff000000u;
+                    }
+                    o[i * PXW] = pix;
                 }
             }
-            *reinterpret_cast<uint32_t *>(o + i * ostride) = pix;
         }
+        __syncthreads();
+
+        // ---- P3c: 16-byte stores of the tile
+        const int W = fr.width, H = fr.height;
+        const int X0 = mx0 * H0 * 8, Y0 = my * V0 * 8;
+        const size_t ostride = fr.rgba_stride;
+        uint8_t *const out = fr.rgba;
+        const bool vec_ok = (ostride & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+#pragma unroll
+        for (int it = 0; it < OUT_IT; it++) {
+            const int q = it * kThreads + tid;
+            if (q >= CHUNKS) break;
+            const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
+            const int Y = Y0 + row, X = X0 + cx;
+            if (Y >= H || X >= W) continue;
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
+            uint8_t *dst = out + static_cast<size_t>(Y) * ostride + static_cast<size_t>(X) * 4;
+            if (vec_ok && X + 4 <= W) {
+                *(ZPX_GLOBAL u32x4 *)dst = v;
+            } else {
+                for (int e = 0; e < 4 && X + e < W; e++) ((ZPX_GLOBAL uint32_t *)dst)[e] = v[e];
+            }
+        }
+        __syncthreads(); // tile / row buffer reused by the next strip
+        f = fn;
+        my = myn;
+        mx0 = mxn;
     }
 }
 
@@ -371,14 +516,29 @@ int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, i
 }
 
 namespace {
+int persistent_workgroups()
+{
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        n = cus * 4; // 4 resident 256-thread workgroups per CU (LDS ~37 KiB each)
+    }
+    return n;
+}
+
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
 void launch_rgba_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int max_myy, hipStream_t stream)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
     constexpr int T = strip_mcus(H0 * V0 + 2 * (kGray ? 0 : HC * VC));
-    dim3 grid((max_mxx + T - 1) / T, n_frames, max_myy);
-    hipLaunchKernelGGL((jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>), grid, dim3(kThreads), 0,
-                       stream, d_frames);
+    const int strips_x = (max_mxx + T - 1) / T;
+    const int per_frame = strips_x * max_myy;
+    const int total = per_frame * n_frames;
+    const int grid = total < persistent_workgroups() ? total : persistent_workgroups();
+    hipLaunchKernelGGL((jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>), dim3(grid), dim3(kThreads), 0,
+                       stream, d_frames, strips_x, per_frame, total);
 }
 
 template <typename CoefT, bool NARROW, int COLOR>
