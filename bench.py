@@ -60,6 +60,23 @@ def dist_env():
     return ws, rank, local
 
 
+def shard_images(total: int, rank: int, ws: int) -> list[int]:
+    """Global image ids owned by `rank`: image i -> GPU i mod N.
+    Images are independent, so the shards share nothing."""
+    return [i for i in range(total) if i % ws == rank]
+
+
+def max_over_ranks(dist, value: float, device) -> float:
+    """The slowest rank's wall time (the whole job ends when it does)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    import torch
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def timed_steps(torch, dist, launch, steps, warmup, ws):
     """W untimed steps; K timed steps bracketed by barrier + synchronize; HIP
     events on the launch stream give the average per-launch kernel time."""
@@ -86,11 +103,7 @@ def timed_steps(torch, dist, launch, steps, warmup, ws):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / steps
-    if ws > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-    return wall, kern_ms
+    return max_over_ranks(dist, wall, "cuda"), kern_ms
 
 
 def cpu_baseline_jpeg(data: bytes, seconds: float):
@@ -161,7 +174,9 @@ def main():
     # ------------------------------------------------------------ JPEG (headline)
     if not args.png_only:
         t0 = time.perf_counter()
-        datas = [S.jpeg_420(rank * args.distinct + j, W, H, args.quality) for j in range(args.distinct)]
+        mine = shard_images(args.images * ws, rank, ws)  # this rank's global image ids
+        # the first `distinct` ids of the shard are synthesised (seed = image id); slots cycle them
+        datas = [S.jpeg_420(i, W, H, args.quality) for i in mine[:args.distinct]]
         t_gen = time.perf_counter() - t0
         t0 = time.perf_counter()
         coeffs = [jpeg.Coefficients(d) for d in datas]
@@ -239,7 +254,8 @@ def main():
     # ------------------------------------------------------------ PNG (configs[2])
     if not args.no_png:
         t0 = time.perf_counter()
-        pdatas = [S.png_tc8_mixed(rank * args.distinct + j, W, H) for j in range(args.distinct)]
+        mine = shard_images(args.images * ws, rank, ws)
+        pdatas = [S.png_tc8_mixed(i, W, H) for i in mine[:args.distinct]]
         t_gen = time.perf_counter() - t0
         t0 = time.perf_counter()
         streams = [png.Stream(d) for d in pdatas]
