@@ -19,9 +19,11 @@ int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int 
 
 // png_kernels.hip
 int png_chunk_bytes(int depth);
+// uint64 granules of boundary buffer per band for rows of up to max_row_bytes
+int png_band_granules(int depth, uint32_t max_row_bytes);
+// ctl: 4 device words {epoch, ticket, status, pad}; boundary: nbands * band_granules
 int launch_png_unfilter(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                        uint32_t *ticket, uint32_t *progress, uint8_t *boundary, uint32_t band_bytes,
-                        uint32_t *status, hipStream_t s);
+                        uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s);
 
 // color_kernels.hip
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);

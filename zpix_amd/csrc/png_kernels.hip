@@ -11,14 +11,16 @@
 //     at step t lane j reconstructs chunk t-j (a one-chunk skew per row);
 //   - the row above arrives from lane j-1 through a DPP wave_shr:1 of the
 //     chunk it produced one step earlier (no LDS round trip);
-//   - lane 0 takes the previous band's last row from a boundary buffer that
-//     the previous band's lane 63 publishes region by region (16 chunks),
-//     with write-through (sc1) stores + s_waitcnt vmcnt(0) + an agent-scope
-//     flag store, consumed with sc1 loads (MI355X_MICROARCH.md visibility
-//     table, row 1).  A region is read only after it is complete.
-//   - bands are dequeued with an atomic ticket in band-major order, so the
-//     predecessor of any running band has already been dequeued by a running
-//     wave: no co-residency assumption, no deadlock; every spin is bounded.
+//   - lane 0 takes the previous band's last row from a boundary buffer the
+//     previous band's lane 63 fills with 8-byte {epoch, data} granules
+//     (agent-scope sc1 stores, no drain), polled with sc1 loads until every
+//     tag equals this launch's epoch (MI355X_MICROARCH.md visibility, R2:
+//     the data is the flag).  A 16-chunk window is prefetched half a window
+//     ahead, so the producer never stalls and the consumer rarely does.
+//   - a persistent grid of waves dequeues bands with an atomic ticket in
+//     band-major order; a wave only waits for a band with a smaller ticket,
+//     which a running wave holds: no co-residency assumption, no deadlock;
+//     every spin is bounded (timeout -> status word).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -30,7 +32,6 @@ namespace zpx {
 namespace {
 
 constexpr int kRegionChunks = 16;
-constexpr uint32_t kRegionBytes = 256;
 constexpr uint32_t kSpinLimit = 1u << 24;
 
 template <int DEPTH>
@@ -62,33 +63,6 @@ ZPX_PNG_TRAITS(ZPX_PNG_TCA16, 64)
 #undef ZPX_PNG_TRAITS
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t *w, int i) { return (w[i >> 2] >> ((i & 3) * 8)) & 0xff; }
-
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Predictor of one byte for filter ft (decoder.zig:806-842, :1152-1182).
-// a = left, b = up, c = up-left (all 0 where the reference uses the
-// "first bpp bytes" special cases, which is the same value).
-__device__ __forceinline__ uint32_t predict(int ft, int a, int b, int c)
-{
-    const int pa = abs(b - c);         // |p - a| with p = a + b - c
-    const int pb = abs(a - c);         // |p - b|
-    const int pc = abs(a + b - 2 * c); // |p - c|
-    const int paeth = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-    const int avg = (a + b) >> 1;
-    int p = 0;
-    p = ft == 1 ? a : p;
-    p = ft == 2 ? b : p;
-    p = ft == 3 ? avg : p;
-    p = ft == 4 ? paeth : p;
-    return static_cast<uint32_t>(p);
-}
 
 // Store n bytes held in dwords w[] to dst, using 16-byte stores when aligned.
 template <int NB>
@@ -283,156 +257,238 @@ __device__ __forceinline__ void store_chunk(const DevPngPass &ps, uint32_t y, ui
     }
 }
 
+__device__ __forceinline__ uint64_t ld_sc1_64(const uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_64(uint64_t *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Reconstruct one byte: out = (f + pred) & 0xff with the predictor of the
+// lane's filter.  b (up), c (up-left) and everything derived from them only
+// are off the left-to-right dependency chain; a (left) is on it.
+// Paeth (:1152-1182) as one v_min3 over keys (dist << 10 | tiebreak << 8 | value):
+// the smallest distance wins, ties go a < b < c, exactly the reference's rule.
+struct LaneFilter {
+    bool sub, up, avg, paeth;
+};
+__device__ __forceinline__ uint32_t recon_byte(const LaneFilter &lf, uint32_t f, uint32_t a, uint32_t b, uint32_t c)
+{
+    const uint32_t pa = __builtin_amdgcn_sad_u16(b, c, 0);      // |p - a| = |b - c|
+    const uint32_t pb = __builtin_amdgcn_sad_u16(a, c, 0);      // |p - b| = |a - c|
+    const uint32_t s = a + b;
+    const uint32_t pc = __builtin_amdgcn_sad_u16(s, 2 * c, 0);  // |p - c| = |a + b - 2c|
+    const uint32_t m = min(min((pa << 10) | a, (pb << 10) | 0x100u | b), (pc << 10) | 0x200u | c);
+    uint32_t t = lf.up ? b : 0u;
+    t = lf.sub ? a : t;
+    t = lf.avg ? (s >> 1) : t;
+    t = lf.paeth ? m : t;
+    return (f + t) & 0xffu;
+}
+
 template <int DEPTH>
 __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__restrict__ passes,
                                                           const DevPngBand *__restrict__ sched, uint32_t nsched,
-                                                          uint32_t *ticket, uint32_t *progress, uint8_t *boundary,
-                                                          uint32_t band_bytes, uint32_t *status)
+                                                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules)
 {
     using Tr = Traits<DEPTH>;
     constexpr int BPP = Tr::kBpp, C = Tr::kC, CW = Tr::kCW;
+    constexpr int WIN = kRegionChunks;          // chunks per window
+    constexpr int WG = WIN * CW;                // granules per window (<= 64)
+    static_assert(WG <= 64, "window must fit one granule per lane");
     const int lane = threadIdx.x;
-
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(ticket, 1u);
-    t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
-    if (t >= nsched) return;
-    const DevPngBand bd = sched[t];
-    const DevPngPass &ps = passes[bd.pass];
-    const uint32_t rb = ps.row_bytes;
-    const uint32_t nunits = (rb + BPP - 1) / BPP;
-    const int nchunks = static_cast<int>((nunits + C - 1) / C);
-    const uint32_t y = bd.band * 64 + lane;
-    const bool row_ok = y < ps.rows;
-    const uint8_t *frow = ps.filtered + static_cast<size_t>(y) * (rb + 1);
-    const int ft = row_ok ? frow[0] : 0;
-    const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(frow + 1) & 3);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(frow + 1 - mis);
-
-    const bool has_prev = bd.band > 0;
-    const bool has_next = bd.band + 1 < ps.nbands;
-    const uint32_t *prev_bnd = reinterpret_cast<const uint32_t *>(
-        boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) * band_bytes);
-    uint32_t *my_bnd = reinterpret_cast<uint32_t *>(boundary + static_cast<size_t>(ps.band_base + bd.band) * band_bytes);
-    const uint32_t *prev_prog = progress + ps.band_base + bd.band - (has_prev ? 1 : 0);
-    uint32_t *my_prog = progress + ps.band_base + bd.band;
-
-    uint32_t left[BPP], ul[BPP];
-#pragma unroll
-    for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
-    uint32_t outp[CW];
-#pragma unroll
-    for (int i = 0; i < CW; i++) outp[i] = 0;
-    uint32_t carry = 0, region = 0, seen = 0;
-    int maxidx = 0;
+    const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
+    uint32_t *ticket = ctl + 1, *status = ctl + 2;
     bool timed_out = false;
 
-    for (int step = 0; step < nchunks + 63; ++step) {
-        const int k = step - lane;
-        const bool act = row_ok && k >= 0 && k < nchunks;
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(ticket, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+        if (t >= nsched) break;
+        const DevPngBand bd = sched[t];
+        const DevPngPass ps = passes[bd.pass]; // registers: no reloads after output stores
+        const uint32_t rb = ps.row_bytes;
+        const uint32_t nunits = (rb + BPP - 1) / BPP;
+        const int nchunks = static_cast<int>((nunits + C - 1) / C);
+        const uint32_t y = bd.band * 64 + lane;
+        const bool row_ok = y < ps.rows;
+        const uint8_t *frow = ps.filtered + static_cast<size_t>(y) * (rb + 1);
+        const int ft = row_ok ? frow[0] : 0;
+        const LaneFilter lf{ft == 1, ft == 2, ft == 3, ft == 4};
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(frow + 1) & 3);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(frow + 1 - mis);
 
-        // ---- the row above: chunk k of row y-1 was produced by lane-1 one step ago
-        uint32_t up[CW];
+        const bool has_prev = bd.band > 0;
+        const bool has_next = bd.band + 1 < ps.nbands;
+        const uint64_t *prev_bnd =
+            boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) * band_granules;
+        uint64_t *my_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band) * band_granules;
+
+        uint32_t left[BPP], ul[BPP];
 #pragma unroll
-        for (int i = 0; i < CW; i++) up[i] = __builtin_amdgcn_update_dpp(0, static_cast<int>(outp[i]), 0x138, 0xf, 0xf, false);
-        if (has_prev && step < nchunks) { // lane 0 needs chunk `step` of the previous band's last row
-            if ((step % kRegionChunks) == 0) {
-                const uint32_t need = static_cast<uint32_t>(min(step + kRegionChunks, nchunks));
+        for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
+        uint32_t outp[CW];
+#pragma unroll
+        for (int i = 0; i < CW; i++) outp[i] = 0;
+        uint32_t carry = 0;
+        uint64_t win = 0, win_next = 0;
+        int maxidx = 0;
+
+        auto load_window = [&](int w0) -> uint64_t {
+            const int k = w0 + lane / CW;
+            return (lane < WG && k < nchunks) ? ld_sc1_64(prev_bnd + static_cast<size_t>(w0) * CW + lane) : 0ull;
+        };
+        if (has_prev) win = load_window(0);
+
+        const uint32_t band_rows = min(64u, ps.rows - bd.band * 64);
+        const int nsteps = nchunks + static_cast<int>(band_rows) - 1;
+        for (int step = 0; step < nsteps; ++step) {
+            const int k = step - lane;
+            const bool act = row_ok && k >= 0 && k < nchunks;
+
+            // ---- the row above: chunk k of row y-1 was produced by lane-1 one step ago
+            uint32_t up[CW];
+#pragma unroll
+            for (int i = 0; i < CW; i++)
+                up[i] = __builtin_amdgcn_update_dpp(0, static_cast<int>(outp[i]), 0x138, 0xf, 0xf, false);
+            if (has_prev && step < nchunks) { // lane 0: chunk `step` of the previous band's last row
+                const int wi = step % WIN;
+                if (wi == 0 && step > 0) win = win_next;
+                if (wi == WIN / 2 && step + WIN / 2 < nchunks) win_next = load_window(step + WIN / 2);
+                const int base = wi * CW;
                 uint32_t spins = 0;
-                while (seen < need) {
-                    seen = __builtin_amdgcn_readfirstlane(ld_sc1(prev_prog));
-                    if (seen >= need) break;
+                for (;;) {
+                    bool ready = true;
+#pragma unroll
+                    for (int i = 0; i < CW; i++) {
+                        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(win >> 32), base + i);
+                        ready &= hi == epoch;
+                    }
+                    if (ready) break;
                     if (++spins > kSpinLimit) {
                         timed_out = true;
-                        seen = need;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
+                    if (lane >= base && lane < base + CW)
+                        win = ld_sc1_64(prev_bnd + static_cast<size_t>(step - wi) * CW + lane);
                 }
-                const uint32_t *rp = prev_bnd + (step / kRegionChunks) * (kRegionBytes / 4);
-                region = lane < kRegionChunks * CW ? ld_sc1(rp + lane) : 0u;
-            }
-            const int base = (step % kRegionChunks) * CW;
 #pragma unroll
-            for (int i = 0; i < CW; i++) {
-                const uint32_t v = __builtin_amdgcn_readlane(static_cast<int>(region), base + i);
-                if (lane == 0) up[i] = v;
-            }
-        } else if (lane == 0) {
+                for (int i = 0; i < CW; i++) {
+                    const uint32_t v = __builtin_amdgcn_readlane(static_cast<int>(win), base + i);
+                    if (lane == 0) up[i] = v;
+                }
+            } else if (lane == 0) {
 #pragma unroll
-            for (int i = 0; i < CW; i++) up[i] = 0; // first row of a pass: zero previous row (:790-793)
-        }
-
-        if (act) {
-            // ---- filtered bytes of chunk k (dword window + funnel shift)
-            if (k == 0) carry = src[0];
-            uint32_t in[CW + 1];
-            in[0] = carry;
-#pragma unroll
-            for (int i = 1; i <= CW; i++) in[i] = src[k * CW + i];
-            carry = in[CW];
-            uint32_t f[CW];
-#pragma unroll
-            for (int i = 0; i < CW; i++) f[i] = __builtin_amdgcn_alignbyte(in[i + 1], in[i], mis);
-            if (k == 0) {
-#pragma unroll
-                for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
+                for (int i = 0; i < CW; i++) up[i] = 0; // first row of a pass: zero previous row (:790-793)
             }
 
-            // ---- reconstruct C units, left to right
-            uint32_t ob[CW];
+            if (act) {
+                // ---- filtered bytes of chunk k (dword window + funnel shift)
+                if (k == 0) carry = src[0];
+                uint32_t in[CW + 1];
+                in[0] = carry;
 #pragma unroll
-            for (int i = 0; i < CW; i++) ob[i] = 0;
+                for (int i = 1; i <= CW; i++) in[i] = src[k * CW + i];
+                carry = in[CW];
+                uint32_t f[CW];
 #pragma unroll
-            for (int u = 0; u < C; u++) {
+                for (int i = 0; i < CW; i++) f[i] = __builtin_amdgcn_alignbyte(in[i + 1], in[i], mis);
+                if (k == 0) {
+#pragma unroll
+                    for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
+                }
+                // ---- reconstruct C units, left to right
+                uint32_t ob[CW];
+#pragma unroll
+                for (int i = 0; i < CW; i++) ob[i] = 0;
+                uint32_t prev_out[BPP], prev_up[BPP];
 #pragma unroll
                 for (int i = 0; i < BPP; i++) {
-                    const int idx = u * BPP + i;
-                    const int a = static_cast<int>(u == 0 ? left[i] : byte_of(ob, idx - BPP));
-                    const int b = static_cast<int>(byte_of(up, idx));
-                    const int c = static_cast<int>(u == 0 ? ul[i] : byte_of(up, idx - BPP));
-                    const uint32_t v = (byte_of(f, idx) + predict(ft, a, b, c)) & 0xff;
-                    ob[idx >> 2] |= v << ((idx & 3) * 8);
+                    prev_out[i] = left[i];
+                    prev_up[i] = ul[i];
+                }
+#pragma unroll
+                for (int u = 0; u < C; u++) {
+#pragma unroll
+                    for (int i = 0; i < BPP; i++) {
+                        const int idx = u * BPP + i;
+                        const uint32_t b = byte_of(up, idx);
+                        const uint32_t v = recon_byte(lf, byte_of(f, idx), prev_out[i], b, prev_up[i]);
+                        ob[idx >> 2] |= v << ((idx & 3) * 8);
+                        prev_out[i] = v;
+                        prev_up[i] = b;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < BPP; i++) {
+                    left[i] = prev_out[i];
+                    ul[i] = prev_up[i];
+                }
+#pragma unroll
+                for (int i = 0; i < CW; i++) outp[i] = ob[i];
+
+                store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
+
+                if (has_next && lane == 63) { // publish: the data is the flag
+                    uint64_t *d = my_bnd + static_cast<size_t>(k) * CW;
+#pragma unroll
+                    for (int i = 0; i < CW; i++) st_sc1_64(d + i, static_cast<uint64_t>(epoch) << 32 | ob[i]);
                 }
             }
-#pragma unroll
-            for (int i = 0; i < BPP; i++) {
-                left[i] = byte_of(ob, (C - 1) * BPP + i);
-                ul[i] = byte_of(up, (C - 1) * BPP + i);
-            }
-#pragma unroll
-            for (int i = 0; i < CW; i++) outp[i] = ob[i];
-
-            store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
-
-            if (has_next && lane == 63) {
-                uint32_t *d = my_bnd + (k / kRegionChunks) * (kRegionBytes / 4) + (k % kRegionChunks) * CW;
-#pragma unroll
-                for (int i = 0; i < CW; i++) st_sc1(d + i, ob[i]);
-            }
         }
-        // ---- publish a completed region of the band's last row (lane 63's chunk step-63)
-        if (has_next) {
-            const int k63 = step - 63;
-            if (k63 >= 0 && k63 < nchunks && ((k63 % kRegionChunks) == kRegionChunks - 1 || k63 == nchunks - 1)) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 63) st_sc1(my_prog, static_cast<uint32_t>(k63 + 1));
-            }
+        if constexpr (DEPTH >= ZPX_PNG_P1 && DEPTH <= ZPX_PNG_P8) {
+            for (int off = 32; off > 0; off >>= 1) maxidx = max(maxidx, __shfl_xor(maxidx, off));
+            if (lane == 0 && ps.max_index) atomicMax(ps.max_index, maxidx);
         }
-    }
-    if constexpr (DEPTH >= ZPX_PNG_P1 && DEPTH <= ZPX_PNG_P8) {
-        for (int off = 32; off > 0; off >>= 1) maxidx = max(maxidx, __shfl_xor(maxidx, off));
-        if (lane == 0 && ps.max_index) atomicMax(ps.max_index, maxidx);
     }
     if (timed_out && lane == 0) atomicOr(status, 1u);
 }
 
-template <int DEPTH>
-void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ticket,
-              uint32_t *progress, uint8_t *boundary, uint32_t band_bytes, uint32_t *status, hipStream_t s)
+// Per-launch control block: epoch++ (fresh granule tags, so the boundary
+// buffer never needs clearing), ticket = 0, status = 0.
+__global__ void png_ctl_kernel(uint32_t *ctl)
 {
-    hipLaunchKernelGGL((png_unfilter_kernel<DEPTH>), dim3(nsched), dim3(64), 0, s, passes, sched, nsched, ticket,
-                       progress, boundary, band_bytes, status);
+    ctl[0] += 1;
+    ctl[1] = 0;
+    ctl[2] = 0;
+}
+
+int png_waves_per_cu()
+{
+    static int n = 0;
+    if (n == 0) {
+        const char *e = getenv("ZPX_PNG_WAVES_PER_CU");
+        n = e ? atoi(e) : 8;
+        if (n < 1) n = 1;
+        if (n > 32) n = 32;
+    }
+    return n;
+}
+
+int cus()
+{
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, c = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        n = c;
+    }
+    return n;
+}
+
+template <int DEPTH>
+void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl, uint64_t *boundary,
+              uint32_t band_granules, hipStream_t s)
+{
+    const uint32_t want = static_cast<uint32_t>(cus() * png_waves_per_cu());
+    const uint32_t grid = nsched < want ? nsched : want;
+    hipLaunchKernelGGL(png_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
+    hipLaunchKernelGGL((png_unfilter_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
+                       band_granules);
 }
 
 } // namespace
@@ -445,12 +501,19 @@ int png_chunk_bytes(int depth)
     }
 }
 
+int png_band_granules(int depth, uint32_t max_row_bytes)
+{
+    const uint32_t cb = static_cast<uint32_t>(png_chunk_bytes(depth));
+    const uint32_t nchunks = (max_row_bytes + cb - 1) / cb;
+    const uint32_t gran = nchunks * (cb / 4) + 64; // + slack for the window's over-read
+    return static_cast<int>((gran + 31) & ~31u);
+}
+
 int launch_png_unfilter(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                        uint32_t *ticket, uint32_t *progress, uint8_t *boundary, uint32_t band_bytes,
-                        uint32_t *status, hipStream_t s)
+                        uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s)
 {
     switch (depth) {
-#define ZPX_CASE(D) case D: launch_t<D>(passes, sched, nsched, ticket, progress, boundary, band_bytes, status, s); break;
+#define ZPX_CASE(D) case D: launch_t<D>(passes, sched, nsched, ctl, boundary, band_granules, s); break;
         ZPX_CASE(ZPX_PNG_G1) ZPX_CASE(ZPX_PNG_G2) ZPX_CASE(ZPX_PNG_G4) ZPX_CASE(ZPX_PNG_G8)
         ZPX_CASE(ZPX_PNG_GA8) ZPX_CASE(ZPX_PNG_TC8) ZPX_CASE(ZPX_PNG_P1) ZPX_CASE(ZPX_PNG_P2)
         ZPX_CASE(ZPX_PNG_P4) ZPX_CASE(ZPX_PNG_P8) ZPX_CASE(ZPX_PNG_TCA8) ZPX_CASE(ZPX_PNG_G16)

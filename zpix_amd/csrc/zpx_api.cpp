@@ -343,34 +343,37 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
                            const std::vector<uint32_t> &pass_rowbytes)
 {
     std::vector<DevPngPass> passes = passes_in;
-    const uint32_t cb = static_cast<uint32_t>(png_chunk_bytes(g.depth));
-    uint32_t base = 0, max_bands = 0, band_bytes = 256;
+    uint32_t base = 0, max_bands = 0, max_rb = 0;
     for (size_t i = 0; i < passes.size(); i++) {
         DevPngPass &p = passes[i];
         p.nbands = (p.rows + 63) / 64;
         p.band_base = base;
         base += p.nbands;
         max_bands = std::max(max_bands, p.nbands);
-        const uint32_t nchunks = (pass_rowbytes[i] + cb - 1) / cb;
-        band_bytes = std::max(band_bytes, ((nchunks + 15) / 16) * 256u);
+        max_rb = std::max(max_rb, pass_rowbytes[i]);
     }
+    // band-major order: band b of every pass before band b+1 of any pass
     std::vector<DevPngBand> sched;
     for (uint32_t b = 0; b < max_bands; b++)
         for (size_t i = 0; i < passes.size(); i++)
             if (b < passes[i].nbands) sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
     g.nsched = static_cast<uint32_t>(sched.size());
     g.nbands = base;
-    g.band_bytes = band_bytes;
+    g.band_bytes = static_cast<uint32_t>(png_band_granules(g.depth, max_rb)); // granules per band
     HIPCHK(ctx, g.passes.alloc(passes.size() * sizeof(DevPngPass)));
     HIPCHK(ctx, hipMemcpy(g.passes.ptr, passes.data(), passes.size() * sizeof(DevPngPass), hipMemcpyHostToDevice));
     HIPCHK(ctx, g.sched.alloc(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand)));
     if (!sched.empty())
         HIPCHK(ctx, hipMemcpy(g.sched.ptr, sched.data(), sched.size() * sizeof(DevPngBand), hipMemcpyHostToDevice));
-    // scratch: [ticket, status, 2 pad][progress x nbands], zeroed before every launch
-    g.scratch_zero_bytes = ((4 + size_t(base)) * sizeof(uint32_t) + 15) & ~size_t(15);
-    HIPCHK(ctx, g.scratch.alloc(g.scratch_zero_bytes));
-    HIPCHK(ctx, hipMemset(g.scratch.ptr, 0, g.scratch_zero_bytes));
-    HIPCHK(ctx, g.boundary.alloc(size_t(base) * band_bytes));
+    // control words {epoch, ticket, status, pad}; the boundary granules start
+    // with tag 0 and every launch uses a fresh epoch >= 1, so neither needs
+    // clearing per launch
+    g.scratch_zero_bytes = 16;
+    HIPCHK(ctx, g.scratch.alloc(16));
+    HIPCHK(ctx, hipMemset(g.scratch.ptr, 0, 16));
+    const size_t bbytes = std::max<size_t>(1, size_t(base)) * g.band_bytes * sizeof(uint64_t);
+    HIPCHK(ctx, g.boundary.alloc(bbytes));
+    HIPCHK(ctx, hipMemset(g.boundary.ptr, 0, bbytes));
     return 0;
 }
 
@@ -486,10 +489,8 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
     for (auto &g : plan->png) {
-        HIPCHK(ctx, hipMemsetAsync(g->scratch.ptr, 0, g->scratch_zero_bytes, st));
-        uint32_t *sc = g->scratch.as<uint32_t>();
         const int rc = launch_png_unfilter(g->depth, g->passes.as<DevPngPass>(), g->sched.as<DevPngBand>(), g->nsched,
-                                           sc + 0, sc + 4, g->boundary.as<uint8_t>(), g->band_bytes, sc + 1, st);
+                                           g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes, st);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
     }
     return ZPX_OK;
@@ -500,7 +501,7 @@ static int png_plan_status(zpx_plan *plan)
 {
     for (auto &g : plan->png) {
         uint32_t st = 0;
-        HIPCHK(plan->ctx, hipMemcpy(&st, g->scratch.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost));
+        HIPCHK(plan->ctx, hipMemcpy(&st, g->scratch.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost));
         if (st) {
             plan->ctx->last_error = "png wavefront hand-off timed out";
             return ZPX_E_HIP;
