@@ -310,25 +310,43 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
         my = r / strips_x;
         mx0 = (r - my * strips_x) * T;
     };
+    // per-strip uniform view of the frame descriptor: the component grids are
+    // read into scalars once, so that row addresses are a per-lane select of
+    // uniform values (a lane-indexed fr.coeffs[comp] compiles to a vector load
+    // plus a full vmcnt(0) wait in front of every prefetch)
+    struct StripSrc {
+        const CoefT *g[3];
+        int gwy, gwc, myy;
+    };
+    auto src_of = [&](const DevJpegFrame &fr) {
+        StripSrc s;
+        s.g[0] = static_cast<const CoefT *>(fr.coeffs[0]);
+        s.g[1] = static_cast<const CoefT *>(fr.coeffs[1]);
+        s.g[2] = static_cast<const CoefT *>(fr.coeffs[2]);
+        s.gwy = fr.mxx * H0;
+        s.gwc = fr.mxx * HC;
+        s.myy = fr.myy;
+        return s;
+    };
     // coefficient row address of row-task k of a strip (nullptr: nothing to load)
-    auto row_ptr = [&](const DevJpegFrame &fr, int my, int mx0, int k) -> const CoefT * {
+    auto row_ptr = [&](const StripSrc &ss, int my, int mx0, int k) -> const CoefT * {
         const int blk = k >> 3, r = k & 7;
-        int comp, bx, by, gw;
+        int bx, by, gw;
+        const CoefT *grid;
         if (blk < NY) {
-            comp = 0;
+            grid = ss.g[0];
             bx = mx0 * H0 + blk % YW;
             by = my * V0 + blk / YW;
-            gw = fr.mxx * H0;
+            gw = ss.gwy;
         } else {
             const int c = blk - NY;
             const int kk = NC > 0 ? c % NC : 0;
-            comp = c < NC ? 1 : 2;
+            grid = c < NC ? ss.g[1] : ss.g[2];
             bx = mx0 * HC + kk % CW;
             by = my * VC + kk / CW;
-            gw = fr.mxx * HC;
+            gw = ss.gwc;
         }
-        const CoefT *grid = static_cast<const CoefT *>(fr.coeffs[comp]);
-        if (grid == nullptr || bx >= gw || blk >= NB || my >= fr.myy) return nullptr; // ragged batch: skip
+        if (grid == nullptr || bx >= gw || blk >= NB || my >= ss.myy) return nullptr; // ragged batch: skip
         return grid + (static_cast<size_t>(by) * gw + bx) * 64 + r * 8;
     };
 
@@ -337,15 +355,17 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
     int f = 0, my = 0, mx0 = 0;
     if (st < total_strips) {
         strip_of(st, f, my, mx0);
+        const StripSrc ss0 = src_of(frames[f]);
 #pragma unroll
         for (int it = 0; it < ROW_IT; it++) {
-            const CoefT *p = row_ptr(frames[f], my, mx0, it * kThreads + tid);
+            const CoefT *p = row_ptr(ss0, my, mx0, it * kThreads + tid);
             if (p) load_row_raw<CoefT>(p, pre[it]);
         }
     }
     int qframe = -1;
     for (; st < total_strips; st += gridDim.x) {
         const DevJpegFrame &fr = frames[f];
+        const StripSrc ss = src_of(fr);
         if (f != qframe) { // quant tables of this frame (natural order)
             for (int i = tid; i < ncomp * 64; i += kThreads) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
             qframe = f;
@@ -359,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
             const int blk = k >> 3, r = k & 7;
             const int comp = blk < NY ? 0 : (blk < NY + NC ? 1 : 2);
             int32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (row_ptr(fr, my, mx0, k) != nullptr) {
+            if (row_ptr(ss, my, mx0, k) != nullptr) {
                 unpack_dequant<CoefT>(pre[it], qs[comp] + r * 8, s);
                 idct_row<NARROW>(s);
             }
@@ -376,9 +396,10 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
         int fn = f, myn = my, mxn = mx0;
         if (st_next < total_strips) {
             strip_of(st_next, fn, myn, mxn);
+            const StripSrc ssn = src_of(frames[fn]);
 #pragma unroll
             for (int it = 0; it < ROW_IT; it++) {
-                const CoefT *p = row_ptr(frames[fn], myn, mxn, it * kThreads + tid);
+                const CoefT *p = row_ptr(ssn, myn, mxn, it * kThreads + tid);
                 if (p) load_row_raw<CoefT>(p, pre[it]);
             }
         }
