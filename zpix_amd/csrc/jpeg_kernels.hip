@@ -350,6 +350,12 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
         return grid + (static_cast<size_t>(by) * gw + bx) * 64 + r * 8;
     };
 
+    // Rows without a block are loaded from a valid dummy address and zeroed in
+    // P1: every prefetch and every store is issued unconditionally, so the
+    // compiler's vmcnt before P1 counts only this strip's stores in flight
+    // (a branchy load/store phase makes it wait for vmcnt(0), i.e. for the
+    // previous strip's stores to complete).
+    const CoefT *const dummy = reinterpret_cast<const CoefT *>(frames);
     RowRegs<CoefT> pre[ROW_IT];
     int st = blockIdx.x;
     int f = 0, my = 0, mx0 = 0;
@@ -359,7 +365,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
 #pragma unroll
         for (int it = 0; it < ROW_IT; it++) {
             const CoefT *p = row_ptr(ss0, my, mx0, it * kThreads + tid);
-            if (p) load_row_raw<CoefT>(p, pre[it]);
+            load_row_raw<CoefT>(p ? p : dummy, pre[it]);
         }
     }
     int qframe = -1;
@@ -392,15 +398,16 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
             *reinterpret_cast<i32x4 *>(d + (sw ? 0 : 4)) = sw ? lo : hi;
         }
         // ---- prefetch the next strip's rows (consumed next iteration)
-        const int st_next = st + gridDim.x;
-        int fn = f, myn = my, mxn = mx0;
-        if (st_next < total_strips) {
+        // (past the end: the last strip again, loaded and never used)
+        const int st_next = min(st + static_cast<int>(gridDim.x), total_strips - 1);
+        int fn, myn, mxn;
+        {
             strip_of(st_next, fn, myn, mxn);
             const StripSrc ssn = src_of(frames[fn]);
 #pragma unroll
             for (int it = 0; it < ROW_IT; it++) {
                 const CoefT *p = row_ptr(ssn, myn, mxn, it * kThreads + tid);
-                if (p) load_row_raw<CoefT>(p, pre[it]);
+                load_row_raw<CoefT>(p ? p : dummy, pre[it]);
             }
         }
         __syncthreads();
@@ -489,25 +496,39 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
         }
         __syncthreads();
 
-        // ---- P3c: 16-byte stores of the tile
+        // ---- P3c: stores of the tile through a per-strip buffer descriptor.
+        // Lanes outside the image get an offset past num_records and the
+        // hardware drops their stores, so no store sits behind a branch.
+        // The host guarantees PXH * rgba_stride < 2^31.
         const int W = fr.width, H = fr.height;
         const int X0 = mx0 * H0 * 8, Y0 = my * V0 * 8;
-        const size_t ostride = fr.rgba_stride;
-        uint8_t *const out = fr.rgba;
-        const bool vec_ok = (ostride & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+        const uint32_t ostride = static_cast<uint32_t>(fr.rgba_stride);
+        uint8_t *const out = fr.rgba + static_cast<size_t>(Y0) * fr.rgba_stride;
+        const int rows_here = min(PXH, H - Y0);
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, rows_here * static_cast<int>(ostride), 0x00020000);
+        constexpr uint32_t kDrop = 0x80000000u;
+        // 16-byte stores when every chunk of a row is whole and aligned
+        const bool vec_ok = (ostride & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (W & 3) == 0;
+        if (vec_ok) {
 #pragma unroll
-        for (int it = 0; it < OUT_IT; it++) {
-            const int q = it * kThreads + tid;
-            if (q >= CHUNKS) break;
-            const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
-            const int Y = Y0 + row, X = X0 + cx;
-            if (Y >= H || X >= W) continue;
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
-            uint8_t *dst = out + static_cast<size_t>(Y) * ostride + static_cast<size_t>(X) * 4;
-            if (vec_ok && X + 4 <= W) {
-                *(ZPX_GLOBAL u32x4 *)dst = v;
-            } else {
-                for (int e = 0; e < 4 && X + e < W; e++) ((ZPX_GLOBAL uint32_t *)dst)[e] = v[e];
+            for (int it = 0; it < OUT_IT; it++) {
+                const int q = min(it * kThreads + tid, CHUNKS - 1); // duplicates store the same bytes
+                const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
+                const uint32_t off = X0 + cx < W ? row * ostride + (X0 + cx) * 4 : kDrop;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < OUT_IT; it++) {
+                const int q = min(it * kThreads + tid, CHUNKS - 1);
+                const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const uint32_t off = X0 + cx + e < W ? row * ostride + (X0 + cx + e) * 4 : kDrop;
+                    __builtin_amdgcn_raw_buffer_store_b32(v[e], rsrc, off, 0, 0);
+                }
             }
         }
         __syncthreads(); // tile / row buffer reused by the next strip

@@ -278,6 +278,10 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
             }
             const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
             if (!jpeg_rgba_supported(color, h0, v0, hc, vc)) return ZPX_E_UNSUPPORTED;
+            // the fused kernel addresses one strip (<= 32 rows) of output
+            // through a buffer descriptor with a 31-bit range
+            if (f.rgba_stride < size_t(f.width) * 4 || f.rgba_stride > (size_t(1) << 31) / 32)
+                return ZPX_E_INVALID_ARGUMENT;
             groups[{f.coeff_bits, f.narrow, color, h0, v0, hc, vc}].push_back(i);
         } else {
             groups[{f.coeff_bits, f.narrow, 0, 0, 0, 0, 0}].push_back(i);
