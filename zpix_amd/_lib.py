@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzpix_amd.so")
+# ZPX_LIB_PATH: an alternative build of the same library (kernel A/B experiments)
+LIB_PATH = os.environ.get("ZPX_LIB_PATH") or os.path.join(HERE, "libzpix_amd.so")
 
 # one HIP runtime per process: if torch is importable, let it load its
 # libamdhip64 first so device pointers from torch tensors and from this

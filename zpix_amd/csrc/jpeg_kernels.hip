@@ -19,6 +19,12 @@ namespace zpx {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef ZPX_RGBA_STORE_AUX
+#define ZPX_RGBA_STORE_AUX 2 // cache policy bits of the fused kernel's output stores (2 = nt)
+#endif
+#ifndef ZPX_COEF_NT
+#define ZPX_COEF_NT 1 // 1: non-temporal coefficient loads (read once)
+#endif
 constexpr int kBlkStride = 72; // dwords per 8x8 block in LDS (64 + 8 pad: conflict-free column reads)
 
 // idct.zig:50-65
@@ -233,7 +239,31 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 #define ZPX_GLOBAL __attribute__((address_space(1)))
 
-constexpr int strip_mcus(int blocks_per_mcu) { return blocks_per_mcu >= 96 ? 1 : 96 / blocks_per_mcu; }
+#ifndef ZPX_JPEG_GROUP
+#define ZPX_JPEG_GROUP 256 // threads that cooperate on one strip: 256 (workgroup) or 64 (one wave)
+#endif
+constexpr int kGroup = ZPX_JPEG_GROUP;
+static_assert(kGroup == 64 || kGroup == kThreads, "a strip group is one wave or the workgroup");
+// about 96 blocks per 256 threads (3 coefficient rows per lane)
+constexpr int kStripBlocks = 96 * kGroup / kThreads;
+constexpr int strip_mcus(int blocks_per_mcu)
+{
+    return blocks_per_mcu >= kStripBlocks ? 1 : kStripBlocks / blocks_per_mcu;
+}
+
+// Barrier among the threads of one strip group.  A one-wave group needs no
+// s_barrier: LDS operations of a wave complete in order, so a compiler fence
+// plus lgkmcnt(0) orders the lanes' LDS writes before the reads.
+template <int G>
+__device__ __forceinline__ void group_sync()
+{
+    if constexpr (G == kThreads) {
+        __syncthreads();
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
 
 template <typename CoefT>
 struct RowRegs { // one coefficient row, raw (not yet dequantized)
@@ -245,8 +275,13 @@ template <typename CoefT>
 __device__ __forceinline__ void load_row_raw(const CoefT *p, RowRegs<CoefT> &r)
 {
     const ZPX_GLOBAL u32x4 *g = (const ZPX_GLOBAL u32x4 *)p;
+#if ZPX_COEF_NT
+    r.a = __builtin_nontemporal_load(g);
+    if constexpr (sizeof(CoefT) == 4) r.b = __builtin_nontemporal_load(g + 1);
+#else
     r.a = g[0];
     if constexpr (sizeof(CoefT) == 4) r.b = g[1];
+#endif
 }
 
 template <typename CoefT>
@@ -280,6 +315,8 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
     constexpr int kYB = H0 * V0;                      // luma blocks per MCU
     constexpr int kCB = kGray ? 0 : HC * VC;          // blocks per chroma component per MCU
+    constexpr int G = kGroup;                         // threads that share a strip
+    constexpr int NG = kThreads / G;                  // strip groups per workgroup
     constexpr int T = strip_mcus(kYB + 2 * kCB);      // MCUs per strip
     constexpr int NY = T * kYB, NC = T * kCB, NB = NY + 2 * NC;
     constexpr int YW = T * H0;                        // luma blocks across the strip
@@ -289,18 +326,21 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
     constexpr int RX = kGray ? 1 : H0 / HC, RY = kGray ? 1 : V0 / VC; // upsample ratios
     constexpr int PXW = YW * 8;                       // strip width in pixels
     constexpr int PXH = V0 * 8;                       // strip height in pixels
-    constexpr int ROW_IT = (NB * 8 + kThreads - 1) / kThreads;
-    constexpr int YCOL_IT = (NY * 8 + kThreads - 1) / kThreads;
-    constexpr int CCOL_IT = (2 * NC * 8 + kThreads - 1) / kThreads;
+    constexpr int ROW_IT = (NB * 8 + G - 1) / G;
+    constexpr int YCOL_IT = (NY * 8 + G - 1) / G;
+    constexpr int CCOL_IT = (2 * NC * 8 + G - 1) / G;
     constexpr int CHUNKS = PXH * PXW / 4;             // 16-byte output chunks per strip
-    constexpr int OUT_IT = (CHUNKS + kThreads - 1) / kThreads;
+    constexpr int OUT_IT = (CHUNKS + G - 1) / G;
     static_assert(PXH * PXW <= NB * kBlkStride, "RGBA tile must fit in the row buffer");
 
-    __shared__ int32_t qs[3][64];
-    __shared__ __attribute__((aligned(16))) int32_t buf[NB * kBlkStride]; // row pass, then RGBA tile
-    __shared__ int32_t ctile[kGray ? 1 : 2][CROWS * CPX];
+    __shared__ int32_t qs_all[NG][3][64];
+    __shared__ __attribute__((aligned(16))) int32_t buf_all[NG][NB * kBlkStride]; // row pass, then RGBA tile
+    __shared__ int32_t ctile_all[NG][kGray ? 1 : 2][CROWS * CPX];
 
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x % G, group = threadIdx.x / G;
+    auto (&qs) = qs_all[group];
+    int32_t *const buf = buf_all[group];
+    auto (&ctile) = ctile_all[group];
     constexpr int ncomp = kGray ? 1 : 3;
 
     // strip -> (frame, MCU row, first MCU column)
@@ -357,30 +397,31 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
     // previous strip's stores to complete).
     const CoefT *const dummy = reinterpret_cast<const CoefT *>(frames);
     RowRegs<CoefT> pre[ROW_IT];
-    int st = blockIdx.x;
+    const int gstride = static_cast<int>(gridDim.x) * NG;
+    int st = blockIdx.x * NG + group;
     int f = 0, my = 0, mx0 = 0;
     if (st < total_strips) {
         strip_of(st, f, my, mx0);
         const StripSrc ss0 = src_of(frames[f]);
 #pragma unroll
         for (int it = 0; it < ROW_IT; it++) {
-            const CoefT *p = row_ptr(ss0, my, mx0, it * kThreads + tid);
+            const CoefT *p = row_ptr(ss0, my, mx0, it * G + tid);
             load_row_raw<CoefT>(p ? p : dummy, pre[it]);
         }
     }
     int qframe = -1;
-    for (; st < total_strips; st += gridDim.x) {
+    for (; st < total_strips; st += gstride) {
         const DevJpegFrame &fr = frames[f];
         const StripSrc ss = src_of(fr);
         if (f != qframe) { // quant tables of this frame (natural order)
-            for (int i = tid; i < ncomp * 64; i += kThreads) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
+            for (int i = tid; i < ncomp * 64; i += G) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
             qframe = f;
-            __syncthreads();
+            group_sync<G>();
         }
         // ---- P1: dequant + row IDCT of the prefetched rows
 #pragma unroll
         for (int it = 0; it < ROW_IT; it++) {
-            const int k = it * kThreads + tid;
+            const int k = it * G + tid;
             if (k >= NB * 8) break;
             const int blk = k >> 3, r = k & 7;
             const int comp = blk < NY ? 0 : (blk < NY + NC ? 1 : 2);
@@ -399,25 +440,26 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
         }
         // ---- prefetch the next strip's rows (consumed next iteration)
         // (past the end: the last strip again, loaded and never used)
-        const int st_next = min(st + static_cast<int>(gridDim.x), total_strips - 1);
+        const int st_next = min(st + gstride, total_strips - 1);
         int fn, myn, mxn;
         {
             strip_of(st_next, fn, myn, mxn);
             const StripSrc ssn = src_of(frames[fn]);
 #pragma unroll
             for (int it = 0; it < ROW_IT; it++) {
-                const CoefT *p = row_ptr(ssn, myn, mxn, it * kThreads + tid);
+                const CoefT *p = row_ptr(ssn, myn, mxn, it * G + tid);
                 load_row_raw<CoefT>(p ? p : dummy, pre[it]);
             }
         }
-        __syncthreads();
+        group_sync<G>();
 
+#ifndef ZPX_JPEG_COPY_ONLY
         // ---- P2: chroma columns -> LDS tile
         if constexpr (!kGray) {
             const bool cb_present = fr.coeffs[1] != nullptr, cr_present = fr.coeffs[2] != nullptr;
 #pragma unroll
             for (int it = 0; it < CCOL_IT; it++) {
-                const int task = it * kThreads + tid;
+                const int task = it * G + tid;
                 if (task >= 2 * NC * 8) break;
                 const int k = task >> 3, c = task & 7;
                 const int comp = k < NC ? 1 : 2;
@@ -432,14 +474,14 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
 #pragma unroll
                 for (int i = 0; i < 8; i++) t[i * CPX] = present ? s[i] : 0;
             }
-            __syncthreads();
+            group_sync<G>();
         }
 
         // ---- P3a: luma columns
         int32_t yv[YCOL_IT][8];
 #pragma unroll
         for (int it = 0; it < YCOL_IT; it++) {
-            const int task = it * kThreads + tid;
+            const int task = it * G + tid;
             if (task < NY * 8) {
                 const int blk = task >> 3, c = task & 7;
 #pragma unroll
@@ -447,13 +489,13 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
                 idct_col_clamp<NARROW>(yv[it]);
             }
         }
-        __syncthreads(); // row buffer is free: reuse it as the RGBA tile
+        group_sync<G>(); // row buffer is free: reuse it as the RGBA tile
 
         // ---- P3b: colour -> RGBA tile [PXH][PXW]
         uint32_t *otile = reinterpret_cast<uint32_t *>(buf);
 #pragma unroll
         for (int it = 0; it < YCOL_IT; it++) {
-            const int task = it * kThreads + tid;
+            const int task = it * G + tid;
             if (task >= NY * 8) break;
             const int blk = task >> 3, c = task & 7;
             const int yrow = blk / YW, ycol = blk % YW;
@@ -494,7 +536,12 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
                 }
             }
         }
-        __syncthreads();
+        group_sync<G>();
+#else
+        // timing-only build: the row buffer (raw dequantized rows) is stored as
+        // the tile, so the launch moves the same bytes with no IDCT/colour work
+        uint32_t *otile = reinterpret_cast<uint32_t *>(buf);
+#endif
 
         // ---- P3c: stores of the tile through a per-strip buffer descriptor.
         // Lanes outside the image get an offset past num_records and the
@@ -512,26 +559,26 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
         if (vec_ok) {
 #pragma unroll
             for (int it = 0; it < OUT_IT; it++) {
-                const int q = min(it * kThreads + tid, CHUNKS - 1); // duplicates store the same bytes
+                const int q = min(it * G + tid, CHUNKS - 1); // duplicates store the same bytes
                 const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
                 const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
                 const uint32_t off = X0 + cx < W ? row * ostride + (X0 + cx) * 4 : kDrop;
-                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, ZPX_RGBA_STORE_AUX);
             }
         } else {
 #pragma unroll
             for (int it = 0; it < OUT_IT; it++) {
-                const int q = min(it * kThreads + tid, CHUNKS - 1);
+                const int q = min(it * G + tid, CHUNKS - 1);
                 const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
                 const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     const uint32_t off = X0 + cx + e < W ? row * ostride + (X0 + cx + e) * 4 : kDrop;
-                    __builtin_amdgcn_raw_buffer_store_b32(v[e], rsrc, off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(v[e], rsrc, off, 0, ZPX_RGBA_STORE_AUX);
                 }
             }
         }
-        __syncthreads(); // tile / row buffer reused by the next strip
+        group_sync<G>(); // tile / row buffer reused by the next strip
         f = fn;
         my = myn;
         mx0 = mxn;
@@ -575,10 +622,12 @@ void launch_rgba_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int 
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
     constexpr int T = strip_mcus(H0 * V0 + 2 * (kGray ? 0 : HC * VC));
+    constexpr int NG = kThreads / kGroup;
     const int strips_x = (max_mxx + T - 1) / T;
     const int per_frame = strips_x * max_myy;
     const int total = per_frame * n_frames;
-    const int grid = total < persistent_workgroups() ? total : persistent_workgroups();
+    const int groups_needed = (total + NG - 1) / NG;
+    const int grid = groups_needed < persistent_workgroups() ? groups_needed : persistent_workgroups();
     hipLaunchKernelGGL((jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>), dim3(grid), dim3(kThreads), 0,
                        stream, d_frames, strips_x, per_frame, total);
 }
