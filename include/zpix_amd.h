@@ -221,6 +221,17 @@ int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_i
 /* jpeg.probeBuffer, src/jpeg/root.zig:17-21 */
 int zpx_jpeg_probe_buffer(const uint8_t *buf, size_t len);
 
+/* color.Model, src/color/color.zig:161-165 */
+enum zpx_model { ZPX_MODEL_RGB = 0, ZPX_MODEL_YCBCR = 1, ZPX_MODEL_RGBA = 2, ZPX_MODEL_GRAY = 3 };
+/* jpeg.decodeConfig, src/jpeg/decoder.zig:178-218 (image.Config: width,
+ * height, color_model; 4-component frames report YCbCr as the reference does).
+ * Host-only header parse: no context needed. */
+int zpx_jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height,
+                           int32_t *color_model);
+/* Width/height of a PNG from its IHDR (signature + IHDR checks of
+ * png/decoder.zig:224-402); host-only.  Used to size batch destinations. */
+int zpx_png_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height);
+
 /* jpeg.decode followed by Image.rgbaPixels, fused on the device (one kernel:
  * dequant + IDCT + level shift + upsample + YCbCr->RGB). */
 int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
@@ -347,6 +358,65 @@ int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out);
 int zpx_png_stream_frame(const zpx_png_stream *s, zpx_png_frame *frame, size_t *filtered_len);
 const uint8_t *zpx_png_stream_data(const zpx_png_stream *s);
 void zpx_png_stream_free(zpx_png_stream *s);
+
+/* ---------------------------------------------------------------------- */
+/* batch / streaming decode                    */
+/* ---------------------------------------------------------------------- */
+/* Many encoded JPEG/PNG buffers -> RGBA8 in the layout of Image.rgbaPixels
+ * (image.zig:103-130), i.e. what `zpix.fromBuffer` + `img.rgbaPixels` give per
+ * image, without any per-image host sync:
+ *   - a pool of host threads runs the serial entropy stages (Huffman /
+ *     inflate, decoder.zig:1148-1455, png/decoder.zig:404-545) into pinned
+ *     buffers;
+ *   - the calling thread streams each result to the device with
+ *     hipMemcpyAsync on a copy stream, the context's compute stream waits on
+ *     that copy's event and runs the kernels, and (dst_on_host) a third
+ *     stream copies the RGBA back;
+ *   - at most `depth` images are staged at once; a slot is recycled when its
+ *     last event completes.
+ * Items complete independently: a malformed image sets its own `status`
+ * (the reference's error for it) and the rest of the batch proceeds. */
+typedef struct zpx_batch_item {
+    const uint8_t *buf;      /* encoded bytes (caller-owned, valid until the batch completes) */
+    size_t len;
+    uint8_t *dst;            /* RGBA8 output: DEVICE pointer, or HOST pointer when dst_on_host */
+    size_t dst_stride;       /* bytes between output rows; 0 = 4 * width */
+    size_t dst_capacity;     /* bytes available at dst (checked: ZPX_E_INVALID_ARGUMENT if short) */
+    int32_t status;          /* out: ZPX_OK or the image's error code */
+    uint32_t width, height;  /* out */
+    int32_t format;          /* out: 1 JPEG, 2 PNG, 0 unknown */
+} zpx_batch_item;
+
+typedef struct zpx_batch_opts {
+    int32_t host_threads;    /* entropy/inflate workers; 0 = min(16, hardware threads) */
+    int32_t depth;           /* images staged on the device at once; 0 = 2 * host_threads */
+    int32_t dst_on_host;     /* 1: dst are host pointers (results copied back over PCIe) */
+} zpx_batch_opts;
+
+typedef struct zpx_batch_stats {
+    double wall_s;           /* batch wall time */
+    double host_s;           /* summed host entropy/inflate time over all workers */
+    double h2d_bytes, d2h_bytes;
+    double pixels;           /* decoded pixels of the successful items */
+    int32_t host_threads, depth;
+    int32_t failed;          /* items with status != ZPX_OK */
+    int32_t pad;
+} zpx_batch_stats;
+
+/* Decodes the whole batch and returns when every item is complete.
+ * Returns ZPX_OK when the batch ran (see each item's status), ZPX_E_HIP on a
+ * device failure, ZPX_E_INVALID_ARGUMENT on bad arguments. */
+int zpx_batch_decode_rgba(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                          zpx_batch_stats *stats /* may be NULL */);
+
+/* Asynchronous form: starts the same pipeline on a background thread and
+ * returns at once; zpx_batch_wait joins it (and frees the handle). The items
+ * array and buffers must stay valid until then; the context must not be used
+ * by other calls meanwhile. */
+typedef struct zpx_batch zpx_batch;
+int zpx_batch_start(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                    zpx_batch **out);
+int zpx_batch_wait(zpx_batch *b, zpx_batch_stats *stats /* may be NULL */);
 
 #ifdef __cplusplus
 }

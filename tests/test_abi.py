@@ -205,3 +205,38 @@ def test_host_png_errors_match_oracle():
         want = _png_err_oracle(d)
         got = _png_err_product(d)
         assert got == want, (got, want)
+
+
+# ---------------------------------------------------------------- decodeConfig
+def test_jpeg_decode_config_matches_decode():
+    """jpeg.decodeConfig (decoder.zig:178-218): dims of every fixture equal the
+    full decode's; 1 component -> Gray, 3 or 4 -> YCbCr (the reference's TODO)."""
+    for p in sorted(glob.glob(golden("testdata", "*.jp*g"))):
+        data = open(p, "rb").read()
+        try:
+            img = O.jpeg_decode(data)
+        except O.OracleError:
+            continue
+        w, h, model = J.decode_config_model(data)
+        assert (w, h) == (img.width, img.height), p
+        assert model == ("Gray" if img.kind == "Gray" else "YCbCr"), p
+
+
+def test_jpeg_decode_config_errors():
+    with pytest.raises(zpix_amd.ZpixError) as e:
+        J.decode_config(b"\x00\x01garbage")
+    assert e.value.name == "InvalidSOIMarker"
+    data = read("testdata", "video-001.q50.420.jpeg")
+    with pytest.raises(zpix_amd.ZpixError) as e:
+        J.decode_config(data[:20])
+    assert e.value.name == "UnexpectedEof"
+
+
+def test_png_decode_config():
+    for p in sorted(glob.glob(golden("pngsuite", "*.png")))[:12]:
+        data = open(p, "rb").read()
+        img = O.png_decode(data)
+        assert P.decode_config(data) == (img.width, img.height)
+    with pytest.raises(zpix_amd.ZpixError) as e:
+        P.decode_config(b"\x89PNX\r\n\x1a\n" + b"\x00" * 30)
+    assert e.value.name == "InvalidPngHeader"

@@ -1,0 +1,145 @@
+"""GPU parity of the batch / streaming pipeline (zpx_batch_decode_rgba).
+
+Every item must equal zpix.fromBuffer + Image.rgbaPixels of the same bytes
+through the CPU oracle, bit-exact, whatever the mix of formats, the number of
+host threads and staging slots, the destination (device or host memory) and
+its row stride; a malformed item carries the reference's error name for it
+and the rest of the batch is unaffected.
+"""
+import ctypes as C
+import glob
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from conftest import golden, read
+from tools import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import zpix_amd  # noqa: E402
+from zpix_amd import _lib, batch  # noqa: E402
+
+FIXTURES = sorted(glob.glob(golden("testdata", "*.jpeg")) + glob.glob(golden("testdata", "*.jpg")) +
+                  glob.glob(golden("testdata", "*.png")) + glob.glob(golden("pngsuite", "*.png")))
+
+
+def oracle_rgba(data):
+    """fromBuffer + rgbaPixels through the oracle (src/root.zig:34-40 probes PNG, then JPEG)."""
+    if data[:8] != b"\x89PNG\r\n\x1a\n" and data[:2] != b"\xff\xd8":
+        return None, "UnknownImageFormat"
+    try:
+        img = O.decode(data)
+    except O.OracleError as e:
+        return None, e.name
+    return img.rgba_pixels().reshape(img.height, img.width, 4), "Ok"
+
+
+def mixed_buffers():
+    bufs = [open(p, "rb").read() for p in FIXTURES]
+    bufs += [S.jpeg_420(7, 333, 211), S.png_tc8_mixed(8, 301, 97), S.jpeg_progressive_444(9, 130, 77),
+             S.png_rgba16_adam7(10, 77, 45)]
+    bufs += [bufs[0][:len(bufs[0]) // 2], b"not an image at all", b""]  # malformed items
+    return bufs
+
+
+def check_results(bufs, res):
+    assert len(res) == len(bufs)
+    for data, r in zip(bufs, res):
+        want, status = oracle_rgba(data)
+        if status != "Ok":
+            # the batch reports the image's own error (fromBuffer's, incl. UnknownImageFormat)
+            assert r.status == status, (r.status, status)
+            assert r.rgba is None
+            continue
+        assert r.status == "Ok", r.status
+        got = r.rgba.cpu().numpy() if hasattr(r.rgba, "cpu") else r.rgba
+        assert got.shape == want.shape
+        assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("threads,depth", [(1, 1), (4, 3), (0, 0)])
+def test_batch_device_dst(threads, depth):
+    bufs = mixed_buffers()
+    res = batch.decode_rgba(bufs, host_threads=threads, depth=depth)
+    check_results(bufs, res)
+
+
+def test_batch_host_dst():
+    bufs = mixed_buffers()
+    res, st = batch.decode_rgba(bufs, on_host=True, host_threads=3, with_stats=True)
+    check_results(bufs, res)
+    ok = [r for r in res if r.status == "Ok"]
+    assert st.pixels == sum(r.width * r.height for r in ok)
+    assert st.failed == len(bufs) - len(ok)
+    assert st.d2h_bytes == st.pixels * 4
+
+
+def test_batch_padded_stride_and_short_capacity():
+    """dst_stride > 4W writes rows at the caller's pitch and leaves the pad
+    alone; a destination that is too small fails only its own item."""
+    data = [S.jpeg_420(3, 100, 37), S.png_tc8_mixed(4, 61, 29), read("pngsuite", "basn3p08.png")]
+    c = zpix_amd.context.default()
+    items = (_lib.zpx_batch_item * 4)()
+    bufs = data + [data[0]]
+    dsts, pitches = [], []
+    for i, d in enumerate(bufs):
+        want, _ = oracle_rgba(d)
+        h, w = want.shape[:2]
+        pitch = w * 4 + 52 if i < 3 else w * 4
+        t = torch.full((h * pitch,), 0xAB, dtype=torch.uint8, device="cuda")
+        dsts.append(t)
+        pitches.append(pitch)
+        items[i].buf = C.cast(C.c_char_p(d), C.c_void_p)
+        items[i].len = len(d)
+        items[i].dst = t.data_ptr()
+        items[i].dst_stride = pitch
+        items[i].dst_capacity = t.numel() if i < 3 else t.numel() - 1
+    torch.cuda.synchronize()
+    opts = _lib.zpx_batch_opts(2, 2, 0)
+    _lib.check(_lib.lib().zpx_batch_decode_rgba(c.handle, items, 4, C.byref(opts), None), c.handle)
+    for i in range(3):
+        want, _ = oracle_rgba(bufs[i])
+        h, w = want.shape[:2]
+        got = dsts[i].cpu().numpy().reshape(h, pitches[i])
+        assert items[i].status == 0
+        assert np.array_equal(got[:, :w * 4].reshape(h, w, 4), want)
+        assert (got[:, w * 4:] == 0xAB).all()
+    assert _lib.error_name(items[3].status) == "InvalidArgument"
+
+
+def test_batch_async_start_wait():
+    bufs = [S.jpeg_420(i, 160 + 16 * i, 90) for i in range(5)] + [S.png_tc8_mixed(5, 200, 64)]
+    c = zpix_amd.context.default()
+    items = (_lib.zpx_batch_item * len(bufs))()
+    outs = []
+    for i, d in enumerate(bufs):
+        want, _ = oracle_rgba(d)
+        arr = np.zeros_like(want)
+        outs.append((arr, want))
+        items[i].buf = C.cast(C.c_char_p(d), C.c_void_p)
+        items[i].len = len(d)
+        items[i].dst = arr.ctypes.data
+        items[i].dst_capacity = arr.nbytes
+    opts = _lib.zpx_batch_opts(2, 0, 1)
+    h = C.c_void_p()
+    _lib.check(_lib.lib().zpx_batch_start(c.handle, items, len(bufs), C.byref(opts), C.byref(h)))
+    st = _lib.zpx_batch_stats()
+    _lib.check(_lib.lib().zpx_batch_wait(h, C.byref(st)), c.handle)
+    assert st.failed == 0
+    for i, (arr, want) in enumerate(outs):
+        assert items[i].status == 0
+        assert np.array_equal(arr, want)
+
+
+def test_batch_empty():
+    assert batch.decode_rgba([]) == []
+
+
+def test_batch_4k_pair_matches_oracle():
+    """One bench-size JPEG and PNG through the streaming path (device dst)."""
+    bufs = [S.jpeg_420(0, 4096, 4096), S.png_tc8_mixed(0, 4096, 4096)]
+    res = batch.decode_rgba(bufs, host_threads=2)
+    check_results(bufs, res)

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-from . import _lib, context, jpeg, png
+from . import _lib, batch, context, jpeg, png
 from ._lib import ZpixError
 from .context import Context
 from .image import Image, Rectangle

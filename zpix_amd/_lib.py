@@ -95,6 +95,38 @@ class zpx_png_frame(C.Structure):
     ]
 
 
+class zpx_batch_item(C.Structure):
+    _fields_ = [
+        ("buf", C.c_void_p),
+        ("len", C.c_size_t),
+        ("dst", C.c_void_p),
+        ("dst_stride", C.c_size_t),
+        ("dst_capacity", C.c_size_t),
+        ("status", C.c_int32),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("format", C.c_int32),
+    ]
+
+
+class zpx_batch_opts(C.Structure):
+    _fields_ = [("host_threads", C.c_int32), ("depth", C.c_int32), ("dst_on_host", C.c_int32)]
+
+
+class zpx_batch_stats(C.Structure):
+    _fields_ = [
+        ("wall_s", C.c_double),
+        ("host_s", C.c_double),
+        ("h2d_bytes", C.c_double),
+        ("d2h_bytes", C.c_double),
+        ("pixels", C.c_double),
+        ("host_threads", C.c_int32),
+        ("depth", C.c_int32),
+        ("failed", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
 # every symbol include/zpix_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "zpx_error_name", "zpx_last_error", "zpx_ctx_create", "zpx_ctx_destroy", "zpx_ctx_stream",
@@ -104,7 +136,8 @@ EXPORTS = [
     "zpx_jpeg_plan_create", "zpx_png_plan_create", "zpx_plan_launch", "zpx_plan_bytes",
     "zpx_plan_kernel_count", "zpx_plan_destroy", "zpx_dev_rgba_pixels", "zpx_jpeg_entropy_decode",
     "zpx_jpeg_coeffs_frame", "zpx_jpeg_coeffs_free", "zpx_png_inflate", "zpx_png_stream_frame",
-    "zpx_png_stream_data", "zpx_png_stream_free",
+    "zpx_png_stream_data", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
+    "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config",
 ]
 
 _lib = None
@@ -153,6 +186,13 @@ def lib():
         "zpx_png_stream_frame": (i32, [vp, C.POINTER(zpx_png_frame), C.POINTER(sz)]),
         "zpx_png_stream_data": (vp, [vp]),
         "zpx_png_stream_free": (None, [vp]),
+        "zpx_batch_decode_rgba": (i32, [vp, C.POINTER(zpx_batch_item), i32, C.POINTER(zpx_batch_opts),
+                                        C.POINTER(zpx_batch_stats)]),
+        "zpx_batch_start": (i32, [vp, C.POINTER(zpx_batch_item), i32, C.POINTER(zpx_batch_opts), C.POINTER(vp)]),
+        "zpx_batch_wait": (i32, [vp, C.POINTER(zpx_batch_stats)]),
+        "zpx_jpeg_decode_config": (i32, [C.c_char_p, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_int32)]),
+        "zpx_png_decode_config": (i32, [C.c_char_p, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

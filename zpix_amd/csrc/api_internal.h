@@ -1,0 +1,97 @@
+// Internals shared by the C-ABI translation units (zpx_api.cpp, batch.cpp):
+// the context, HIP error reporting, device buffers and allocator helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "zpix_amd.h"
+
+struct zpx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+};
+
+namespace zpx {
+
+inline int hip_fail(zpx_ctx *ctx, hipError_t e, const char *what)
+{
+    if (ctx) {
+        char buf[256];
+        snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+        ctx->last_error = buf;
+    }
+    return ZPX_E_HIP;
+}
+
+#define HIPCHK(ctx, call)                                                      \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) return ::zpx::hip_fail((ctx), e_, #call);        \
+    } while (0)
+
+// Device buffer (RAII).
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    hipError_t alloc(size_t n)
+    {
+        release();
+        bytes = n ? n : 1;
+        return hipMalloc(&ptr, bytes);
+    }
+    // grow-only: keeps the buffer when it is already large enough
+    hipError_t reserve(size_t n)
+    {
+        if (ptr && bytes >= n) return hipSuccess;
+        return alloc(n);
+    }
+    template <typename T> T *as() const { return static_cast<T *>(ptr); }
+};
+
+inline void *al_alloc(const zpx_allocator *al, size_t n)
+{
+    if (al && al->alloc) return al->alloc(al->user, n ? n : 1);
+    return malloc(n ? n : 1);
+}
+inline void al_free(const zpx_allocator *al, void *p, size_t n)
+{
+    if (!p) return;
+    if (al && al->free) al->free(al->user, p, n);
+    else free(p);
+}
+
+struct CtxScope { // make ctx->device current for this call
+    explicit CtxScope(zpx_ctx *c) { (void)hipSetDevice(c->device); }
+};
+
+struct JpegCoeffs;
+struct DevJpegFrame;
+struct DevPngPass;
+struct DevImage;
+
+// zpx_api.cpp helpers shared with the batch pipeline
+void jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes);
+DevJpegFrame dev_jpeg_frame(const zpx_jpeg_frame &f);
+bool jpeg_fusable(const zpx_jpeg_frame &f); // the fused RGBA kernel takes this frame
+int launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_frame, hipStream_t st);
+void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
+                      uint64_t &bytes);
+DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette);
+
+} // namespace zpx

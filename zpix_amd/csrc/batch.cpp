@@ -1,0 +1,588 @@
+// Batch / streaming decode (include/zpix_amd.h, zpx_batch_*): the host
+// entropy stages run on a thread pool while the calling thread streams their
+// results to the GPU and runs the kernels, so Huffman/inflate of image k+1..
+// overlaps the PCIe copy of image k and the kernels of image k-1.
+//
+//   workers (host_threads)          dispatcher (calling thread)
+//   ----------------------          -----------------------------------------
+//   take item i, wait for a slot    pop a decoded item, bind it to a free slot
+//   jpeg_entropy_decode / png_parse copy stream : H2D coefficients / filtered
+//     into pinned (pooled) buffers                bytes -> ev_in
+//   push to the ready queue         compute     : wait ev_in, descriptor H2D,
+//                                                 fused JPEG / PNG kernels
+//                                   d2h stream  : (dst_on_host) RGBA -> host
+//                                   retire a slot once its ev_done completes
+//
+// Per image this is exactly zpix.fromBuffer + Image.rgbaPixels (src/root.zig:24-40,
+// src/image/image.zig:103-130): the fused JPEG kernel for the interleaved
+// geometries, the PNG unfilter kernel (+ rgbaPixels kernel when the decoded
+// image type is not already RGBA8), and the per-image entry point for the
+// rare JPEG kinds the fused kernel does not take (CMYK, YCCK, non-interleaved).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "api_internal.h"
+#include "device_types.h"
+#include "jpeg_host.h"
+#include "kernels.h"
+#include "png_host.h"
+#include "zpix_amd.h"
+
+using namespace zpx;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t n) { return (n + kAlign - 1) & ~(kAlign - 1); }
+
+double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Decoded {
+    int item = -1;
+    int fmt = 0; // 1 JPEG, 2 PNG
+    int status = ZPX_OK;
+    JpegCoeffs jc;
+    PngStream ps;
+};
+
+struct Slot {
+    DevBuf din, dout, dimg, ddesc, dctl, dbound;
+    HostBuf hdesc, hstatus; // pinned descriptor staging, PNG status word
+    hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
+    std::unique_ptr<Decoded> dec;
+    bool busy = false;
+    bool check_png = false;
+};
+
+bool host_reserve(HostBuf &b, size_t n) { return b.bytes >= n || b.alloc(n, false); }
+
+class Pipeline {
+  public:
+    Pipeline(zpx_ctx *ctx, zpx_batch_item *items, int n, const zpx_batch_opts *o) : ctx_(ctx), items_(items), n_(n)
+    {
+        const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+        threads_ = o && o->host_threads > 0 ? o->host_threads : std::min(16, hw);
+        depth_ = o && o->depth > 0 ? o->depth : 2 * threads_;
+        depth_ = std::max(depth_, 1);
+        on_host_ = o && o->dst_on_host;
+        tokens_ = depth_;
+    }
+    ~Pipeline();
+    int run(zpx_batch_stats *stats);
+
+  private:
+    void worker();
+    int setup();
+    int issue(Slot &s, bool &sync_done);
+    int issue_jpeg(Slot &s, bool &sync_done);
+    int issue_png(Slot &s);
+    int finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32_t W, uint32_t H, hipStream_t producer);
+    void retire(Slot &s);
+    void give_token();
+
+    zpx_ctx *ctx_;
+    zpx_batch_item *items_;
+    int n_;
+    int threads_ = 1, depth_ = 1;
+    bool on_host_ = false;
+
+    hipStream_t h2d_ = nullptr, d2h_ = nullptr;
+    std::vector<std::unique_ptr<Slot>> slots_;
+    std::vector<std::thread> workers_;
+
+    std::mutex mu_;
+    std::condition_variable cv_ready_, cv_token_;
+    std::deque<std::unique_ptr<Decoded>> ready_;
+    int tokens_ = 0;
+    bool stop_ = false;
+    std::atomic<int> next_{0};
+    double host_s_ = 0;
+    double h2d_bytes_ = 0, d2h_bytes_ = 0, pixels_ = 0;
+    int failed_ = 0;
+};
+
+Pipeline::~Pipeline()
+{
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_token_.notify_all();
+    for (auto &t : workers_)
+        if (t.joinable()) t.join();
+    (void)hipStreamSynchronize(ctx_->stream);
+    if (h2d_) (void)hipStreamSynchronize(h2d_);
+    if (d2h_) (void)hipStreamSynchronize(d2h_);
+    for (auto &s : slots_) {
+        if (s->ev_in) (void)hipEventDestroy(s->ev_in);
+        if (s->ev_kernel) (void)hipEventDestroy(s->ev_kernel);
+        if (s->ev_done) (void)hipEventDestroy(s->ev_done);
+    }
+    if (h2d_) (void)hipStreamDestroy(h2d_);
+    if (d2h_) (void)hipStreamDestroy(d2h_);
+}
+
+void Pipeline::worker()
+{
+    for (;;) {
+        const int i = next_.fetch_add(1);
+        if (i >= n_) return;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_token_.wait(lk, [&] { return tokens_ > 0 || stop_; });
+            if (stop_) return;
+            tokens_--;
+        }
+        std::unique_ptr<Decoded> d(new Decoded);
+        d->item = i;
+        const zpx_batch_item &it = items_[i];
+        const double t0 = now_s();
+        if (zpx_png_probe_buffer(it.buf, it.len)) {
+            d->fmt = 2;
+            d->status = png_parse(it.buf, it.len, d->ps);
+        } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
+            d->fmt = 1;
+            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc);
+        } else if (it.buf && it.len >= 4 && (memcmp(it.buf, "qoif", 4) == 0 || (it.buf[0] == 'B' && it.buf[1] == 'M'))) {
+            d->status = ZPX_E_UNSUPPORTED; // QOI / BMP: out of scope (zpx_from_buffer)
+        } else {
+            d->status = ZPX_E_UNKNOWN_IMAGE_FORMAT;
+        }
+        const double dt = now_s() - t0;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            host_s_ += dt;
+            ready_.push_back(std::move(d));
+        }
+        cv_ready_.notify_one();
+    }
+}
+
+void Pipeline::give_token()
+{
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        tokens_++;
+    }
+    cv_token_.notify_one();
+}
+
+int Pipeline::setup()
+{
+    HIPCHK(ctx_, hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
+    HIPCHK(ctx_, hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
+    for (int i = 0; i < depth_; i++) {
+        std::unique_ptr<Slot> s(new Slot);
+        HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming));
+        HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_kernel, hipEventDisableTiming));
+        HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
+        // PNG control words {epoch, ticket, status, pad}: zero once; every
+        // launch bumps the epoch (png_ctl_kernel), so they are never cleared
+        HIPCHK(ctx_, s->dctl.alloc(16));
+        HIPCHK(ctx_, hipMemsetAsync(s->dctl.ptr, 0, 16, ctx_->stream));
+        if (!s->hstatus.alloc(16, true)) return ZPX_E_OUT_OF_MEMORY;
+        slots_.push_back(std::move(s));
+    }
+    HIPCHK(ctx_, hipStreamSynchronize(ctx_->stream));
+    return ZPX_OK;
+}
+
+// Copies a finished contiguous RGBA8 result (4W stride) into the item's dst.
+int Pipeline::finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32_t W, uint32_t H,
+                          hipStream_t producer)
+{
+    const zpx_batch_item &it = items_[s.dec->item];
+    const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
+    if (on_host_) {
+        HIPCHK(ctx_, hipEventRecord(s.ev_kernel, producer));
+        HIPCHK(ctx_, hipStreamWaitEvent(d2h_, s.ev_kernel, 0));
+        HIPCHK(ctx_, hipMemcpy2DAsync(it.dst, stride, src, src_stride, size_t(W) * 4, H, hipMemcpyDeviceToHost, d2h_));
+        HIPCHK(ctx_, hipEventRecord(s.ev_done, d2h_));
+        d2h_bytes_ += double(W) * H * 4;
+    } else {
+        if (src != it.dst)
+            HIPCHK(ctx_, hipMemcpy2DAsync(it.dst, stride, src, src_stride, size_t(W) * 4, H, hipMemcpyDeviceToDevice,
+                                          producer));
+        HIPCHK(ctx_, hipEventRecord(s.ev_done, producer));
+    }
+    return ZPX_OK;
+}
+
+int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
+{
+    Decoded &d = *s.dec;
+    zpx_batch_item &it = items_[d.item];
+    zpx_jpeg_frame f;
+    size_t cb[4];
+    jpeg_fill_frame(d.jc, &f, cb);
+    const uint32_t W = f.width, H = f.height;
+    const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
+    const JpegOut kind = jpeg_output_kind(d.jc);
+    if (kind == JpegOut::CMYK || kind == JpegOut::YCCK || !jpeg_fusable(f)) {
+        // planes + colour pass through the per-image entry point (synchronous)
+        uint8_t *rgba = nullptr;
+        size_t rlen = 0;
+        uint32_t w = 0, h = 0;
+        int e = zpx_jpeg_decode_rgba(ctx_, nullptr, it.buf, it.len, &rgba, &rlen, &w, &h);
+        if (!e) {
+            if (on_host_) {
+                for (uint32_t y = 0; y < h; y++) memcpy(it.dst + y * stride, rgba + size_t(y) * w * 4, size_t(w) * 4);
+            } else {
+                hipError_t he = hipMemcpy2D(it.dst, stride, rgba, size_t(w) * 4, size_t(w) * 4, h, hipMemcpyHostToDevice);
+                if (he != hipSuccess) e = hip_fail(ctx_, he, "batch: rgba upload");
+            }
+            free(rgba);
+        }
+        it.status = e;
+        sync_done = true;
+        return e == ZPX_E_HIP ? e : ZPX_OK;
+    }
+    // fused dequant + IDCT + upsample + colour straight into the destination
+    size_t total = 0;
+    for (int c = 0; c < 4; c++) total += f.coeffs[c] ? align_up(cb[c]) : 0;
+    HIPCHK(ctx_, s.din.reserve(total));
+    size_t off = 0;
+    for (int c = 0; c < 4; c++) {
+        if (!f.coeffs[c]) continue;
+        uint8_t *dst = s.din.as<uint8_t>() + off;
+        HIPCHK(ctx_, hipMemcpyAsync(dst, f.coeffs[c], cb[c], hipMemcpyHostToDevice, h2d_));
+        f.coeffs[c] = dst;
+        off += align_up(cb[c]);
+        h2d_bytes_ += double(cb[c]);
+    }
+    HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
+    HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
+    const bool direct = !on_host_;
+    uint8_t *out;
+    if (direct) {
+        out = it.dst;
+        f.rgba_stride = stride;
+    } else {
+        HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+        out = s.dout.as<uint8_t>();
+        f.rgba_stride = size_t(W) * 4;
+    }
+    f.rgba = out;
+    const DevJpegFrame df = dev_jpeg_frame(f);
+    if (!host_reserve(s.hdesc, sizeof(df))) return ZPX_E_OUT_OF_MEMORY;
+    memcpy(s.hdesc.ptr, &df, sizeof(df));
+    HIPCHK(ctx_, s.ddesc.reserve(sizeof(df)));
+    HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.ptr, s.hdesc.ptr, sizeof(df), hipMemcpyHostToDevice, ctx_->stream));
+    if (int rc = launch_jpeg_rgba_frame(f, s.ddesc.as<DevJpegFrame>(), ctx_->stream))
+        return rc == -2 ? ZPX_E_UNSUPPORTED : hip_fail(ctx_, hipGetLastError(), "batch: jpeg kernel");
+    if (direct) {
+        HIPCHK(ctx_, hipEventRecord(s.ev_done, ctx_->stream));
+        return ZPX_OK;
+    }
+    return finish_copy(s, out, size_t(W) * 4, W, H, ctx_->stream);
+}
+
+int Pipeline::issue_png(Slot &s)
+{
+    Decoded &d = *s.dec;
+    zpx_batch_item &it = items_[d.item];
+    PngStream &ps = d.ps;
+    const uint32_t W = ps.width, H = ps.height;
+    const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
+    HIPCHK(ctx_, s.din.reserve(ps.data_len + ZPX_PNG_INPUT_PAD));
+    HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, ps.data.ptr, ps.data_len + ZPX_PNG_INPUT_PAD, hipMemcpyHostToDevice, h2d_));
+    h2d_bytes_ += double(ps.data_len);
+    HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
+    HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
+
+    // readImagePass's image type: RGBA8 already is the rgbaPixels layout
+    const bool rgba_native = ps.kind == ZPX_RGBA;
+    const bool direct = !on_host_ && (rgba_native || stride == size_t(W) * 4);
+    uint8_t *img_out;
+    size_t img_stride;
+    if (rgba_native) {
+        if (direct) {
+            img_out = it.dst;
+            img_stride = stride;
+        } else {
+            HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+            img_out = s.dout.as<uint8_t>();
+            img_stride = size_t(W) * 4;
+        }
+    } else {
+        img_stride = size_t(W) * ps.out_bpp;
+        HIPCHK(ctx_, s.dimg.reserve(img_stride * H));
+        img_out = s.dimg.as<uint8_t>();
+    }
+    zpx_png_frame f;
+    memset(&f, 0, sizeof(f));
+    f.width = W;
+    f.height = H;
+    f.depth = ps.depth;
+    f.interlace = ps.interlace;
+    f.use_transparent = ps.use_transparent;
+    memcpy(f.transparent, ps.transparent, 6);
+    f.filtered = s.din.as<uint8_t>();
+    f.out = img_out;
+    f.out_stride = img_stride;
+    f.max_index = nullptr; // palette handled below with all 256 entries
+    std::vector<DevPngPass> passes;
+    std::vector<uint32_t> rowbytes;
+    uint64_t bytes = 0;
+    png_frame_passes(f, passes, rowbytes, bytes);
+    uint32_t base = 0, max_bands = 0, max_rb = 0;
+    for (size_t i = 0; i < passes.size(); i++) {
+        DevPngPass &p = passes[i];
+        p.nbands = (p.rows + 63) / 64;
+        p.band_base = base;
+        base += p.nbands;
+        max_bands = std::max(max_bands, p.nbands);
+        max_rb = std::max(max_rb, rowbytes[i]);
+    }
+    std::vector<DevPngBand> sched; // band-major over the passes (as zpx_png_plan_create)
+    for (uint32_t b = 0; b < max_bands; b++)
+        for (size_t i = 0; i < passes.size(); i++)
+            if (b < passes[i].nbands) sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
+    const uint32_t granules = static_cast<uint32_t>(png_band_granules(ps.depth, max_rb));
+    // descriptor staging: passes | sched | palette (256 zpx_color)
+    const size_t pass_b = align_up(passes.size() * sizeof(DevPngPass));
+    const size_t sched_b = align_up(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand));
+    const size_t pal_b = 256 * sizeof(zpx_color);
+    const size_t desc_b = pass_b + sched_b + pal_b;
+    if (!host_reserve(s.hdesc, desc_b)) return ZPX_E_OUT_OF_MEMORY;
+    uint8_t *h = static_cast<uint8_t *>(s.hdesc.ptr);
+    memcpy(h, passes.data(), passes.size() * sizeof(DevPngPass));
+    if (!sched.empty()) memcpy(h + pass_b, sched.data(), sched.size() * sizeof(DevPngBand));
+    memcpy(h + pass_b + sched_b, ps.palette, pal_b);
+    HIPCHK(ctx_, s.ddesc.reserve(desc_b));
+    HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.ptr, h, desc_b, hipMemcpyHostToDevice, ctx_->stream));
+    const size_t bound_b = std::max<size_t>(1, base) * granules * sizeof(uint64_t);
+    if (s.dbound.bytes < bound_b) { // fresh granules carry tag 0, older than any epoch
+        HIPCHK(ctx_, s.dbound.alloc(bound_b));
+        HIPCHK(ctx_, hipMemsetAsync(s.dbound.ptr, 0, bound_b, ctx_->stream));
+    }
+    uint8_t *dd = s.ddesc.as<uint8_t>();
+    if (launch_png_unfilter(ps.depth, reinterpret_cast<const DevPngPass *>(dd),
+                            reinterpret_cast<const DevPngBand *>(dd + pass_b), static_cast<uint32_t>(sched.size()),
+                            s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(), granules, ctx_->stream))
+        return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
+    HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, ctx_->stream));
+    s.check_png = true;
+    if (rgba_native) {
+        if (direct) {
+            HIPCHK(ctx_, hipEventRecord(s.ev_done, ctx_->stream));
+            return ZPX_OK;
+        }
+        return finish_copy(s, img_out, size_t(W) * 4, W, H, ctx_->stream);
+    }
+    // Image.rgbaPixels of the decoded image type (premultiply, palette, 16-bit)
+    zpx_image img{};
+    img.kind = ps.kind;
+    img.max_x = static_cast<int32_t>(W);
+    img.max_y = static_cast<int32_t>(H);
+    img.stride = img_stride;
+    img.pixels_len = img_stride * H;
+    // grown palette entries are opaque black (readImagePass :1079-1134), which
+    // is what entries past PLTE/tRNS already hold, so all 256 are live
+    img.palette_len = ps.kind == ZPX_PALETTED ? 256 : 0;
+    const DevImage m = dev_image_of(&img, img_out, ps.kind == ZPX_PALETTED ? dd + pass_b + sched_b : nullptr);
+    uint8_t *rgba;
+    if (direct) {
+        rgba = it.dst;
+    } else {
+        HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+        rgba = s.dout.as<uint8_t>();
+    }
+    if (launch_rgba_pixels(m, rgba, ctx_->stream)) return hip_fail(ctx_, hipGetLastError(), "batch: rgba kernel");
+    if (direct) {
+        HIPCHK(ctx_, hipEventRecord(s.ev_done, ctx_->stream));
+        return ZPX_OK;
+    }
+    return finish_copy(s, rgba, size_t(W) * 4, W, H, ctx_->stream);
+}
+
+int Pipeline::issue(Slot &s, bool &sync_done)
+{
+    Decoded &d = *s.dec;
+    zpx_batch_item &it = items_[d.item];
+    const uint32_t W = d.fmt == 1 ? d.jc.width : d.ps.width, H = d.fmt == 1 ? d.jc.height : d.ps.height;
+    it.width = W;
+    it.height = H;
+    const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
+    const size_t need = H ? (size_t(H) - 1) * stride + size_t(W) * 4 : 0;
+    if (!it.dst || stride < size_t(W) * 4 || it.dst_capacity < need || stride > (size_t(1) << 31) / 32) {
+        it.status = ZPX_E_INVALID_ARGUMENT;
+        sync_done = true;
+        return ZPX_OK;
+    }
+    sync_done = false;
+    s.check_png = false;
+    return d.fmt == 1 ? issue_jpeg(s, sync_done) : issue_png(s);
+}
+
+void Pipeline::retire(Slot &s)
+{
+    zpx_batch_item &it = items_[s.dec->item];
+    if (s.check_png && *static_cast<volatile uint32_t *>(s.hstatus.ptr) != 0) {
+        ctx_->last_error = "png wavefront hand-off timed out";
+        it.status = ZPX_E_HIP;
+    } else {
+        it.status = ZPX_OK;
+        pixels_ += double(it.width) * it.height;
+    }
+    s.dec.reset(); // pinned host buffers go back to the pool
+    s.busy = false;
+    give_token();
+}
+
+int Pipeline::run(zpx_batch_stats *stats)
+{
+    const double t0 = now_s();
+    for (int i = 0; i < n_; i++) {
+        items_[i].status = ZPX_E_HIP; // until completed
+        items_[i].width = items_[i].height = 0;
+        items_[i].format = zpx_png_probe_buffer(items_[i].buf, items_[i].len) ? 2
+                           : zpx_jpeg_probe_buffer(items_[i].buf, items_[i].len) ? 1 : 0;
+    }
+    if (int e = setup()) return e;
+    try {
+        for (int t = 0; t < std::min(threads_, std::max(n_, 1)); t++) workers_.emplace_back([this] { worker(); });
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+    int done = 0, rc = ZPX_OK;
+    while (done < n_ && rc == ZPX_OK) {
+        std::unique_ptr<Decoded> d;
+        bool any_busy = false;
+        for (auto &s : slots_) any_busy |= s->busy;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            if (ready_.empty()) {
+                if (any_busy) cv_ready_.wait_for(lk, std::chrono::microseconds(100));
+                else cv_ready_.wait(lk, [&] { return !ready_.empty(); });
+            }
+            if (!ready_.empty()) {
+                d = std::move(ready_.front());
+                ready_.pop_front();
+            }
+        }
+        if (d) {
+            if (d->status != ZPX_OK) {
+                items_[d->item].status = d->status;
+                done++;
+                give_token();
+            } else {
+                Slot *free_slot = nullptr;
+                for (auto &s : slots_)
+                    if (!s->busy) {
+                        free_slot = s.get();
+                        break;
+                    }
+                // a worker holds a token for every decoded item, and there are
+                // as many tokens as slots, so a free slot always exists here
+                Slot &s = *free_slot;
+                s.dec = std::move(d);
+                s.busy = true;
+                bool sync_done = false;
+                rc = issue(s, sync_done);
+                if (rc == ZPX_OK && sync_done) {
+                    if (items_[s.dec->item].status == ZPX_OK)
+                        pixels_ += double(items_[s.dec->item].width) * items_[s.dec->item].height;
+                    s.dec.reset();
+                    s.busy = false;
+                    done++;
+                    give_token();
+                }
+            }
+        }
+        for (auto &sp : slots_) {
+            Slot &s = *sp;
+            if (!s.busy) continue;
+            const hipError_t q = hipEventQuery(s.ev_done);
+            if (q == hipSuccess) {
+                retire(s);
+                done++;
+            } else if (q != hipErrorNotReady) {
+                rc = hip_fail(ctx_, q, "batch: event");
+                break;
+            }
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_token_.notify_all();
+    for (auto &t : workers_) t.join();
+    workers_.clear();
+    for (int i = 0; i < n_; i++) failed_ += items_[i].status != ZPX_OK;
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->wall_s = now_s() - t0;
+        stats->host_s = host_s_;
+        stats->h2d_bytes = h2d_bytes_;
+        stats->d2h_bytes = d2h_bytes_;
+        stats->pixels = pixels_;
+        stats->host_threads = threads_;
+        stats->depth = depth_;
+        stats->failed = failed_;
+    }
+    return rc;
+}
+
+} // namespace
+
+extern "C" int zpx_batch_decode_rgba(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                                     zpx_batch_stats *stats)
+{
+    if (!ctx || n_items < 0 || (n_items > 0 && !items)) return ZPX_E_INVALID_ARGUMENT;
+    CtxScope scope(ctx);
+    try {
+        Pipeline p(ctx, items, n_items, opts);
+        return p.run(stats);
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+}
+
+struct zpx_batch {
+    std::thread th;
+    int rc = ZPX_OK;
+    zpx_batch_stats stats{};
+};
+
+extern "C" int zpx_batch_start(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                               zpx_batch **out)
+{
+    if (!ctx || !out || n_items < 0 || (n_items > 0 && !items)) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    zpx_batch_opts o{};
+    if (opts) o = *opts;
+    try {
+        std::unique_ptr<zpx_batch> b(new zpx_batch);
+        zpx_batch *bp = b.get();
+        b->th = std::thread([=] { bp->rc = zpx_batch_decode_rgba(ctx, items, n_items, &o, &bp->stats); });
+        *out = b.release();
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+    return ZPX_OK;
+}
+
+extern "C" int zpx_batch_wait(zpx_batch *b, zpx_batch_stats *stats)
+{
+    if (!b) return ZPX_E_INVALID_ARGUMENT;
+    if (b->th.joinable()) b->th.join();
+    const int rc = b->rc;
+    if (stats) *stats = b->stats;
+    delete b;
+    return rc;
+}

@@ -8,6 +8,8 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 namespace zpx {
 
@@ -18,9 +20,11 @@ HostBuf &HostBuf::operator=(HostBuf &&o) noexcept
         release();
         ptr = o.ptr;
         bytes = o.bytes;
+        cap = o.cap;
         pinned = o.pinned;
         o.ptr = nullptr;
         o.bytes = 0;
+        o.cap = 0;
         o.pinned = false;
     }
     return *this;
@@ -37,15 +41,68 @@ static bool pinned_allowed()
     return ok == 1;
 }
 
+namespace {
+// Free pinned buffers by capacity.  Never freed at exit (the HIP runtime may
+// already be gone); bounded by ZPX_PINNED_POOL_MB (default 2048).
+struct PinnedPool {
+    std::mutex mu;
+    std::multimap<size_t, void *> free_;
+    size_t held = 0, limit = 0;
+    PinnedPool()
+    {
+        const char *env = getenv("ZPX_PINNED_POOL_MB");
+        limit = size_t(env ? atol(env) : 2048) << 20;
+    }
+    static size_t size_class(size_t n)
+    {
+        const size_t g = n >= (size_t(1) << 20) ? (size_t(1) << 20) : 4096;
+        return (n + g - 1) / g * g;
+    }
+    void *take(size_t c, size_t &got) // a buffer of capacity got in [c, 1.25c]
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = free_.lower_bound(c);
+        if (it == free_.end() || it->first > c + c / 4) return nullptr;
+        void *p = it->second;
+        got = it->first;
+        held -= it->first;
+        free_.erase(it);
+        return p;
+    }
+    bool give(void *p, size_t c)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (held + c > limit) return false;
+        free_.emplace(c, p);
+        held += c;
+        return true;
+    }
+};
+PinnedPool &pinned_pool()
+{
+    static PinnedPool *pool = new PinnedPool; // intentionally leaked
+    return *pool;
+}
+} // namespace
+
 bool HostBuf::alloc(size_t n, bool zero)
 {
     release();
     if (n == 0) n = 1;
-    if (pinned_allowed() && hipHostMalloc(&ptr, n, hipHostMallocDefault) == hipSuccess) {
-        pinned = true;
-    } else {
+    if (pinned_allowed()) {
+        const size_t c = PinnedPool::size_class(n);
+        size_t got = c;
+        ptr = pinned_pool().take(c, got);
+        if (!ptr && hipHostMalloc(&ptr, c, hipHostMallocDefault) != hipSuccess) ptr = nullptr;
+        if (ptr) {
+            pinned = true;
+            cap = got;
+        }
+    }
+    if (!ptr) {
         ptr = aligned_alloc(64, (n + 63) & ~size_t(63));
         pinned = false;
+        cap = 0;
         if (!ptr) return false;
     }
     bytes = n;
@@ -56,11 +113,15 @@ bool HostBuf::alloc(size_t n, bool zero)
 void HostBuf::release()
 {
     if (ptr) {
-        if (pinned) (void)hipHostFree(ptr);
-        else free(ptr);
+        if (pinned) {
+            if (!pinned_pool().give(ptr, cap)) (void)hipHostFree(ptr);
+        } else {
+            free(ptr);
+        }
     }
     ptr = nullptr;
     bytes = 0;
+    cap = 0;
     pinned = false;
 }
 
@@ -139,8 +200,12 @@ struct Huff { // HuffTable.zig
 
 class Decoder {
   public:
-    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out) : src_(p), len_(n), o_(out) {}
+    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out, bool config_only = false)
+        : src_(p), len_(n), o_(out), config_only_(config_only)
+    {
+    }
     int run();
+    static constexpr int kConfigOnly = -1; // decodeInner's error.ConfigOnly
 
   private:
     // --- byte source (the whole input stays addressable, so the
@@ -320,6 +385,7 @@ class Decoder {
     int32_t quant_[4][64] = {}; // zig-zag order, as the reference keeps it
     uint8_t tmp_[128] = {};
     bool seen_sos_ = false;
+    bool config_only_ = false;
     bool interleaved_[4] = {}, noninterleaved_[4] = {};
 };
 
@@ -705,15 +771,29 @@ int Decoder::run()
             o_.baseline = marker == 0xc0;
             o_.progressive = marker == 0xc2;
             ZTRY(sof(n));
+            if (config_only_ && o_.jfif) return kConfigOnly; // :311-313
             break;
-        case 0xdb: ZTRY(dqt(n)); break;
+        case 0xdb:
+            if (config_only_) ZTRY(skip(n)); // :315-321
+            else ZTRY(dqt(n));
+            break;
         case 0xdd: // processDri :621-627
+            if (config_only_) {
+                ZTRY(skip(n));
+                break;
+            }
             if (n != 2) return ZPX_E_DRI_WRONG_LENGTH;
             ZTRY(full(tmp_, 2));
             restart_interval_ = static_cast<uint16_t>((tmp_[0] << 8) + tmp_[1]);
             break;
-        case 0xc4: ZTRY(dht(n)); break;
-        case 0xda: ZTRY(sos(n)); break;
+        case 0xc4:
+            if (config_only_) ZTRY(skip(n));
+            else ZTRY(dht(n));
+            break;
+        case 0xda:
+            if (config_only_) return kConfigOnly; // :336-340
+            ZTRY(sos(n));
+            break;
         case 0xe0: // processApp0Marker :668-680
             if (n < 5) {
                 ZTRY(skip(n));
@@ -763,6 +843,21 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out)
 {
     Decoder d(buf, len, out);
     return d.run();
+}
+
+int jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h, int &model)
+{ // decodeConfig :178-218
+    JpegCoeffs c;
+    Decoder d(buf, len, c, true);
+    const int e = d.run();
+    if (e != Decoder::kConfigOnly) return e ? e : ZPX_E_MISSING_SOS_MARKER;
+    w = c.width;
+    h = c.height;
+    switch (c.n_comp) {
+    case 1: model = ZPX_MODEL_GRAY; return ZPX_OK;
+    case 3: case 4: model = ZPX_MODEL_YCBCR; return ZPX_OK; // "TODO: Support CMYK" (:212-216)
+    default: return ZPX_E_INVALID_SOI_MARKER;
+    }
 }
 
 JpegOut jpeg_output_kind(const JpegCoeffs &c)

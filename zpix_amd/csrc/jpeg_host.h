@@ -14,9 +14,12 @@ namespace zpx {
 
 // Host buffer that prefers pinned (page-locked) memory so H2D copies are
 // DMA-direct; falls back to ordinary memory when no HIP device is usable.
+// Pinned buffers are recycled through a process-wide pool (hipHostMalloc of a
+// 50 MB grid costs milliseconds; a batch decodes thousands of them).
 struct HostBuf {
     void *ptr = nullptr;
     size_t bytes = 0;
+    size_t cap = 0; // allocation size (pool size class) of a pinned buffer
     bool pinned = false;
     HostBuf() = default;
     HostBuf(const HostBuf &) = delete;
@@ -74,6 +77,10 @@ struct JpegCoeffs {
 // Decode `buf` into coefficient grids.  Returns ZPX_E_* (ZPX_E_OK on success),
 // with the reference's error for malformed input.
 int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out);
+
+// jpeg.decodeConfig (decoder.zig:178-218): markers up to SOF (JFIF) or SOS,
+// skipping DQT/DRI/DHT.  model: ZPX_MODEL_GRAY or ZPX_MODEL_YCBCR.
+int jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h, int &model);
 
 // Output kind decodeInner would return (decoder.zig:361-372).
 enum class JpegOut { Gray, YCbCr, RGB, CMYK, YCCK };

@@ -42,7 +42,7 @@ bool paletted(int d) { return d >= ZPX_PNG_P1 && d <= ZPX_PNG_P8; }
 class Parser {
   public:
     Parser(const uint8_t *p, size_t n, PngStream &o) : src_(p), len_(n), o_(o) {}
-    int run();
+    int run(bool header_only = false);
 
   private:
     int read(uint8_t *p, size_t n)
@@ -362,12 +362,16 @@ int Parser::chunk()
     return verify();
 }
 
-int Parser::run()
+int Parser::run(bool header_only)
 {
     static const uint8_t kSig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     uint8_t sig[8];
     if (int e = read(sig, 8)) return e;
     if (memcmp(sig, kSig, 8) != 0) return ZPX_E_INVALID_PNG_HEADER;
+    if (header_only) { // first chunk must be IHDR (parseChunk's stage check)
+        if (int e = chunk()) return e;
+        return stage_ == 1 ? 0 : ZPX_E_CHUNK_ORDER_IN_HEADER_ERROR;
+    }
     while (stage_ != 5)
         if (int e = chunk()) return e;
     if (!have_image_) return ZPX_E_INVALID_IMAGE_DIMENSIONS;
@@ -380,6 +384,16 @@ int png_parse(const uint8_t *buf, size_t len, PngStream &out)
 {
     Parser p(buf, len, out);
     return p.run();
+}
+
+int png_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h)
+{
+    PngStream s;
+    Parser p(buf, len, s);
+    if (int e = p.run(true)) return e;
+    w = s.width;
+    h = s.height;
+    return 0;
 }
 
 } // namespace zpx

@@ -41,4 +41,7 @@ struct PngStream {
 // chunk-level error.
 int png_parse(const uint8_t *buf, size_t len, PngStream &out);
 
+// Signature + IHDR only (dimensions of the image png.decode would return).
+int png_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h);
+
 } // namespace zpx

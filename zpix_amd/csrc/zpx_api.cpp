@@ -15,6 +15,7 @@
 #include <tuple>
 #include <vector>
 
+#include "api_internal.h"
 #include "device_types.h"
 #include "jpeg_host.h"
 #include "kernels.h"
@@ -36,70 +37,9 @@ extern "C" const char *zpx_error_name(int code)
     return kErrorNames[code];
 }
 
-struct zpx_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string last_error;
-};
-
 extern "C" const char *zpx_last_error(const zpx_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
 namespace {
-
-int hip_fail(zpx_ctx *ctx, hipError_t e, const char *what)
-{
-    if (ctx) {
-        char buf[256];
-        snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
-        ctx->last_error = buf;
-    }
-    return ZPX_E_HIP;
-}
-
-#define HIPCHK(ctx, call)                                                      \
-    do {                                                                       \
-        hipError_t e_ = (call);                                                \
-        if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);               \
-    } while (0)
-
-// Device buffer (RAII).
-struct DevBuf {
-    void *ptr = nullptr;
-    size_t bytes = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf &) = delete;
-    DevBuf &operator=(const DevBuf &) = delete;
-    ~DevBuf() { release(); }
-    void release()
-    {
-        if (ptr) (void)hipFree(ptr);
-        ptr = nullptr;
-        bytes = 0;
-    }
-    hipError_t alloc(size_t n)
-    {
-        release();
-        bytes = n ? n : 1;
-        return hipMalloc(&ptr, bytes);
-    }
-    template <typename T> T *as() const { return static_cast<T *>(ptr); }
-};
-
-void *al_alloc(const zpx_allocator *al, size_t n)
-{
-    if (al && al->alloc) return al->alloc(al->user, n ? n : 1);
-    return malloc(n ? n : 1);
-}
-void al_free(const zpx_allocator *al, void *p, size_t n)
-{
-    if (!p) return;
-    if (al && al->free) al->free(al->user, p, n);
-    else free(p);
-}
-
-struct CtxScope { // make ctx->device current for this call
-    explicit CtxScope(zpx_ctx *c) { (void)hipSetDevice(c->device); }
-};
 
 int read_file(const char *path, std::vector<uint8_t> &out)
 {
@@ -165,7 +105,7 @@ extern "C" void zpx_image_free(const zpx_allocator *al, zpx_image *img)
     img->pixels_len = 0;
 }
 
-static DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette)
+DevImage zpx::dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette)
 {
     DevImage m{};
     m.pixels = static_cast<const uint8_t *>(d_pixels);
@@ -230,6 +170,46 @@ extern "C" int zpx_image_rgba_pixels(zpx_ctx *ctx, const zpx_allocator *al, cons
 }
 
 // ------------------------------------------------------------------ plans
+DevJpegFrame zpx::dev_jpeg_frame(const zpx_jpeg_frame &f)
+{
+    DevJpegFrame d{};
+    for (int c = 0; c < 4; c++) {
+        d.coeffs[c] = c < f.n_comp ? f.coeffs[c] : nullptr;
+        d.planes[c] = f.planes[c];
+        d.strides[c] = f.strides[c];
+        d.h[c] = f.h[c];
+        d.v[c] = f.v[c];
+        d.rule[c] = c < f.n_comp ? f.rule[c] : ZPX_BLOCKS_NONE;
+        memcpy(d.qt[c], f.qt[c], sizeof(d.qt[c]));
+    }
+    if (f.n_comp == 1) d.h[0] = d.v[0] = 1;
+    d.rgba = f.rgba;
+    d.rgba_stride = f.rgba_stride;
+    d.width = static_cast<int32_t>(f.width);
+    d.height = static_cast<int32_t>(f.height);
+    d.mxx = f.mxx;
+    d.myy = f.myy;
+    d.n_comp = f.n_comp;
+    d.color = f.color;
+    return d;
+}
+
+bool zpx::jpeg_fusable(const zpx_jpeg_frame &f)
+{
+    if (f.n_comp == 4) return false;
+    const int color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
+    const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
+    const int hc = f.n_comp == 3 ? f.h[1] : 1, vc = f.n_comp == 3 ? f.v[1] : 1;
+    return jpeg_rgba_supported(color, h0, v0, hc, vc);
+}
+
+int zpx::launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_frame, hipStream_t st)
+{
+    const int color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
+    const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
+    const int hc = f.n_comp == 3 ? f.h[1] : 1, vc = f.n_comp == 3 ? f.v[1] : 1;
+    return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits == 32, f.narrow != 0, st);
+}
 struct JpegGroup {
     DevBuf frames;
     int n = 0;
@@ -300,26 +280,8 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
         std::vector<DevJpegFrame> df;
         for (int idx : kv.second) {
             const zpx_jpeg_frame &f = frames[idx];
-            DevJpegFrame d{};
+            const DevJpegFrame d = dev_jpeg_frame(f);
             const size_t esz = f.coeff_bits / 8;
-            for (int c = 0; c < 4; c++) {
-                d.coeffs[c] = c < f.n_comp ? f.coeffs[c] : nullptr;
-                d.planes[c] = f.planes[c];
-                d.strides[c] = f.strides[c];
-                d.h[c] = f.h[c];
-                d.v[c] = f.v[c];
-                d.rule[c] = c < f.n_comp ? f.rule[c] : ZPX_BLOCKS_NONE;
-                memcpy(d.qt[c], f.qt[c], sizeof(d.qt[c]));
-            }
-            if (f.n_comp == 1) d.h[0] = d.v[0] = 1;
-            d.rgba = f.rgba;
-            d.rgba_stride = f.rgba_stride;
-            d.width = static_cast<int32_t>(f.width);
-            d.height = static_cast<int32_t>(f.height);
-            d.mxx = f.mxx;
-            d.myy = f.myy;
-            d.n_comp = f.n_comp;
-            d.color = f.color;
             df.push_back(d);
             for (int c = 0; c < f.n_comp; c++) {
                 const int gw = f.mxx * d.h[c], gh = f.myy * d.v[c];
@@ -381,8 +343,8 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
     return 0;
 }
 
-static void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
-                             uint64_t &bytes)
+void zpx::png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
+                           uint64_t &bytes)
 {
     static const uint32_t kA7[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
                                        {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
@@ -544,7 +506,7 @@ extern "C" int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_
     return ZPX_OK;
 }
 
-static void fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes)
+void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes)
 {
     memset(f, 0, sizeof(*f));
     f->width = c.width;
@@ -581,7 +543,7 @@ static void fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_byt
 extern "C" int zpx_jpeg_coeffs_frame(const zpx_jpeg_coeffs *cc, zpx_jpeg_frame *f, size_t *coeff_bytes)
 {
     if (!cc || !f) return ZPX_E_INVALID_ARGUMENT;
-    fill_frame(cc->c, f, coeff_bytes);
+    jpeg_fill_frame(cc->c, f, coeff_bytes);
     return ZPX_OK;
 }
 
@@ -631,7 +593,7 @@ struct JpegDeviceFrame {
 int upload_jpeg(zpx_ctx *ctx, const JpegCoeffs &c, JpegDeviceFrame &d)
 {
     size_t cbytes[4];
-    fill_frame(c, &d.f, cbytes);
+    jpeg_fill_frame(c, &d.f, cbytes);
     for (int i = 0; i < c.n_comp; i++) {
         if (!d.f.coeffs[i]) continue;
         HIPCHK(ctx, d.coeffs[i].alloc(cbytes[i]));
@@ -885,6 +847,29 @@ extern "C" int zpx_png_probe_buffer(const uint8_t *buf, size_t len)
 {
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
     return buf && len >= 8 && memcmp(buf, sig, 8) == 0;
+}
+
+extern "C" int zpx_jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height,
+                                      int32_t *color_model)
+{
+    if (!width || !height || !color_model || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    uint32_t w = 0, h = 0;
+    int m = 0;
+    if (int e = jpeg_decode_config(buf, len, w, h, m)) return e;
+    *width = w;
+    *height = h;
+    *color_model = m;
+    return ZPX_OK;
+}
+
+extern "C" int zpx_png_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height)
+{
+    if (!width || !height || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
+    uint32_t w = 0, h = 0;
+    if (int e = png_decode_config(buf, len, w, h)) return e;
+    *width = w;
+    *height = h;
+    return ZPX_OK;
 }
 
 extern "C" int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)

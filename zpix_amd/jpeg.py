@@ -32,6 +32,22 @@ def load(path: str, ctx: context.Context | None = None) -> Image:
     return Image._from_c(raw)
 
 
+MODELS = {0: "RGB", 1: "YCbCr", 2: "RGBA", 3: "Gray"}
+
+
+def decode_config(data: bytes):
+    """jpeg.decodeConfig (src/jpeg/decoder.zig:178-218) -> (width, height).
+    `decode_config_model` also returns the colour model name."""
+    w, h, _ = decode_config_model(data)
+    return w, h
+
+
+def decode_config_model(data: bytes):
+    w, h, m = C.c_uint32(0), C.c_uint32(0), C.c_int32(0)
+    _lib.check(_lib.lib().zpx_jpeg_decode_config(bytes(data), len(data), C.byref(w), C.byref(h), C.byref(m)))
+    return w.value, h.value, MODELS[m.value]
+
+
 def probe_buffer(data: bytes) -> bool:
     """jpeg.probeBuffer (src/jpeg/root.zig:17-21)."""
     return bool(_lib.lib().zpx_jpeg_probe_buffer(bytes(data[:2]), min(len(data), 2)))

@@ -37,6 +37,13 @@ def load(path: str, ctx: context.Context | None = None) -> Image:
     return Image._from_c(raw)
 
 
+def decode_config(data: bytes):
+    """(width, height) from the signature + IHDR (png/decoder.zig:224-401)."""
+    w, h = C.c_uint32(0), C.c_uint32(0)
+    _lib.check(_lib.lib().zpx_png_decode_config(bytes(data), len(data), C.byref(w), C.byref(h)))
+    return w.value, h.value
+
+
 def probe_buffer(data: bytes) -> bool:
     """png.probeBuffer (src/png/root.zig:37-40)."""
     return bytes(data[:8]) == PNG_SIGNATURE
