@@ -240,6 +240,7 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
         if (!e) {
             if (on_host_) {
                 for (uint32_t y = 0; y < h; y++) memcpy(it.dst + y * stride, rgba + size_t(y) * w * 4, size_t(w) * 4);
+                d2h_bytes_ += double(w) * h * 4; // came back over PCIe inside zpx_jpeg_decode_rgba
             } else {
                 hipError_t he = hipMemcpy2D(it.dst, stride, rgba, size_t(w) * 4, size_t(w) * 4, h, hipMemcpyHostToDevice);
                 if (he != hipSuccess) e = hip_fail(ctx_, he, "batch: rgba upload");
