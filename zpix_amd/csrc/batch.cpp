@@ -45,6 +45,20 @@ namespace {
 constexpr size_t kAlign = 256;
 size_t align_up(size_t n) { return (n + kAlign - 1) & ~(kAlign - 1); }
 
+// ZPX_BATCH_TRACE=1: one stderr line per pipeline event (debug aid)
+bool trace_on()
+{
+    static const bool on = getenv("ZPX_BATCH_TRACE") != nullptr;
+    return on;
+}
+#define ZPX_TRACE(...)                                                                                     \
+    do {                                                                                                   \
+        if (trace_on()) {                                                                                  \
+            fprintf(stderr, "[zpx batch] " __VA_ARGS__);                                                    \
+            fputc('\n', stderr);                                                                           \
+        }                                                                                                  \
+    } while (0)
+
 double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -162,6 +176,7 @@ void Pipeline::worker()
             d->status = ZPX_E_UNKNOWN_IMAGE_FORMAT;
         }
         const double dt = now_s() - t0;
+        ZPX_TRACE("worker: item %d fmt %d status %d decoded in %.3fs", i, d->fmt, d->status, dt);
         {
             std::lock_guard<std::mutex> lk(mu_);
             host_s_ += dt;
@@ -371,6 +386,8 @@ int Pipeline::issue_png(Slot &s)
         HIPCHK(ctx_, hipMemsetAsync(s.dbound.ptr, 0, bound_b, ctx_->stream));
     }
     uint8_t *dd = s.ddesc.as<uint8_t>();
+    ZPX_TRACE("png: item %d %ux%u depth %d interlace %d passes %zu bands %zu granules %u", d.item, W, H, ps.depth,
+              ps.interlace, passes.size(), sched.size(), granules);
     if (launch_png_unfilter(ps.depth, reinterpret_cast<const DevPngPass *>(dd),
                             reinterpret_cast<const DevPngBand *>(dd + pass_b), static_cast<uint32_t>(sched.size()),
                             s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(), granules, ctx_->stream))
@@ -403,6 +420,7 @@ int Pipeline::issue_png(Slot &s)
         rgba = s.dout.as<uint8_t>();
     }
     if (launch_rgba_pixels(m, rgba, ctx_->stream)) return hip_fail(ctx_, hipGetLastError(), "batch: rgba kernel");
+    ZPX_TRACE("png: item %d rgba kernel launched (kind %d)", d.item, ps.kind);
     if (direct) {
         HIPCHK(ctx_, hipEventRecord(s.ev_done, ctx_->stream));
         return ZPX_OK;
@@ -493,7 +511,9 @@ int Pipeline::run(zpx_batch_stats *stats)
                 s.dec = std::move(d);
                 s.busy = true;
                 bool sync_done = false;
+                ZPX_TRACE("dispatch: item %d -> slot %p", s.dec->item, static_cast<void *>(&s));
                 rc = issue(s, sync_done);
+                ZPX_TRACE("dispatch: item %d issued rc %d sync %d", s.dec->item, rc, sync_done ? 1 : 0);
                 if (rc == ZPX_OK && sync_done) {
                     if (items_[s.dec->item].status == ZPX_OK)
                         pixels_ += double(items_[s.dec->item].width) * items_[s.dec->item].height;
@@ -509,6 +529,7 @@ int Pipeline::run(zpx_batch_stats *stats)
             if (!s.busy) continue;
             const hipError_t q = hipEventQuery(s.ev_done);
             if (q == hipSuccess) {
+                ZPX_TRACE("retire: item %d", s.dec->item);
                 retire(s);
                 done++;
             } else if (q != hipErrorNotReady) {

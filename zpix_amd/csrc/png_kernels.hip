@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 
 #include "device_types.h"
 #include "kernels.h"
@@ -32,7 +34,14 @@ namespace zpx {
 namespace {
 
 constexpr int kRegionChunks = 16;
-constexpr uint32_t kSpinLimit = 1u << 24;
+#ifndef ZPX_PNG_RING
+#define ZPX_PNG_RING 8
+#endif
+constexpr int kRing = ZPX_PNG_RING;
+#ifndef ZPX_PNG_SPIN_LIMIT
+#define ZPX_PNG_SPIN_LIMIT (1u << 20)
+#endif
+constexpr uint32_t kSpinLimit = ZPX_PNG_SPIN_LIMIT;
 
 template <int DEPTH>
 struct Traits;
@@ -64,23 +73,31 @@ ZPX_PNG_TRAITS(ZPX_PNG_TCA16, 64)
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t *w, int i) { return (w[i >> 2] >> ((i & 3) * 8)) & 0xff; }
 
+// Output pointers are global-address-space so stores are global_store_* (a
+// flat store also counts against lgkmcnt and costs an aperture check).
+#define ZPX_GLOBAL __attribute__((address_space(1)))
+typedef ZPX_GLOBAL uint8_t gu8;
+typedef uint32_t gv4 __attribute__((ext_vector_type(4)));
+typedef uint32_t gv2 __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gcast(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
+
 // Store n bytes held in dwords w[] to dst, using 16-byte stores when aligned.
 template <int NB>
-__device__ __forceinline__ void store_bytes(uint8_t *dst, const uint32_t (&w)[(NB + 3) / 4])
+__device__ __forceinline__ void store_bytes(gu8 *dst, const uint32_t (&w)[(NB + 3) / 4])
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
     if constexpr (NB % 16 == 0) {
         if ((a & 15) == 0) {
 #pragma unroll
             for (int i = 0; i < NB / 16; i++)
-                reinterpret_cast<uint4 *>(dst)[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+                gcast<gv4>(dst)[i] = gv4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
             return;
         }
     }
     if constexpr (NB % 4 == 0) {
         if ((a & 3) == 0) {
 #pragma unroll
-            for (int i = 0; i < NB / 4; i++) reinterpret_cast<uint32_t *>(dst)[i] = w[i];
+            for (int i = 0; i < NB / 4; i++) gcast<uint32_t>(dst)[i] = w[i];
             return;
         }
     }
@@ -110,7 +127,7 @@ __device__ __forceinline__ void store_chunk(const DevPngPass &ps, uint32_t y, ui
     constexpr int C = Tr::kC, BPP = Tr::kBpp;
     const bool trns = ps.use_trns != 0;
     const int obpp = out_bpp<DEPTH>(trns);
-    uint8_t *row = ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride;
+    gu8 *row = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
     const uint32_t W = ps.width;
 
     if constexpr (Tr::kBits < 8 || DEPTH == ZPX_PNG_G8 || DEPTH == ZPX_PNG_P8) {
@@ -152,7 +169,7 @@ __device__ __forceinline__ void store_chunk(const DevPngPass &ps, uint32_t y, ui
                 uint32_t v = (byte >> (8 - kBits * (j + 1))) & ((1u << kBits) - 1);
                 if (kPal) maxidx = max(maxidx, static_cast<int>(v));
                 else v *= kMul;
-                uint8_t *d = row + static_cast<size_t>(x * ps.xf + ps.xo) * obpp;
+                gu8 *d = row + static_cast<size_t>(x * ps.xf + ps.xo) * obpp;
                 if (trns && !kPal) {
                     d[0] = d[1] = d[2] = static_cast<uint8_t>(v);
                     d[3] = v == ty ? 0x00 : 0xff;
@@ -238,16 +255,16 @@ __device__ __forceinline__ void store_chunk(const DevPngPass &ps, uint32_t y, ui
         for (int u = 0; u < C; u++) {
             const uint32_t x = x0 + u;
             if (x >= W) break;
-            uint8_t *d = row + static_cast<size_t>(x * ps.xf + ps.xo) * obpp;
+            gu8 *d = row + static_cast<size_t>(x * ps.xf + ps.xo) * obpp;
             if (obpp == 2) {
                 d[0] = static_cast<uint8_t>(pix[u][0]);
                 d[1] = static_cast<uint8_t>(pix[u][0] >> 8);
             } else if (obpp == 4) {
-                if ((reinterpret_cast<uintptr_t>(d) & 3) == 0) *reinterpret_cast<uint32_t *>(d) = pix[u][0];
+                if ((reinterpret_cast<uintptr_t>(d) & 3) == 0) *gcast<uint32_t>(d) = pix[u][0];
                 else for (int i = 0; i < 4; i++) d[i] = static_cast<uint8_t>(pix[u][0] >> (8 * i));
             } else {
                 if ((reinterpret_cast<uintptr_t>(d) & 7) == 0) {
-                    *reinterpret_cast<uint2 *>(d) = make_uint2(pix[u][0], pix[u][1]);
+                    *gcast<gv2>(d) = gv2{pix[u][0], pix[u][1]};
                 } else {
                     for (int i = 0; i < 4; i++) d[i] = static_cast<uint8_t>(pix[u][0] >> (8 * i));
                     for (int i = 0; i < 4; i++) d[4 + i] = static_cast<uint8_t>(pix[u][1] >> (8 * i));
@@ -257,10 +274,6 @@ __device__ __forceinline__ void store_chunk(const DevPngPass &ps, uint32_t y, ui
     }
 }
 
-__device__ __forceinline__ uint64_t ld_sc1_64(const uint64_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void st_sc1_64(uint64_t *p, uint64_t v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -288,6 +301,92 @@ __device__ __forceinline__ uint32_t recon_byte(const LaneFilter &lf, uint32_t f,
     return (f + t) & 0xffu;
 }
 
+// ---------------------------------------------------------------------------
+// Input staging.  The filtered bytes of every lane's row and the previous
+// band's boundary granules reach the wave through LDS-DMA (buffer_load ...
+// lds, no VGPR destination) into a per-wave LDS ring, issued R steps ahead
+// and waited for with an explicit s_waitcnt vmcnt(N).  hipcc cannot count
+// VMEM ops across the unrolled step loop's back-edge (it falls back to
+// vmcnt(0) or near it, serialising each step behind the prefetch it just
+// issued), and register-destination asm loads are unsafe (the compiler may
+// copy their registers before the data lands), so the DMA route is the one
+// that both prefetches and stays register-safe.  Counting rule (gfx950:
+// VMEM ops retire in issue order under one counter): a wait vmcnt(N) covers a
+// DMA when at least N of our DMAs were issued after it; VMEM ops hipcc
+// interleaves only make the wait stricter.  Every wait and DMA carries a
+// "memory" clobber so no LDS read moves across it.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+template <int CW> struct ChunkVec;
+template <> struct ChunkVec<3> { using T = u32x3; };
+template <> struct ChunkVec<4> { using T = u32x4; };
+
+// Raw buffer descriptor: base, stride 0, num_records bytes (the builtin's
+// resource type keeps it in SGPRs for the asm "s" operand).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void *base, uint32_t bytes)
+{
+    // readfirstlane: the inputs are wave-uniform, but hipcc cannot always
+    // prove it, and a divergent descriptor would be placed in VGPRs
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base);
+    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a)));
+    const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32)));
+    void *ua = reinterpret_cast<void *>(static_cast<uintptr_t>(hi << 32 | lo));
+    return __builtin_amdgcn_make_buffer_rsrc(ua, 0, static_cast<int>(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
+}
+
+// One chunk (CW dwords) of a lane's row, a load hipcc counts.
+template <int CW>
+__device__ __forceinline__ typename ChunkVec<CW>::T load_chunk(Rsrc rsrc, int voff)
+{
+    if constexpr (CW == 3) return __builtin_amdgcn_raw_buffer_load_b96(rsrc, voff, 0, 0);
+    else return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, 0);
+}
+
+// 16 bytes per lane, buffer[voff] -> LDS[lds_addr + 16*lane].  Offsets
+// outside the descriptor read as zero.  SC1 selects the agent-scope
+// (cross-XCD coherent) load used for the boundary granules.
+// FRESH: the descriptor was just written by v_readfirstlane (VALU -> SGPR ->
+// VMEM descriptor read needs 5 wait states, which hipcc does not insert
+// around inline asm).
+#define ZPX_DMA16(PRE, POL)                                                                      \
+    asm volatile(PRE "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"                       \
+                 "buffer_load_dwordx4 %1, %2, 0 offen " POL "lds\n\ts_mov_b32 m0, %0"            \
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_addr) : "memory")
+template <bool SC1, bool FRESH = false>
+__device__ __forceinline__ void dma16(uint32_t lds_addr, Rsrc rsrc, int voff)
+{
+    uint32_t keep;
+    if constexpr (SC1 && FRESH) ZPX_DMA16("s_nop 4\n\t", "sc1 ");
+    else if constexpr (SC1) ZPX_DMA16("", "sc1 ");
+    else if constexpr (FRESH) ZPX_DMA16("s_nop 4\n\t", "");
+    else ZPX_DMA16("", "");
+}
+#undef ZPX_DMA16
+
+template <int N> __device__ __forceinline__ void wait_vm()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Boundary window, synchronously: lane l fetches granules 2l and 2l+1 with
+// one agent-scope (sc1) 16-byte load; load and wait are one asm statement
+// with early-clobber outputs, so the registers are complete when hipcc sees
+// them.  vmcnt(0) also retires the ring DMAs in flight; this happens once per
+// window of WIN chunks.
+__device__ __forceinline__ u32x4 load_window_sync(const uint64_t *p)
+{
+    // two agent-scope 8-byte loads (global_load_dwordx2 sc1), visible to
+    // hipCC's waitcnt bookkeeping (inline asm here made it drain every
+    // outstanding ring load at every step)
+    const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return u32x4{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
+                 static_cast<uint32_t>(b >> 32)};
+}
+
 template <int DEPTH>
 __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__restrict__ passes,
                                                           const DevPngBand *__restrict__ sched, uint32_t nsched,
@@ -295,9 +394,20 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
 {
     using Tr = Traits<DEPTH>;
     constexpr int BPP = Tr::kBpp, C = Tr::kC, CW = Tr::kCW;
-    constexpr int WIN = kRegionChunks;          // chunks per window
-    constexpr int WG = WIN * CW;                // granules per window (<= 64)
-    static_assert(WG <= 64, "window must fit one granule per lane");
+    constexpr int WIN = kRegionChunks;          // chunks per boundary window
+    constexpr int WG = WIN * CW;                // granules per window (2 per DMA lane)
+    constexpr int R = kRing;                    // input prefetch distance (steps) = ring slots
+    constexpr int kSlot = 1024;                 // one DMA = 64 lanes x 16 B
+    static_assert(WG <= 128, "a window is one 16-byte load per lane");
+    __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
+    static_assert(R >= 2 && R - 2 <= 63, "vmcnt range");
+#ifdef ZPX_PNG_LDS_RING
+    __shared__ __attribute__((aligned(16))) uint8_t lds[R * kSlot];
+    const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)lds)));
+    const uint8_t *ring_p = lds;
+#endif
+
     const int lane = threadIdx.x;
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
     uint32_t *ticket = ctl + 1, *status = ctl + 2;
@@ -315,17 +425,61 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         const int nchunks = static_cast<int>((nunits + C - 1) / C);
         const uint32_t y = bd.band * 64 + lane;
         const bool row_ok = y < ps.rows;
-        const uint8_t *frow = ps.filtered + static_cast<size_t>(y) * (rb + 1);
-        const int ft = row_ok ? frow[0] : 0;
+        const uint32_t band_rows = min(64u, ps.rows - bd.band * 64);
+
+        const int ft = row_ok ? ps.filtered[static_cast<size_t>(y) * (rb + 1)] : 0;
         const LaneFilter lf{ft == 1, ft == 2, ft == 3, ft == 4};
-        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(frow + 1) & 3);
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(frow + 1 - mis);
+        // Dependency-aware skew: a row filtered with Up/Avg/Paeth needs the row
+        // above one chunk ahead of it; a None/Sub row needs nothing above, so
+        // it starts at step 0 and restarts the chain (lane 0 synchronises with
+        // the previous band through the boundary granules instead).
+        // skew(j) = j - (last lane <= j that restarts the chain).
+        const bool dep = ft >= 2;
+        const uint64_t restart = __ballot(!dep || lane == 0);
+        const uint64_t upto = restart & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        const int skew = lane - (63 - __builtin_clzll(upto));
+        int max_skew = row_ok ? skew : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) max_skew = max(max_skew, __shfl_xor(max_skew, off));
+        max_skew = __builtin_amdgcn_readfirstlane(max_skew);
+        const bool dep0 = (__ballot(dep) & 1ull) != 0;
+
+        // band input: one descriptor based at the dword below the band's
+        // first byte; its extent covers the band's rows plus 64 bytes (the
+        // next band, the next pass or ZPX_PNG_INPUT_PAD is always behind them)
+        const uint8_t *band0 = ps.filtered + static_cast<size_t>(bd.band) * 64 * (rb + 1);
+        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
+        const uint32_t delta = static_cast<uint32_t>(band0 - base4);
+        const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + 64;
+        const uint32_t nrec = extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent);
+        const Rsrc rsrc = make_rsrc(base4, nrec);
+        const uint32_t row_off = delta + static_cast<uint32_t>(lane) * (rb + 1); // filter byte of my row
+        const uint32_t mis = (row_off + 1) & 3;
+        const int data_off = static_cast<int>(row_off + 1 - mis); // dword holding my row's first data byte
+        // Every DMA stays inside the descriptor: offsets are clamped rather than
+        // left to the range check (chunks before a row's start, or past the
+        // band's data, are never consumed, so any in-range bytes will do).
+        const int max_off = static_cast<int>((nrec - 16u) & ~3u);
+        auto chunk_off = [&](int k) { return k >= 0 ? min(data_off + k * CW * 4, max_off) : 0; };
 
         const bool has_prev = bd.band > 0;
         const bool has_next = bd.band + 1 < ps.nbands;
+        const bool poll = has_prev && dep0; // lane 0 reads the previous band's last row
         const uint64_t *prev_bnd =
             boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) * band_granules;
         uint64_t *my_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band) * band_granules;
+        // window starting at chunk w0: lane l < WG/2 holds granules 2l, 2l+1
+        auto window_ptr = [&](int w0) { return prev_bnd + (2 * lane < WG ? w0 * CW + 2 * lane : 0); };
+        // the current window is staged in LDS (one 16-byte write per lane) and
+        // read back at a wave-uniform address: per-step polling then waits on
+        // lgkmcnt only, never on the ring's outstanding vector loads
+        auto fill_window = [&](int w0) {
+            const u32x4 v = load_window_sync(window_ptr(w0));
+            if (2 * lane < WG) reinterpret_cast<u32x4 *>(win_lds)[lane] = v;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
 
         uint32_t left[BPP], ul[BPP];
 #pragma unroll
@@ -333,70 +487,108 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         uint32_t outp[CW];
 #pragma unroll
         for (int i = 0; i < CW; i++) outp[i] = 0;
-        uint32_t carry = 0;
-        uint64_t win = 0, win_next = 0;
         int maxidx = 0;
 
-        auto load_window = [&](int w0) -> uint64_t {
-            const int k = w0 + lane / CW;
-            return (lane < WG && k < nchunks) ? ld_sc1_64(prev_bnd + static_cast<size_t>(w0) * CW + lane) : 0ull;
-        };
-        if (has_prev) win = load_window(0);
-
-        const uint32_t band_rows = min(64u, ps.rows - bd.band * 64);
-        const int nsteps = nchunks + static_cast<int>(band_rows) - 1;
-        for (int step = 0; step < nsteps; ++step) {
-            const int k = step - lane;
-            const bool act = row_ok && k >= 0 && k < nchunks;
-
-            // ---- the row above: chunk k of row y-1 was produced by lane-1 one step ago
-            uint32_t up[CW];
+        // prologue: the ring (slot r = step r)
+#ifdef ZPX_PNG_LDS_RING
 #pragma unroll
-            for (int i = 0; i < CW; i++)
-                up[i] = __builtin_amdgcn_update_dpp(0, static_cast<int>(outp[i]), 0x138, 0xf, 0xf, false);
-            if (has_prev && step < nchunks) { // lane 0: chunk `step` of the previous band's last row
-                const int wi = step % WIN;
-                if (wi == 0 && step > 0) win = win_next;
-                if (wi == WIN / 2 && step + WIN / 2 < nchunks) win_next = load_window(step + WIN / 2);
-                const int base = wi * CW;
-                uint32_t spins = 0;
-                for (;;) {
-                    bool ready = true;
+        for (int r = 0; r < R; r++) dma16<false, true>(lds_ring + r * kSlot, rsrc, chunk_off(r - skew));
+#else
+        // CW dwords per slot: a dword the step never reads would be a dead
+        // register the compiler reuses at once, forcing a vmcnt(0) (WAW)
+        typename ChunkVec<CW>::T ring[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) ring[r] = load_chunk<CW>(rsrc, chunk_off(r - skew));
+#endif
+
+        const int nsteps = nchunks + max_skew;
+        for (int step0 = 0; step0 < nsteps; step0 += R) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int step = step0 + r;
+                if (step >= nsteps) break;
+                const int k = step - skew;
+                const bool act = row_ok && k >= 0 && k < nchunks;
+                // ring slots r and r+1 have landed (R-2 DMAs were issued after slot r+1's)
+#ifdef ZPX_PNG_LDS_RING
+                wait_vm<R - 2>();
+#endif
+
+                // ---- the row above: chunk k of row y-1 was produced by lane-1 one step ago
+                uint32_t up[CW];
+#pragma unroll
+                for (int i = 0; i < CW; i++)
+                    up[i] = __builtin_amdgcn_update_dpp(0, static_cast<int>(outp[i]), 0x138, 0xf, 0xf, false);
+                if (poll && step < nchunks) { // lane 0: chunk `step` of the previous band's last row
+                    // At a window's first chunk, wait until the previous band has
+                    // published the WHOLE window (its last chunk's granules carry
+                    // this launch's epoch), so the next WIN-1 steps read it with no
+                    // reload: a band trails the one above by its skew + WIN chunks.
+                    const int wi = step % WIN;
+                    const int last = min(WIN, nchunks - (step - wi)) - 1; // last chunk of this window
+                    if (wi == 0) fill_window(step);
+                    auto chunk_ready = [&](int c) {
+                        bool ok = true;
+#pragma unroll
+                        for (int i = 0; i < CW; i++) {
+                            const int gi = c * CW + i;
+                            const uint32_t tag = static_cast<uint32_t>(win_lds[gi] >> 32);
+                            ok &= tag == epoch;
+                        }
+                        return ok;
+                    };
+                    uint32_t spins = 0;
+                    for (;;) {
+                        // this chunk's granules (publication order is not visibility
+                        // order), and at a window's start also its last chunk
+                        const bool ready = chunk_ready(wi) && (wi != 0 || chunk_ready(last));
+                        if (ready) break;
+                        if (++spins > kSpinLimit) {
+#ifdef ZPX_PNG_DEBUG
+                            if (!timed_out && lane == 0)
+                                printf("png timeout: pass %u band %u step %d wi %d last %d nchunks %d epoch %u "
+                                       "tag(wi)=%u tag(last)=%u ptr=%p\n",
+                                       bd.pass, bd.band, step, wi, last, nchunks, epoch,
+                                       static_cast<uint32_t>(win_lds[wi * CW] >> 32),
+                                       static_cast<uint32_t>(win_lds[last * CW] >> 32),
+                                       (const void *)window_ptr(step - wi));
+#endif
+                            timed_out = true;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                        fill_window(step - wi);
+                    }
+                    uint32_t gv[CW];
 #pragma unroll
                     for (int i = 0; i < CW; i++) {
-                        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(win >> 32), base + i);
-                        ready &= hi == epoch;
+                        const int gi = wi * CW + i;
+                        gv[i] = static_cast<uint32_t>(win_lds[gi]);
                     }
-                    if (ready) break;
-                    if (++spins > kSpinLimit) {
-                        timed_out = true;
-                        break;
+                    if (lane == 0) {
+#pragma unroll
+                        for (int i = 0; i < CW; i++) up[i] = gv[i];
                     }
-                    __builtin_amdgcn_s_sleep(1);
-                    if (lane >= base && lane < base + CW)
-                        win = ld_sc1_64(prev_bnd + static_cast<size_t>(step - wi) * CW + lane);
-                }
+                } else if (lane == 0) {
 #pragma unroll
-                for (int i = 0; i < CW; i++) {
-                    const uint32_t v = __builtin_amdgcn_readlane(static_cast<int>(win), base + i);
-                    if (lane == 0) up[i] = v;
+                    for (int i = 0; i < CW; i++) up[i] = 0; // first row of a pass: zero previous row (:790-793)
                 }
-            } else if (lane == 0) {
-#pragma unroll
-                for (int i = 0; i < CW; i++) up[i] = 0; // first row of a pass: zero previous row (:790-793)
-            }
 
-            if (act) {
-                // ---- filtered bytes of chunk k (dword window + funnel shift)
-                if (k == 0) carry = src[0];
-                uint32_t in[CW + 1];
-                in[0] = carry;
-#pragma unroll
-                for (int i = 1; i <= CW; i++) in[i] = src[k * CW + i];
-                carry = in[CW];
+                // ---- filtered bytes of chunk k: slot r + the first dword of slot r+1
+                // (every lane computes; only active lanes store)
+#ifdef ZPX_PNG_LDS_RING
+                const u32x4 cur = *reinterpret_cast<const u32x4 *>(ring_p + r * kSlot + lane * 16);
+                const uint32_t nxt = *reinterpret_cast<const uint32_t *>(ring_p + ((r + 1) % R) * kSlot + lane * 16);
+#else
+                const auto cur = ring[r];
+                const uint32_t nxt = ring[(r + 1) % R][0];
+#endif
                 uint32_t f[CW];
 #pragma unroll
-                for (int i = 0; i < CW; i++) f[i] = __builtin_amdgcn_alignbyte(in[i + 1], in[i], mis);
+                for (int i = 0; i < CW; i++) {
+                    const uint32_t hi = i + 1 < CW ? cur[i + 1] : nxt;
+                    f[i] = __builtin_amdgcn_alignbyte(hi, cur[i], mis);
+                }
                 if (k == 0) {
 #pragma unroll
                     for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
@@ -405,41 +597,40 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 uint32_t ob[CW];
 #pragma unroll
                 for (int i = 0; i < CW; i++) ob[i] = 0;
-                uint32_t prev_out[BPP], prev_up[BPP];
-#pragma unroll
-                for (int i = 0; i < BPP; i++) {
-                    prev_out[i] = left[i];
-                    prev_up[i] = ul[i];
-                }
 #pragma unroll
                 for (int u = 0; u < C; u++) {
 #pragma unroll
                     for (int i = 0; i < BPP; i++) {
                         const int idx = u * BPP + i;
                         const uint32_t b = byte_of(up, idx);
-                        const uint32_t v = recon_byte(lf, byte_of(f, idx), prev_out[i], b, prev_up[i]);
+                        const uint32_t v = recon_byte(lf, byte_of(f, idx), left[i], b, ul[i]);
                         ob[idx >> 2] |= v << ((idx & 3) * 8);
-                        prev_out[i] = v;
-                        prev_up[i] = b;
+                        left[i] = v;
+                        ul[i] = b;
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < BPP; i++) {
-                    left[i] = prev_out[i];
-                    ul[i] = prev_up[i];
-                }
-#pragma unroll
                 for (int i = 0; i < CW; i++) outp[i] = ob[i];
+                // refill slot r with the chunk R steps ahead (slot r was read above)
+#ifdef ZPX_PNG_LDS_RING
+                dma16<false>(lds_ring + r * kSlot, rsrc, chunk_off(k + R));
+#else
+                ring[r] = load_chunk<CW>(rsrc, chunk_off(k + R));
+#endif
 
-                store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
-
-                if (has_next && lane == 63) { // publish: the data is the flag
-                    uint64_t *d = my_bnd + static_cast<size_t>(k) * CW;
+                if (act) {
+                    store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
+                    if (has_next && lane == 63) { // publish: the data is the flag
+                        uint64_t *d = my_bnd + static_cast<size_t>(k) * CW;
 #pragma unroll
-                    for (int i = 0; i < CW; i++) st_sc1_64(d + i, static_cast<uint64_t>(epoch) << 32 | ob[i]);
+                        for (int i = 0; i < CW; i++) st_sc1_64(d + i, static_cast<uint64_t>(epoch) << 32 | ob[i]);
+                    }
                 }
             }
         }
+#ifdef ZPX_PNG_LDS_RING
+        wait_vm<0>(); // the ring's last DMAs land before the next band reuses the slots
+#endif
         if constexpr (DEPTH >= ZPX_PNG_P1 && DEPTH <= ZPX_PNG_P8) {
             for (int off = 32; off > 0; off >>= 1) maxidx = max(maxidx, __shfl_xor(maxidx, off));
             if (lane == 0 && ps.max_index) atomicMax(ps.max_index, maxidx);
@@ -484,11 +675,16 @@ template <int DEPTH>
 void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl, uint64_t *boundary,
               uint32_t band_granules, hipStream_t s)
 {
+    static const bool trace = getenv("ZPX_BATCH_TRACE") != nullptr;
+    if (trace) fprintf(stderr, "[zpx png] launch depth %d nsched %u\n", DEPTH, nsched);
     const uint32_t want = static_cast<uint32_t>(cus() * png_waves_per_cu());
     const uint32_t grid = nsched < want ? nsched : want;
+    if (trace) fprintf(stderr, "[zpx png] grid %u; ctl kernel\n", grid);
     hipLaunchKernelGGL(png_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
+    if (trace) fprintf(stderr, "[zpx png] unfilter kernel\n");
     hipLaunchKernelGGL((png_unfilter_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
                        band_granules);
+    if (trace) fprintf(stderr, "[zpx png] launched\n");
 }
 
 } // namespace
