@@ -307,7 +307,7 @@ enum zpx_png_depth {
     ZPX_PNG_GA16, ZPX_PNG_TC16, ZPX_PNG_TCA16,
 };
 /* Readable bytes the device input must have past its last filtered row. */
-#define ZPX_PNG_INPUT_PAD 64
+#define ZPX_PNG_INPUT_PAD 256
 
 /* One PNG image after host inflate (parseIdat, png/decoder.zig:404-545). */
 typedef struct zpx_png_frame {

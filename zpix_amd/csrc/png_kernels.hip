@@ -34,10 +34,10 @@ namespace zpx {
 namespace {
 
 constexpr int kRegionChunks = 16;
-#ifndef ZPX_PNG_RING
-#define ZPX_PNG_RING 8
+#ifndef ZPX_PNG_GROUP
+#define ZPX_PNG_GROUP 8
 #endif
-constexpr int kRing = ZPX_PNG_RING;
+constexpr int kGroup = ZPX_PNG_GROUP; // steps per input/output burst
 #ifndef ZPX_PNG_SPIN_LIMIT
 #define ZPX_PNG_SPIN_LIMIT (1u << 20)
 #endif
@@ -70,6 +70,9 @@ ZPX_PNG_TRAITS(ZPX_PNG_GA16, 32)
 ZPX_PNG_TRAITS(ZPX_PNG_TC16, 48)
 ZPX_PNG_TRAITS(ZPX_PNG_TCA16, 64)
 #undef ZPX_PNG_TRAITS
+
+// Steps a band takes: its chunks plus the largest lane skew.
+__device__ __forceinline__ int nsteps_of(int nchunks, int max_skew) { return nchunks + max_skew; }
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t *w, int i) { return (w[i >> 2] >> ((i & 3) * 8)) & 0xff; }
 
@@ -302,89 +305,91 @@ __device__ __forceinline__ uint32_t recon_byte(const LaneFilter &lf, uint32_t f,
 }
 
 // ---------------------------------------------------------------------------
-// Input staging.  The filtered bytes of every lane's row and the previous
-// band's boundary granules reach the wave through LDS-DMA (buffer_load ...
-// lds, no VGPR destination) into a per-wave LDS ring, issued R steps ahead
-// and waited for with an explicit s_waitcnt vmcnt(N).  hipcc cannot count
-// VMEM ops across the unrolled step loop's back-edge (it falls back to
-// vmcnt(0) or near it, serialising each step behind the prefetch it just
-// issued), and register-destination asm loads are unsafe (the compiler may
-// copy their registers before the data lands), so the DMA route is the one
-// that both prefetches and stays register-safe.  Counting rule (gfx950:
-// VMEM ops retire in issue order under one counter): a wait vmcnt(N) covers a
-// DMA when at least N of our DMAs were issued after it; VMEM ops hipcc
-// interleaves only make the wait stricter.  Every wait and DMA carries a
-// "memory" clobber so no LDS read moves across it.
+// Input and output staging.  A wave owns 64 rows, one per lane, and each lane
+// walks its own row: every vector memory instruction touches 64 different
+// cache lines.  Reading 12-16 bytes of a row per step and writing 16 bytes per
+// step kept ~2 lines per row live in L2 for 8-10 steps each; at 2048 waves
+// (131k rows in flight) that working set is several times the 4 MB L2 of an
+// XCD, and PMC showed ~4x the algorithmic bytes fetched and ~3x written.  So
+// the step loop runs in groups of G steps: a lane loads the G chunks (+1
+// carry dword) of its next group in one burst of 16-byte loads one group
+// ahead, and (RGBA8 outputs) writes its G finished chunks as one contiguous
+// burst at the end of the group, so a line is fetched once and written whole.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-template <int CW> struct ChunkVec;
-template <> struct ChunkVec<3> { using T = u32x3; };
-template <> struct ChunkVec<4> { using T = u32x4; };
-
 // Raw buffer descriptor: base, stride 0, num_records bytes (the builtin's
-// resource type keeps it in SGPRs for the asm "s" operand).
+// resource type keeps it in SGPRs).  Offsets outside [0, num_records) --
+// negative ones included, as unsigned -- read as zero.
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 __device__ __forceinline__ Rsrc make_rsrc(const void *base, uint32_t bytes)
 {
     // readfirstlane: the inputs are wave-uniform, but hipcc cannot always
-    // prove it, and a divergent descriptor would be placed in VGPRs
-    const uintptr_t a = reinterpret_cast<uintptr_t>(base);
+    // prove it, and a divergent descriptor would be placed in VGPRs.
     // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base);
     const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a)));
     const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32)));
     void *ua = reinterpret_cast<void *>(static_cast<uintptr_t>(hi << 32 | lo));
     return __builtin_amdgcn_make_buffer_rsrc(ua, 0, static_cast<int>(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
 }
 
-// One chunk (CW dwords) of a lane's row, a load hipcc counts.
-template <int CW>
-__device__ __forceinline__ typename ChunkVec<CW>::T load_chunk(Rsrc rsrc, int voff)
+// N dwords from byte offset off (dword aligned) into d[0..N): 16-byte loads
+// then the remainder (no dead destination dwords: a register the code never
+// reads would be reused at once and force a wait on the whole burst).
+template <int N>
+__device__ __forceinline__ void load_dwords(uint32_t (&d)[N], Rsrc rsrc, int off)
 {
-    if constexpr (CW == 3) return __builtin_amdgcn_raw_buffer_load_b96(rsrc, voff, 0, 0);
-    else return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, 0);
+#pragma unroll
+    for (int i = 0; i + 4 <= N; i += 4) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 4 * i, 0, 0);
+        d[i] = v[0];
+        d[i + 1] = v[1];
+        d[i + 2] = v[2];
+        d[i + 3] = v[3];
+    }
+    constexpr int T = N & ~3;
+    if constexpr (N - T == 1) {
+        d[T] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4 * T, 0, 0);
+    } else if constexpr (N - T == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off + 4 * T, 0, 0);
+        d[T] = v[0];
+        d[T + 1] = v[1];
+    } else if constexpr (N - T == 3) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, off + 4 * T, 0, 0);
+        d[T] = v[0];
+        d[T + 1] = v[1];
+        d[T + 2] = v[2];
+    }
 }
 
-// 16 bytes per lane, buffer[voff] -> LDS[lds_addr + 16*lane].  Offsets
-// outside the descriptor read as zero.  SC1 selects the agent-scope
-// (cross-XCD coherent) load used for the boundary granules.
-// FRESH: the descriptor was just written by v_readfirstlane (VALU -> SGPR ->
-// VMEM descriptor read needs 5 wait states, which hipcc does not insert
-// around inline asm).
-#define ZPX_DMA16(PRE, POL)                                                                      \
-    asm volatile(PRE "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"                       \
-                 "buffer_load_dwordx4 %1, %2, 0 offen " POL "lds\n\ts_mov_b32 m0, %0"            \
-                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds_addr) : "memory")
-template <bool SC1, bool FRESH = false>
-__device__ __forceinline__ void dma16(uint32_t lds_addr, Rsrc rsrc, int voff)
+// Boundary window: lane l fetches granules 2l and 2l+1 with two agent-scope
+// (sc1) 8-byte loads.
+__device__ __forceinline__ u32x4 load_window(const uint64_t *p)
 {
-    uint32_t keep;
-    if constexpr (SC1 && FRESH) ZPX_DMA16("s_nop 4\n\t", "sc1 ");
-    else if constexpr (SC1) ZPX_DMA16("", "sc1 ");
-    else if constexpr (FRESH) ZPX_DMA16("s_nop 4\n\t", "");
-    else ZPX_DMA16("", "");
-}
-#undef ZPX_DMA16
-
-template <int N> __device__ __forceinline__ void wait_vm()
-{
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Boundary window, synchronously: lane l fetches granules 2l and 2l+1 with
-// one agent-scope (sc1) 16-byte load; load and wait are one asm statement
-// with early-clobber outputs, so the registers are complete when hipcc sees
-// them.  vmcnt(0) also retires the ring DMAs in flight; this happens once per
-// window of WIN chunks.
-__device__ __forceinline__ u32x4 load_window_sync(const uint64_t *p)
-{
-    // two agent-scope 8-byte loads (global_load_dwordx2 sc1), visible to
-    // hipCC's waitcnt bookkeeping (inline asm here made it drain every
-    // outstanding ring load at every step)
     const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return u32x4{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
                  static_cast<uint32_t>(b >> 32)};
+}
+
+// RGBA8 output words of one chunk of 4 pixels (TC8 -> RGBA / NRGBA with the
+// tRNS colour key, TCA8 -> NRGBA raw), as store_chunk's contiguous path.
+template <int DEPTH, int CW>
+__device__ __forceinline__ void pack_rgba4(const DevPngPass &ps, const uint32_t (&ob)[CW], uint32_t (&w)[4])
+{
+    if constexpr (DEPTH == ZPX_PNG_TCA8) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) w[u] = ob[u];
+    } else {
+        const bool trns = ps.use_trns != 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t r = byte_of(ob, 3 * u), g = byte_of(ob, 3 * u + 1), b = byte_of(ob, 3 * u + 2);
+            uint32_t a = 0xff;
+            if (trns && r == ps.trns[1] && g == ps.trns[3] && b == ps.trns[5]) a = 0;
+            w[u] = r | g << 8 | b << 16 | a << 24;
+        }
+    }
 }
 
 template <int DEPTH>
@@ -394,19 +399,15 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
 {
     using Tr = Traits<DEPTH>;
     constexpr int BPP = Tr::kBpp, C = Tr::kC, CW = Tr::kCW;
+    constexpr int CB = CW * 4;                  // bytes per chunk
     constexpr int WIN = kRegionChunks;          // chunks per boundary window
-    constexpr int WG = WIN * CW;                // granules per window (2 per DMA lane)
-    constexpr int R = kRing;                    // input prefetch distance (steps) = ring slots
-    constexpr int kSlot = 1024;                 // one DMA = 64 lanes x 16 B
-    static_assert(WG <= 128, "a window is one 16-byte load per lane");
+    constexpr int WG = WIN * CW;                // granules per window
+    constexpr int G = kGroup;                   // steps per group
+    constexpr int GD = G * CW + 1;              // input dwords per lane per group (+1: alignbyte carry)
+    constexpr bool kGroupStore = DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TCA8;
+    static_assert(C == 4 || !kGroupStore, "RGBA8 group stores take 4-pixel chunks");
+    static_assert(WG <= 128, "a window is two 8-byte granules per lane");
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
-    static_assert(R >= 2 && R - 2 <= 63, "vmcnt range");
-#ifdef ZPX_PNG_LDS_RING
-    __shared__ __attribute__((aligned(16))) uint8_t lds[R * kSlot];
-    const uint32_t lds_ring = __builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t *)lds)));
-    const uint8_t *ring_p = lds;
-#endif
 
     const int lane = threadIdx.x;
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
@@ -445,22 +446,19 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         const bool dep0 = (__ballot(dep) & 1ull) != 0;
 
         // band input: one descriptor based at the dword below the band's
-        // first byte; its extent covers the band's rows plus 64 bytes (the
-        // next band, the next pass or ZPX_PNG_INPUT_PAD is always behind them)
+        // first byte; its extent covers the band's rows plus ZPX_PNG_INPUT_PAD
+        // bytes (the next band, the next pass or the pad is always behind
+        // them), so a 16-byte load holding a row's last bytes is never cut by
+        // the range check; loads wholly past it read zeros
         const uint8_t *band0 = ps.filtered + static_cast<size_t>(bd.band) * 64 * (rb + 1);
         const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
         const uint32_t delta = static_cast<uint32_t>(band0 - base4);
-        const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + 64;
+        const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
         const uint32_t nrec = extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent);
         const Rsrc rsrc = make_rsrc(base4, nrec);
         const uint32_t row_off = delta + static_cast<uint32_t>(lane) * (rb + 1); // filter byte of my row
         const uint32_t mis = (row_off + 1) & 3;
         const int data_off = static_cast<int>(row_off + 1 - mis); // dword holding my row's first data byte
-        // Every DMA stays inside the descriptor: offsets are clamped rather than
-        // left to the range check (chunks before a row's start, or past the
-        // band's data, are never consumed, so any in-range bytes will do).
-        const int max_off = static_cast<int>((nrec - 16u) & ~3u);
-        auto chunk_off = [&](int k) { return k >= 0 ? min(data_off + k * CW * 4, max_off) : 0; };
 
         const bool has_prev = bd.band > 0;
         const bool has_next = bd.band + 1 < ps.nbands;
@@ -468,18 +466,20 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         const uint64_t *prev_bnd =
             boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) * band_granules;
         uint64_t *my_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band) * band_granules;
-        // window starting at chunk w0: lane l < WG/2 holds granules 2l, 2l+1
-        auto window_ptr = [&](int w0) { return prev_bnd + (2 * lane < WG ? w0 * CW + 2 * lane : 0); };
         // the current window is staged in LDS (one 16-byte write per lane) and
-        // read back at a wave-uniform address: per-step polling then waits on
-        // lgkmcnt only, never on the ring's outstanding vector loads
+        // read back at a wave-uniform address: per-step polling waits on
+        // lgkmcnt only, never on the input loads in flight
         auto fill_window = [&](int w0) {
-            const u32x4 v = load_window_sync(window_ptr(w0));
+            const u32x4 v = load_window(prev_bnd + (2 * lane < WG ? w0 * CW + 2 * lane : 0));
             if (2 * lane < WG) reinterpret_cast<u32x4 *>(win_lds)[lane] = v;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
+
+        // RGBA8 group stores: contiguous rows (xf == 1), 16-byte aligned
+        const bool gstore = kGroupStore && ps.xf == 1 && ((reinterpret_cast<uintptr_t>(ps.out) | ps.out_stride) & 15) == 0;
+        gu8 *out_row = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
 
         uint32_t left[BPP], ul[BPP];
 #pragma unroll
@@ -489,30 +489,16 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         for (int i = 0; i < CW; i++) outp[i] = 0;
         int maxidx = 0;
 
-        // prologue: the ring (slot r = step r)
-#ifdef ZPX_PNG_LDS_RING
+        // One group: G steps from step0 over this lane's chunks k0 .. k0+G-1
+        // (k0 = step0 - skew), input dwords in `in`.
+        auto run_group = [&](const uint32_t (&in)[GD], int step0) {
+            uint32_t gw[kGroupStore ? G : 1][4];
 #pragma unroll
-        for (int r = 0; r < R; r++) dma16<false, true>(lds_ring + r * kSlot, rsrc, chunk_off(r - skew));
-#else
-        // CW dwords per slot: a dword the step never reads would be a dead
-        // register the compiler reuses at once, forcing a vmcnt(0) (WAW)
-        typename ChunkVec<CW>::T ring[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) ring[r] = load_chunk<CW>(rsrc, chunk_off(r - skew));
-#endif
-
-        const int nsteps = nchunks + max_skew;
-        for (int step0 = 0; step0 < nsteps; step0 += R) {
-#pragma unroll
-            for (int r = 0; r < R; r++) {
+            for (int r = 0; r < G; r++) {
                 const int step = step0 + r;
-                if (step >= nsteps) break;
+                if (step >= nsteps_of(nchunks, max_skew)) break;
                 const int k = step - skew;
                 const bool act = row_ok && k >= 0 && k < nchunks;
-                // ring slots r and r+1 have landed (R-2 DMAs were issued after slot r+1's)
-#ifdef ZPX_PNG_LDS_RING
-                wait_vm<R - 2>();
-#endif
 
                 // ---- the row above: chunk k of row y-1 was produced by lane-1 one step ago
                 uint32_t up[CW];
@@ -530,29 +516,15 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     auto chunk_ready = [&](int c) {
                         bool ok = true;
 #pragma unroll
-                        for (int i = 0; i < CW; i++) {
-                            const int gi = c * CW + i;
-                            const uint32_t tag = static_cast<uint32_t>(win_lds[gi] >> 32);
-                            ok &= tag == epoch;
-                        }
+                        for (int i = 0; i < CW; i++) ok &= static_cast<uint32_t>(win_lds[c * CW + i] >> 32) == epoch;
                         return ok;
                     };
                     uint32_t spins = 0;
                     for (;;) {
                         // this chunk's granules (publication order is not visibility
                         // order), and at a window's start also its last chunk
-                        const bool ready = chunk_ready(wi) && (wi != 0 || chunk_ready(last));
-                        if (ready) break;
+                        if (chunk_ready(wi) && (wi != 0 || chunk_ready(last))) break;
                         if (++spins > kSpinLimit) {
-#ifdef ZPX_PNG_DEBUG
-                            if (!timed_out && lane == 0)
-                                printf("png timeout: pass %u band %u step %d wi %d last %d nchunks %d epoch %u "
-                                       "tag(wi)=%u tag(last)=%u ptr=%p\n",
-                                       bd.pass, bd.band, step, wi, last, nchunks, epoch,
-                                       static_cast<uint32_t>(win_lds[wi * CW] >> 32),
-                                       static_cast<uint32_t>(win_lds[last * CW] >> 32),
-                                       (const void *)window_ptr(step - wi));
-#endif
                             timed_out = true;
                             break;
                         }
@@ -561,10 +533,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     }
                     uint32_t gv[CW];
 #pragma unroll
-                    for (int i = 0; i < CW; i++) {
-                        const int gi = wi * CW + i;
-                        gv[i] = static_cast<uint32_t>(win_lds[gi]);
-                    }
+                    for (int i = 0; i < CW; i++) gv[i] = static_cast<uint32_t>(win_lds[wi * CW + i]);
                     if (lane == 0) {
 #pragma unroll
                         for (int i = 0; i < CW; i++) up[i] = gv[i];
@@ -574,21 +543,10 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     for (int i = 0; i < CW; i++) up[i] = 0; // first row of a pass: zero previous row (:790-793)
                 }
 
-                // ---- filtered bytes of chunk k: slot r + the first dword of slot r+1
-                // (every lane computes; only active lanes store)
-#ifdef ZPX_PNG_LDS_RING
-                const u32x4 cur = *reinterpret_cast<const u32x4 *>(ring_p + r * kSlot + lane * 16);
-                const uint32_t nxt = *reinterpret_cast<const uint32_t *>(ring_p + ((r + 1) % R) * kSlot + lane * 16);
-#else
-                const auto cur = ring[r];
-                const uint32_t nxt = ring[(r + 1) % R][0];
-#endif
+                // ---- filtered bytes of chunk k (every lane computes; only active lanes store)
                 uint32_t f[CW];
 #pragma unroll
-                for (int i = 0; i < CW; i++) {
-                    const uint32_t hi = i + 1 < CW ? cur[i + 1] : nxt;
-                    f[i] = __builtin_amdgcn_alignbyte(hi, cur[i], mis);
-                }
+                for (int i = 0; i < CW; i++) f[i] = __builtin_amdgcn_alignbyte(in[r * CW + i + 1], in[r * CW + i], mis);
                 if (k == 0) {
 #pragma unroll
                     for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
@@ -611,15 +569,11 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 }
 #pragma unroll
                 for (int i = 0; i < CW; i++) outp[i] = ob[i];
-                // refill slot r with the chunk R steps ahead (slot r was read above)
-#ifdef ZPX_PNG_LDS_RING
-                dma16<false>(lds_ring + r * kSlot, rsrc, chunk_off(k + R));
-#else
-                ring[r] = load_chunk<CW>(rsrc, chunk_off(k + R));
-#endif
 
+                if constexpr (kGroupStore) pack_rgba4<DEPTH, CW>(ps, ob, gw[r]);
                 if (act) {
-                    store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
+                    const bool full = static_cast<uint32_t>(k + 1) * C <= ps.width;
+                    if (!(gstore && full)) store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
                     if (has_next && lane == 63) { // publish: the data is the flag
                         uint64_t *d = my_bnd + static_cast<size_t>(k) * CW;
 #pragma unroll
@@ -627,10 +581,49 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     }
                 }
             }
+            if constexpr (kGroupStore) {
+                if (gstore) { // the group's full chunks, one contiguous burst per lane
+#pragma unroll
+                    for (int r = 0; r < G; r++) {
+                        const int k = step0 + r - skew;
+                        if (step0 + r < nsteps_of(nchunks, max_skew) && row_ok && k >= 0 && k < nchunks &&
+                            static_cast<uint32_t>(k + 1) * C <= ps.width)
+                            gcast<gv4>(out_row + static_cast<size_t>(k) * 16)[0] = gv4{gw[r][0], gw[r][1], gw[r][2], gw[r][3]};
+                    }
+                }
+            }
+        };
+
+        // groups alternate between two input buffers: the loads of group g+1
+        // are issued before group g runs (no register copies of loads in flight)
+        const int nsteps = nsteps_of(nchunks, max_skew);
+        // a group's burst starts before the row for a lane still in its skew
+        // (k0 < 0): a 16-byte load at a negative offset reads as zeros whole,
+        // so such groups (the first max_skew/G) load dword by dword
+        auto load_group = [&](uint32_t (&b)[GD], int step0) {
+            const int off = data_off + (step0 - skew) * CB;
+            if (__ballot(off < 0) != 0) {
+#pragma unroll
+                for (int i = 0; i < GD; i++) {
+                    // the range check does not wrap voffset + the instruction's
+                    // immediate offset: a negative base with a folded +4i reads
+                    // zero even where the sum is in range, so select per dword
+                    const int o = off + 4 * i;
+                    b[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
+                }
+            } else {
+                load_dwords<GD>(b, rsrc, off);
+            }
+        };
+        uint32_t bufA[GD], bufB[GD];
+        load_group(bufA, 0);
+        for (int step0 = 0; step0 < nsteps; step0 += 2 * G) {
+            load_group(bufB, step0 + G);
+            run_group(bufA, step0);
+            if (step0 + G >= nsteps) break;
+            load_group(bufA, step0 + 2 * G);
+            run_group(bufB, step0 + G);
         }
-#ifdef ZPX_PNG_LDS_RING
-        wait_vm<0>(); // the ring's last DMAs land before the next band reuses the slots
-#endif
         if constexpr (DEPTH >= ZPX_PNG_P1 && DEPTH <= ZPX_PNG_P8) {
             for (int off = 32; off > 0; off >>= 1) maxidx = max(maxidx, __shfl_xor(maxidx, off));
             if (lane == 0 && ps.max_index) atomicMax(ps.max_index, maxidx);

@@ -10,7 +10,7 @@ from . import _lib, context
 from .image import Image
 
 PNG_SIGNATURE = b"\x89PNG\r\n\x1a\n"
-INPUT_PAD = 64  # ZPX_PNG_INPUT_PAD
+INPUT_PAD = 256  # ZPX_PNG_INPUT_PAD
 # zpx_png_depth (ColorBitDepth, src/png/decoder.zig:88-118)
 DEPTHS = {"g1": 1, "g2": 2, "g4": 3, "g8": 4, "ga8": 5, "tc8": 6, "p1": 7, "p2": 8, "p4": 9, "p8": 10,
           "tca8": 11, "g16": 12, "ga16": 13, "tc16": 14, "tca16": 15}
