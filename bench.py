@@ -48,6 +48,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
     ap.add_argument("--gather", action="store_true", help="RCCL-gather all RGBA outputs to rank 0 (timed apart)")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end streaming line (host entropy threads + H2D + kernels)")
+    ap.add_argument("--e2e-images", type=int, default=16, help="encoded images in the end-to-end batch")
+    ap.add_argument("--host-threads", type=int, default=16, help="host entropy/inflate threads (end-to-end)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/)")
     return ap.parse_args()
@@ -145,6 +151,93 @@ def cpu_baseline_jpeg(data: bytes, seconds: float):
     return {"value": round(multi, 2), "unit": "MPixels/sec", "cores": cores, "kind": "port",
             "sample": f"{cores * per_thread + 1} x oracle jpeg.decode+rgbaPixels of one 4096x4096 q75 4:2:0 frame "
                       f"({tm + t1:.1f}s)", "single_core_mpix_s": round(single, 2)}
+
+
+def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
+    """configs[4]: 4096^2 progressive 4:4:4 JPEG (fused kernel, 786,432 blocks
+    per frame) and 4096^2 Adam7 RGBA16 PNG (7 passes scattered into NRGBA64),
+    each as a resident batch of `images` slots; parity of slot 0 vs the oracle."""
+    import numpy as np
+    import oracle_py as O
+
+    W = H = args.size
+    out = {}
+    d = S.jpeg_progressive_444(1000 + rank, W, H, args.quality)
+    t0 = time.perf_counter()
+    co = jpeg.Coefficients(d)
+    t_ent = time.perf_counter() - t0
+    jb = device.JpegBatch([co], slots=[0] * args.images, output="rgba", ctx=ctx)
+    if rank == 0:
+        jb.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = O.jpeg_decode(d).rgba_pixels()
+        if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want)):
+            raise SystemExit("parity failure: progressive 4:4:4 JPEG != oracle")
+    steps = max(3, args.steps // 2)
+    wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, 1, ws)
+    out["jpeg_progressive_444"] = {
+        "value": round(jb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
+        "kernel_ms_per_launch": round(kern_ms, 3),
+        "roofline": {"bound": "hbm", "achieved": round(jb.bytes / (kern_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(jb.bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                     "algorithmic_bytes_per_launch": jb.bytes},
+        "host_entropy_mpix_s": round(W * H / t_ent / 1e6, 1),
+        "config": {"workload": f"{args.images}x {W}x{H} progressive 4:4:4 JPEG -> RGBA, configs[4]"}}
+    del jb
+    pd = S.png_rgba16_adam7(2000 + rank, W, H)
+    t0 = time.perf_counter()
+    st = png.Stream(pd)
+    t_inf = time.perf_counter() - t0
+    pb = device.PngBatch([st], slots=[0] * args.images, ctx=ctx)
+    if rank == 0:
+        pb.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = O.png_decode(pd).pixels
+        got = pb.output_tensor(0).cpu().numpy()
+        if not np.array_equal(got.reshape(-1)[:want.size], want.reshape(-1)):
+            raise SystemExit("parity failure: Adam7 RGBA16 PNG != oracle")
+    wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, 1, ws)
+    out["png_adam7_rgba16"] = {
+        "value": round(pb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
+        "kernel_ms_per_launch": round(kern_ms, 3),
+        "roofline": {"bound": "hbm", "achieved": round(pb.bytes / (kern_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(pb.bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                     "algorithmic_bytes_per_launch": pb.bytes},
+        "host_inflate_mpix_s": round(W * H / t_inf / 1e6, 1),
+        "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64, configs[4]"}}
+    del pb
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_e2e(args, torch, dist, ws, rank, ctx, S):
+    """End to end, from encoded bytes in host memory: zpx_batch_decode_rgba
+    with a pool of host entropy/inflate threads overlapped with pinned H2D
+    copies and the kernels, RGBA8 into device memory (configs[3]'s per-GPU
+    shard: alternating 4096^2 JPEG 4:2:0 and tc8 PNG).  Never `value`."""
+    from zpix_amd import batch
+
+    W = H = args.size
+    mine = shard_images(args.e2e_images * ws, rank, ws)
+    uniq = {0: S.jpeg_420(0, W, H, args.quality), 1: S.png_tc8_mixed(1, W, H)}
+    bufs = [uniq[i % 2] for i in mine]
+    batch.decode_rgba(bufs[:2], host_threads=args.host_threads, ctx=ctx)  # warm-up (pools, code objects)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res, st = batch.decode_rgba(bufs, host_threads=args.host_threads, ctx=ctx, with_stats=True)
+    torch.cuda.synchronize()
+    wall = max_over_ranks(dist, time.perf_counter() - t0, "cuda")
+    bad = [r.status for r in res if r.status != "Ok"]
+    if bad:
+        raise SystemExit(f"end-to-end batch failed: {bad[:3]}")
+    return {"value": round(len(bufs) * ws * W * H / wall / 1e6, 1), "unit": "MPixels/sec",
+            "images_per_gpu": len(bufs), "host_threads": st.host_threads, "depth": st.depth,
+            "wall_s": round(wall, 3), "host_cpu_s": round(st.host_s, 3),
+            "h2d_gb": round(st.h2d_bytes / 1e9, 3),
+            "config": {"workload": f"{len(bufs)}x {W}x{H} alternating JPEG 4:2:0 / tc8 PNG, encoded bytes in host "
+                                   "memory -> RGBA8 in HBM (zpx_batch_decode_rgba), configs[3] shard"}}
 
 
 def main():
@@ -287,6 +380,11 @@ def main():
             result = dict(pres, n_gpus=ws, warmup=1, higher_is_better=True, scaling="weak", vs_baseline=None,
                           dtype="u8", data="synthetic PNG")
         del pb
+    # ------------------------------------------------------------ configs[4] and end to end
+    if not args.no_config5 and not args.png_only:
+        result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)
+    if not args.no_e2e and not args.png_only:
+        result["end_to_end"] = bench_e2e(args, torch, dist, ws, rank, ctx, S)
     # ------------------------------------------------------------ CPU baseline (rank 0, N=1)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.png_only:
         result["cpu_baseline"] = cpu_baseline_jpeg(datas[0], args.cpu_seconds)

@@ -5,7 +5,7 @@
 set -u
 ROOTDIR=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOTDIR/gpurun_out/pmc
-ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --distinct 1 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --distinct 1 --no-cpu-baseline --no-config5 --no-e2e"}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 run() {
