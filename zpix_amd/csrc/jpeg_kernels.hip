@@ -10,6 +10,8 @@
 // stage is a dense contraction.  The kernels are HBM-bound streaming passes.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 
 #include "device_types.h"
@@ -309,7 +311,10 @@ __device__ __forceinline__ void unpack_dequant(const RowRegs<CoefT> &r, const in
 }
 
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
-__global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames, int strips_x,
+#ifndef ZPX_JPEG_WAVES_PER_EU
+#define ZPX_JPEG_WAVES_PER_EU 5
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JPEG_WAVES_PER_EU))) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames, int strips_x,
                                                              int strips_per_frame, int total_strips)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
@@ -335,7 +340,9 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
 
     __shared__ int32_t qs_all[NG][3][64];
     __shared__ __attribute__((aligned(16))) int32_t buf_all[NG][NB * kBlkStride]; // row pass, then RGBA tile
-    __shared__ int32_t ctile_all[NG][kGray ? 1 : 2][CROWS * CPX];
+    // chroma samples are clamped to 0..255: bytes keep the workgroup's LDS
+    // at ~31 KiB, so 5 workgroups (20 waves) fit a CU instead of 4
+    __shared__ uint8_t ctile_all[NG][kGray ? 1 : 2][CROWS * CPX];
 
     const int tid = threadIdx.x % G, group = threadIdx.x / G;
     auto (&qs) = qs_all[group];
@@ -470,9 +477,9 @@ __global__ __launch_bounds__(kThreads) void jpeg_rgba_kernel(const DevJpegFrame 
                 for (int i = 0; i < 8; i++) s[i] = buf[blk * kBlkStride + i * 8 + c];
                 idct_col_clamp<NARROW>(s);
                 const bool present = comp == 1 ? cb_present : cr_present; // never scanned: samples 0
-                int32_t *t = ctile[comp - 1] + ((kk / CW) * 8) * CPX + (kk % CW) * 8 + c;
+                uint8_t *t = ctile[comp - 1] + ((kk / CW) * 8) * CPX + (kk % CW) * 8 + c;
 #pragma unroll
-                for (int i = 0; i < 8; i++) t[i * CPX] = present ? s[i] : 0;
+                for (int i = 0; i < 8; i++) t[i * CPX] = static_cast<uint8_t>(present ? s[i] : 0);
             }
             group_sync<G>();
         }
@@ -605,14 +612,30 @@ int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, i
 }
 
 namespace {
-int persistent_workgroups()
+int cu_count()
 {
     static int n = 0;
     if (n == 0) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess)
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        n = cus * 4; // 4 resident 256-thread workgroups per CU (LDS ~37 KiB each)
+        n = cus;
+    }
+    return n;
+}
+
+// Resident workgroups per CU for one kernel instance: the occupancy API
+// (registers + LDS), capped by ZPX_JPEG_WG_PER_CU when set (A/B runs).
+template <typename K>
+int persistent_workgroups(K kernel)
+{
+    static int n = 0;
+    if (n == 0) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu < 1)
+            per_cu = 4;
+        if (const char *e = getenv("ZPX_JPEG_WG_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+        n = cu_count() * per_cu;
     }
     return n;
 }
@@ -627,9 +650,10 @@ void launch_rgba_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int 
     const int per_frame = strips_x * max_myy;
     const int total = per_frame * n_frames;
     const int groups_needed = (total + NG - 1) / NG;
-    const int grid = groups_needed < persistent_workgroups() ? groups_needed : persistent_workgroups();
-    hipLaunchKernelGGL((jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>), dim3(grid), dim3(kThreads), 0,
-                       stream, d_frames, strips_x, per_frame, total);
+    auto kernel = jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>;
+    const int resident = persistent_workgroups(kernel);
+    const int grid = groups_needed < resident ? groups_needed : resident;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, stream, d_frames, strips_x, per_frame, total);
 }
 
 template <typename CoefT, bool NARROW, int COLOR>
