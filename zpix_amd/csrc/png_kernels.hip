@@ -372,15 +372,23 @@ __device__ __forceinline__ u32x4 load_window(const uint64_t *p)
                  static_cast<uint32_t>(b >> 32)};
 }
 
-// RGBA8 output words of one chunk of 4 pixels (TC8 -> RGBA / NRGBA with the
-// tRNS colour key, TCA8 -> NRGBA raw), as store_chunk's contiguous path.
-template <int DEPTH, int CW>
-__device__ __forceinline__ void pack_rgba4(const DevPngPass &ps, const uint32_t (&ob)[CW], uint32_t (&w)[4])
+// Depths whose contiguous store of one chunk is exactly 16 bytes of the
+// output image (store_chunk's fast path): Gray/indices 8 (16 px), Gray16
+// (8 px), RGB8 -> RGBA8/NRGBA8 (4 px), RGBA8 (4 px), RGB16 -> RGBA64 /
+// NRGBA64 (2 px), RGBA16 (2 px).
+template <int DEPTH>
+constexpr bool group_store_depth()
 {
-    if constexpr (DEPTH == ZPX_PNG_TCA8) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) w[u] = ob[u];
-    } else {
+    return DEPTH == ZPX_PNG_G8 || DEPTH == ZPX_PNG_P8 || DEPTH == ZPX_PNG_G16 || DEPTH == ZPX_PNG_TC8 ||
+           DEPTH == ZPX_PNG_TCA8 || DEPTH == ZPX_PNG_TC16 || DEPTH == ZPX_PNG_TCA16;
+}
+
+// The 16 output bytes of one whole chunk, as store_chunk writes them
+// (readImagePass :947-950, :963-968, :994-1015, :1033-1039, :1062-1078).
+template <int DEPTH, int CW>
+__device__ __forceinline__ void pack_chunk16(const DevPngPass &ps, const uint32_t (&ob)[CW], uint32_t (&w)[4])
+{
+    if constexpr (DEPTH == ZPX_PNG_TC8) { // RGBA (or NRGBA with the colour key)
         const bool trns = ps.use_trns != 0;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -389,6 +397,25 @@ __device__ __forceinline__ void pack_rgba4(const DevPngPass &ps, const uint32_t 
             if (trns && r == ps.trns[1] && g == ps.trns[3] && b == ps.trns[5]) a = 0;
             w[u] = r | g << 8 | b << 16 | a << 24;
         }
+    } else if constexpr (DEPTH == ZPX_PNG_TC16) { // RGBA64 / NRGBA64, big-endian channels
+        const bool trns = ps.use_trns != 0;
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int b0 = 6 * u;
+            const uint32_t r = byte_of(ob, b0) | byte_of(ob, b0 + 1) << 8;
+            const uint32_t g = byte_of(ob, b0 + 2) | byte_of(ob, b0 + 3) << 8;
+            const uint32_t b = byte_of(ob, b0 + 4) | byte_of(ob, b0 + 5) << 8;
+            uint32_t a = 0xffff;
+            if (trns && r == (uint32_t(ps.trns[0]) | uint32_t(ps.trns[1]) << 8) &&
+                g == (uint32_t(ps.trns[2]) | uint32_t(ps.trns[3]) << 8) &&
+                b == (uint32_t(ps.trns[4]) | uint32_t(ps.trns[5]) << 8))
+                a = 0;
+            w[2 * u] = r | g << 16;
+            w[2 * u + 1] = b | a << 16;
+        }
+    } else { // the chunk's bytes are the output bytes (G8, P8, G16 BE, TCA8, TCA16)
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = ob[i];
     }
 }
 
@@ -404,8 +431,8 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     constexpr int WG = WIN * CW;                // granules per window
     constexpr int G = kGroup;                   // steps per group
     constexpr int GD = G * CW + 1;              // input dwords per lane per group (+1: alignbyte carry)
-    constexpr bool kGroupStore = DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TCA8;
-    static_assert(C == 4 || !kGroupStore, "RGBA8 group stores take 4-pixel chunks");
+    constexpr bool kGroupStore = group_store_depth<DEPTH>();
+    static_assert(!kGroupStore || CW == 4 || DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TC16, "16-byte output chunks");
     static_assert(WG <= 128, "a window is two 8-byte granules per lane");
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
 
@@ -477,8 +504,11 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
 
-        // RGBA8 group stores: contiguous rows (xf == 1), 16-byte aligned
-        const bool gstore = kGroupStore && ps.xf == 1 && ((reinterpret_cast<uintptr_t>(ps.out) | ps.out_stride) & 15) == 0;
+        // group stores: contiguous rows (xf == 1), 16-byte aligned, and an
+        // output type a colour key does not change (Gray8/16 + tRNS -> NRGBA)
+        constexpr bool kKeyWidens = DEPTH == ZPX_PNG_G8 || DEPTH == ZPX_PNG_G16;
+        const bool gstore = kGroupStore && ps.xf == 1 && !(kKeyWidens && ps.use_trns) &&
+                            ((reinterpret_cast<uintptr_t>(ps.out) | ps.out_stride) & 15) == 0;
         gu8 *out_row = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
 
         uint32_t left[BPP], ul[BPP];
@@ -570,10 +600,15 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
 #pragma unroll
                 for (int i = 0; i < CW; i++) outp[i] = ob[i];
 
-                if constexpr (kGroupStore) pack_rgba4<DEPTH, CW>(ps, ob, gw[r]);
+                if constexpr (kGroupStore) pack_chunk16<DEPTH, CW>(ps, ob, gw[r]);
                 if (act) {
                     const bool full = static_cast<uint32_t>(k + 1) * C <= ps.width;
-                    if (!(gstore && full)) store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
+                    if (!(gstore && full)) {
+                        store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
+                    } else if constexpr (DEPTH == ZPX_PNG_P8) { // palette growth (:1079-1134)
+#pragma unroll
+                        for (int i = 0; i < 16; i++) maxidx = max(maxidx, static_cast<int>(byte_of(ob, i)));
+                    }
                     if (has_next && lane == 63) { // publish: the data is the flag
                         uint64_t *d = my_bnd + static_cast<size_t>(k) * CW;
 #pragma unroll
