@@ -284,7 +284,7 @@ typedef struct zpx_jpeg_frame {
     int32_t h[4], v[4];      /* sampling factors after processSof (decoder.zig:490-618) */
     int32_t mxx, myy;        /* MCU grid (decoder.zig:1262-1263) */
     int32_t rule[4];         /* zpx_block_rule per component */
-    int32_t coeff_bits;      /* 16 or 32 */
+    int32_t coeff_bits;      /* 8, 16 or 32: int8 / int16 / int32 grids (the narrowest that holds the frame) */
     int32_t narrow;          /* 1 if max|coef*q| <= 16384 for every component */
     int32_t color;           /* zpx_jpeg_color (fused output only) */
     const void *coeffs[4];   /* DEVICE: (mxx*h) x (myy*v) blocks, 64 natural-order coefs each */
@@ -351,6 +351,11 @@ int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **ou
 int zpx_jpeg_coeffs_frame(const zpx_jpeg_coeffs *c, zpx_jpeg_frame *frame,
                           size_t *coeff_bytes_per_comp /* [4] */);
 void zpx_jpeg_coeffs_free(zpx_jpeg_coeffs *c);
+/* Widens every grid to at least `bits` (16 or 32) coefficient bits.  The
+ * entropy stage keeps the narrowest width that holds the frame (8, 16 or 32:
+ * zpx_jpeg_frame.coeff_bits); a caller that wants one fixed transport format
+ * (or an A/B of the transports) widens here. */
+int zpx_jpeg_coeffs_widen(zpx_jpeg_coeffs *c, int bits);
 
 typedef struct zpx_png_stream zpx_png_stream;
 /* Host half of png.decode: chunk parse + CRC + inflate into pinned memory. */

@@ -101,6 +101,25 @@ def test_host_entropy_matches_oracle(path):
             assert np.array_equal(np.array(f.qt[c][:]), nat)
 
 
+@pytest.mark.parametrize("path", JPEGS, ids=os.path.basename)
+def test_host_coefficient_width_is_narrowest(path):
+    """The frame's coefficient grids share the narrowest of int8/int16/int32
+    that holds every coefficient of every component."""
+    data = open(path, "rb").read()
+    try:
+        oc = O.jpeg_coefficients(data)
+    except O.OracleError:
+        return
+    m = max(int(np.abs(g).max()) for g in oc.grids if g is not None)
+    want = 8 if m <= 127 else 16 if m <= 32767 else 32
+    pc = J.Coefficients(data)
+    assert pc.frame.coeff_bits == want
+    for c in range(oc.n_comp):
+        if oc.grids[c] is not None:
+            assert pc.grid(c).dtype == {8: np.int8, 16: np.int16, 32: np.int32}[want]
+            assert pc.coeff_bytes[c] == oc.grids[c].size * want // 8
+
+
 def _jpeg_err_product(data):
     try:
         J.Coefficients(data)

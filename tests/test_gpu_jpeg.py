@@ -120,10 +120,10 @@ def _run_planar_grids(grids, qts, h, v, mxx, myy, width, height, rule, coeff_bit
     f.coeff_bits, f.narrow, f.color = coeff_bits, narrow, 0
     keep = []
     planes = []
-    dt = torch.int16 if coeff_bits == 16 else torch.int32
+    npt = {8: np.int8, 16: np.int16, 32: np.int32}[coeff_bits]
     for c in range(n_comp):
         f.h[c], f.v[c], f.rule[c] = h[c], v[c], rule
-        g = torch.from_numpy(np.ascontiguousarray(grids[c]).astype(np.int16 if coeff_bits == 16 else np.int32)).to("cuda")
+        g = torch.from_numpy(np.ascontiguousarray(grids[c]).astype(npt)).to("cuda")
         keep.append(g)
         f.coeffs[c] = g.data_ptr()
         for i in range(64):
@@ -150,6 +150,7 @@ UNZIG = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19
 
 @pytest.mark.parametrize("coeff_bits,scale,narrow,rule", [
     (16, 64, 1, 0), (16, 2000, 0, 0), (32, 1 << 20, 0, 0), (32, 1 << 27, 0, 1), (16, 300, 1, 2),
+    (8, 128, 1, 0), (8, 128, 0, 1), (8, 128, 1, 2),
 ])
 def test_planar_kernel_random_grids(coeff_bits, scale, narrow, rule):
     """Random (incl. overflowing) coefficient grids: wrap-around i32 IDCT,
@@ -159,7 +160,8 @@ def test_planar_kernel_random_grids(coeff_bits, scale, narrow, rule):
     grids, qz = [], []
     for c in range(3):
         nb = mxx * h[c] * myy * v[c]
-        g = rng.integers(-scale, scale, (nb, 64)) if coeff_bits == 32 else rng.integers(-min(scale, 32767), min(scale, 32767), (nb, 64))
+        lim = {8: 128, 16: 32767, 32: scale}[coeff_bits]
+        g = rng.integers(-min(scale, lim), min(scale, lim), (nb, 64))
         sparse = rng.random((nb, 64)) < 0.7
         g[sparse] = 0
         g[rng.random(nb) < 0.2, 1:] = 0  # DC-only blocks
@@ -194,14 +196,25 @@ def test_jpeg_batch_4k_fused_matches_oracle():
     """The bench workload (4096^2 4:2:0, q75) for one frame, slot-replicated."""
     data = S.jpeg_420(0, 4096, 4096)
     co = J.Coefficients(data)
-    assert co.frame.narrow == 1 and co.frame.coeff_bits == 16
+    # the bench content fits int8 coefficients (max |coef| 75), so this is the
+    # int8 transport the bench measures
+    assert co.frame.narrow == 1 and co.frame.coeff_bits == 8
     batch = device.JpegBatch([co], slots=[0, 0], output="rgba")
     batch.launch(torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     want = O.jpeg_decode(data).rgba_pixels().reshape(4096, 4096, 4)
     for s in range(2):
         assert torch.equal(batch.output_tensor(s).cpu(), torch.from_numpy(want))
-    assert batch.bytes == 2 * (393216 * 128 + 4096 * 4096 * 4 + 3 * 256)
+    assert batch.bytes == 2 * (393216 * 64 + 4096 * 4096 * 4 + 3 * 256)
+    # the same frame through the int16 transport (bench's int16_transport line)
+    del batch
+    co.widen(16)
+    assert co.frame.coeff_bits == 16
+    batch = device.JpegBatch([co], slots=[0], output="rgba")
+    batch.launch(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(batch.output_tensor(0).cpu(), torch.from_numpy(want))
+    assert batch.bytes == 393216 * 128 + 4096 * 4096 * 4 + 3 * 256
 
 
 def test_jpeg_batch_planes_matches_oracle():

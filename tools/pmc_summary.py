@@ -35,6 +35,10 @@ if len(sys.argv) > 2 and "jpeg_rgba" in out:
           "fetch_bytes_per_launch": 2 * j["FETCH_SIZE"] * 1024, "write_bytes_per_launch": j["WRITE_SIZE"] * 1024,
           "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, KiB -> B, mean per dispatch"}
     tr["hbm_bytes_per_launch"] = tr["fetch_bytes_per_launch"] + tr["write_bytes_per_launch"]
+    try:  # the coefficient transport the passes ran with (bench config)
+        tr["coeff_bits"] = json.load(open(os.path.join(base, "fetch.json")))["config"]["coeff_bits"]
+    except Exception:
+        tr["coeff_bits"] = 16
     if "png_unfilter" in out:
         p = out["png_unfilter"]
         tr["png_unfilter"] = {"fetch_bytes_per_launch": 2 * p["FETCH_SIZE"] * 1024,

@@ -129,30 +129,37 @@ void HostBuf::release()
 bool CoeffGrid::init(size_t blocks)
 {
     blocks_ = blocks;
-    wide_ = false;
+    bits_ = 8;
     max_abs_ = 0;
-    return buf_.alloc(blocks * 64 * sizeof(int16_t), true);
+    return buf_.alloc(blocks * 64 * sizeof(int8_t), true);
 }
 
 void CoeffGrid::load(size_t blk, int32_t *b) const
 {
-    if (wide_) {
+    if (bits_ == 32) {
         memcpy(b, static_cast<const int32_t *>(buf_.ptr) + blk * 64, 64 * sizeof(int32_t));
-    } else {
+    } else if (bits_ == 16) {
         const int16_t *s = static_cast<const int16_t *>(buf_.ptr) + blk * 64;
+        for (int i = 0; i < 64; i++) b[i] = s[i];
+    } else {
+        const int8_t *s = static_cast<const int8_t *>(buf_.ptr) + blk * 64;
         for (int i = 0; i < 64; i++) b[i] = s[i];
     }
 }
 
-bool CoeffGrid::widen()
+bool CoeffGrid::widen_to(int bits)
 {
+    if (bits <= bits_) return true;
     HostBuf nb;
-    if (!nb.alloc(blocks_ * 64 * sizeof(int32_t), false)) return false;
-    const int16_t *s = static_cast<const int16_t *>(buf_.ptr);
-    int32_t *d = static_cast<int32_t *>(nb.ptr);
-    for (size_t i = 0; i < blocks_ * 64; i++) d[i] = s[i];
+    const size_t n = blocks_ * 64;
+    if (!nb.alloc(n * (bits / 8), false)) return false;
+    for (size_t i = 0; i < n; i++) {
+        const int32_t v = bits_ == 8 ? static_cast<const int8_t *>(buf_.ptr)[i] : static_cast<const int16_t *>(buf_.ptr)[i];
+        if (bits == 16) static_cast<int16_t *>(nb.ptr)[i] = static_cast<int16_t>(v);
+        else static_cast<int32_t *>(nb.ptr)[i] = v;
+    }
     buf_ = static_cast<HostBuf &&>(nb);
-    wide_ = true;
+    bits_ = bits;
     return true;
 }
 
@@ -164,12 +171,16 @@ bool CoeffGrid::store(size_t blk, const int32_t *b)
         if (a > m || a < 0) m = (a < 0) ? INT32_MAX : a;
     }
     max_abs_ = m;
-    if (!wide_ && m > 32767 && !widen()) return false;
-    if (wide_) {
+    const int need = m > 32767 ? 32 : m > 127 ? 16 : 8;
+    if (need > bits_ && !widen_to(need)) return false;
+    if (bits_ == 32) {
         memcpy(static_cast<int32_t *>(buf_.ptr) + blk * 64, b, 64 * sizeof(int32_t));
-    } else {
+    } else if (bits_ == 16) {
         int16_t *d = static_cast<int16_t *>(buf_.ptr) + blk * 64;
         for (int i = 0; i < 64; i++) d[i] = static_cast<int16_t>(b[i]);
+    } else {
+        int8_t *d = static_cast<int8_t *>(buf_.ptr) + blk * 64;
+        for (int i = 0; i < 64; i++) d[i] = static_cast<int8_t>(b[i]);
     }
     return true;
 }
@@ -842,7 +853,14 @@ int Decoder::run()
 int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out)
 {
     Decoder d(buf, len, out);
-    return d.run();
+    if (int e = d.run()) return e;
+    // one width per frame (the kernels take one coefficient type per frame)
+    int bits = 8;
+    for (int i = 0; i < 4; i++)
+        if (out.has_grid[i]) bits = std::max(bits, out.grid[i].bits());
+    for (int i = 0; i < 4; i++)
+        if (out.has_grid[i] && !out.grid[i].widen_to(bits)) return ZPX_E_OUT_OF_MEMORY;
+    return ZPX_OK;
 }
 
 int jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h, int &model)

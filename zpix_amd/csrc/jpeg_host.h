@@ -39,22 +39,26 @@ struct JpegComponent {
 
 class CoeffGrid {
   public:
-    // Blocks of 64 natural-order coefficients, stored as int16 while every
-    // value fits, widened to int32 the first time one does not.
+    // Blocks of 64 natural-order coefficients, stored in the narrowest of
+    // int8 / int16 / int32 that holds every value so far: a grid starts as
+    // int8 and is widened (copied) the first time a value does not fit.
+    // Conforming 8-bit streams never need int32; the bench's q75 frames fit
+    // int8, natural photos usually need int16 (iceberg.jpg: max |AC| 157).
     bool init(size_t blocks);
-    bool wide() const { return wide_; }
+    int bits() const { return bits_; }
+    bool wide() const { return bits_ == 32; }
     size_t blocks() const { return blocks_; }
     const void *data() const { return buf_.ptr; }
-    size_t bytes() const { return buf_.bytes; }
+    size_t bytes() const { return blocks_ * 64 * (bits_ / 8); }
     void load(size_t blk, int32_t *b) const;
     bool store(size_t blk, const int32_t *b); // false only on allocation failure
+    bool widen_to(int bits);                  // no-op when already that wide
     int32_t max_abs() const { return max_abs_; }
 
   private:
-    bool widen();
     HostBuf buf_;
     size_t blocks_ = 0;
-    bool wide_ = false;
+    int bits_ = 8;
     int32_t max_abs_ = 0;
 };
 
@@ -76,6 +80,8 @@ struct JpegCoeffs {
 
 // Decode `buf` into coefficient grids.  Returns ZPX_E_* (ZPX_E_OK on success),
 // with the reference's error for malformed input.
+// Host entropy stage; on success every grid of the frame has the same
+// coefficient width (the widest any grid needed).
 int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out);
 
 // jpeg.decodeConfig (decoder.zig:178-218): markers up to SOF (JFIF) or SOS,

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include <cstdint>
 
@@ -143,7 +144,12 @@ template <typename CoefT>
 __device__ __forceinline__ void load_row(const CoefT *__restrict__ p, const int32_t *__restrict__ q,
                                          int32_t s[8])
 {
-    if constexpr (sizeof(CoefT) == 2) {
+    if constexpr (sizeof(CoefT) == 1) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(p);
+        const uint32_t w[2] = {v.x, v.y};
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = static_cast<int32_t>(w[i >> 2] << (24 - 8 * (i & 3))) >> 24;
+    } else if constexpr (sizeof(CoefT) == 2) {
         const uint4 v = *reinterpret_cast<const uint4 *>(p);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -157,11 +163,11 @@ __device__ __forceinline__ void load_row(const CoefT *__restrict__ p, const int3
         s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
         s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
     }
-    // coefficients fit in 16 bits for the int16 transport and q in 17 bits,
-    // so the 24-bit multiply is exact there
+    // coefficients fit in 16 bits for the int8/int16 transports and q in 17
+    // bits, so the 24-bit multiply is exact there
 #pragma unroll
     for (int i = 0; i < 8; i++)
-        s[i] = (sizeof(CoefT) == 2) ? __mul24(s[i], q[i]) : s[i] * q[i];
+        s[i] = (sizeof(CoefT) <= 2) ? __mul24(s[i], q[i]) : s[i] * q[i];
 }
 
 __device__ __forceinline__ bool block_in_rule(int rule, int bx, int by, int hh, int vv, int W, int H)
@@ -267,29 +273,41 @@ __device__ __forceinline__ void group_sync()
     }
 }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// One coefficient row, raw (not yet dequantized): 8 B (int8), 16 B (int16)
+// or 32 B (int32).
 template <typename CoefT>
-struct RowRegs { // one coefficient row, raw (not yet dequantized)
-    u32x4 a;
+struct RowRegs {
+    using A = typename std::conditional<sizeof(CoefT) == 1, u32x2, u32x4>::type;
+    A a;
     u32x4 b; // int32 coefficients only
 };
 
 template <typename CoefT>
 __device__ __forceinline__ void load_row_raw(const CoefT *p, RowRegs<CoefT> &r)
 {
-    const ZPX_GLOBAL u32x4 *g = (const ZPX_GLOBAL u32x4 *)p;
+    using A = typename RowRegs<CoefT>::A;
+    const ZPX_GLOBAL A *g = (const ZPX_GLOBAL A *)p;
 #if ZPX_COEF_NT
     r.a = __builtin_nontemporal_load(g);
-    if constexpr (sizeof(CoefT) == 4) r.b = __builtin_nontemporal_load(g + 1);
+    if constexpr (sizeof(CoefT) == 4) r.b = __builtin_nontemporal_load((const ZPX_GLOBAL u32x4 *)p + 1);
 #else
     r.a = g[0];
-    if constexpr (sizeof(CoefT) == 4) r.b = g[1];
+    if constexpr (sizeof(CoefT) == 4) r.b = ((const ZPX_GLOBAL u32x4 *)p)[1];
 #endif
 }
 
 template <typename CoefT>
 __device__ __forceinline__ void unpack_dequant(const RowRegs<CoefT> &r, const int32_t *__restrict__ q, int32_t s[8])
 {
-    if constexpr (sizeof(CoefT) == 2) {
+    if constexpr (sizeof(CoefT) == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = static_cast<int32_t>(r.a[i >> 2] << (24 - 8 * (i & 3))) >> 24;
+        // |coef| < 2^7 and q < 2^17: the 24-bit multiply is exact
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = __mul24(s[i], q[i]);
+    } else if constexpr (sizeof(CoefT) == 2) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t w = r.a[i];
@@ -598,10 +616,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
 // launchers
 // ---------------------------------------------------------------------------
 int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh,
-                       bool wide_coeffs, bool narrow, hipStream_t stream)
+                       int coeff_bits, bool narrow, hipStream_t stream)
 {
     dim3 grid((max_gw + 31) / 32, max_gh, n_frames * 4);
-    if (wide_coeffs) {
+    if (coeff_bits == 8) {
+        if (narrow) hipLaunchKernelGGL((jpeg_planar_kernel<int8_t, true>), grid, dim3(kThreads), 0, stream, d_frames);
+        else hipLaunchKernelGGL((jpeg_planar_kernel<int8_t, false>), grid, dim3(kThreads), 0, stream, d_frames);
+    } else if (coeff_bits == 32) {
         if (narrow) hipLaunchKernelGGL((jpeg_planar_kernel<int32_t, true>), grid, dim3(kThreads), 0, stream, d_frames);
         else hipLaunchKernelGGL((jpeg_planar_kernel<int32_t, false>), grid, dim3(kThreads), 0, stream, d_frames);
     } else {
@@ -703,11 +724,14 @@ bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc)
 }
 
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc,
-                     int vc, int max_mxx, int max_myy, bool wide_coeffs, bool narrow, hipStream_t stream)
+                     int vc, int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream)
 {
     const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
     int rc;
-    if (wide_coeffs)
+    if (coeff_bits == 8)
+        rc = narrow ? dispatch_color<int8_t, true>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
+                    : dispatch_color<int8_t, false>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
+    else if (coeff_bits == 32)
         rc = narrow ? dispatch_color<int32_t, true>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
                     : dispatch_color<int32_t, false>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
     else

@@ -11,11 +11,12 @@
 namespace zpx {
 
 // jpeg_kernels.hip
-int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh, bool wide_coeffs,
+// coeff_bits: 8, 16 or 32 (int8 / int16 / int32 coefficient grids)
+int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh, int coeff_bits,
                        bool narrow, hipStream_t stream);
 bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc);
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
-                     int max_mxx, int max_myy, bool wide_coeffs, bool narrow, hipStream_t stream);
+                     int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream);
 
 // png_kernels.hip
 int png_chunk_bytes(int depth);

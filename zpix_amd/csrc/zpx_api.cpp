@@ -208,12 +208,13 @@ int zpx::launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_f
     const int color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
     const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
     const int hc = f.n_comp == 3 ? f.h[1] : 1, vc = f.n_comp == 3 ? f.v[1] : 1;
-    return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits == 32, f.narrow != 0, st);
+    return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits, f.narrow != 0, st);
 }
 struct JpegGroup {
     DevBuf frames;
     int n = 0;
-    bool wide = false, narrow = true;
+    int bits = 16;
+    bool narrow = true;
     int color = 0, h0 = 1, v0 = 1, hc = 1, vc = 1;
     int max_gw = 0, max_gh = 0, max_mxx = 0, max_myy = 0;
 };
@@ -247,7 +248,7 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
     for (int i = 0; i < n_frames; i++) {
         const zpx_jpeg_frame &f = frames[i];
         if (f.n_comp != 1 && f.n_comp != 3 && f.n_comp != 4) return ZPX_E_INVALID_ARGUMENT;
-        if (f.coeff_bits != 16 && f.coeff_bits != 32) return ZPX_E_INVALID_ARGUMENT;
+        if (f.coeff_bits != 8 && f.coeff_bits != 16 && f.coeff_bits != 32) return ZPX_E_INVALID_ARGUMENT;
         int color = 0, hc = 1, vc = 1;
         if (output == ZPX_JPEG_RGBA) {
             color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
@@ -270,7 +271,7 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
     uint64_t bytes = 0;
     for (auto &kv : groups) {
         std::unique_ptr<JpegGroup> g(new JpegGroup);
-        g->wide = std::get<0>(kv.first) == 32;
+        g->bits = std::get<0>(kv.first);
         g->narrow = std::get<1>(kv.first) != 0;
         g->color = std::get<2>(kv.first);
         g->h0 = std::get<3>(kv.first);
@@ -447,10 +448,10 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
     for (auto &g : plan->jpeg) {
         int rc;
         if (plan->kind == 0)
-            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->max_gw, g->max_gh, g->wide, g->narrow, st);
+            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->max_gw, g->max_gh, g->bits, g->narrow, st);
         else
             rc = launch_jpeg_rgba(g->frames.as<DevJpegFrame>(), g->n, g->color, g->h0, g->v0, g->hc, g->vc,
-                                  g->max_mxx, g->max_myy, g->wide, g->narrow, st);
+                                  g->max_mxx, g->max_myy, g->bits, g->narrow, st);
         if (rc == -2) return ZPX_E_UNSUPPORTED;
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
@@ -514,7 +515,7 @@ void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_
     f->n_comp = c.n_comp;
     f->mxx = c.mxx;
     f->myy = c.myy;
-    bool wide = false;
+    int bits = 8;
     int64_t m = 0;
     for (int i = 0; i < c.n_comp; i++) {
         f->h[i] = c.comp[i].h;
@@ -522,11 +523,11 @@ void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_
         f->rule[i] = c.rule[i];
         memcpy(f->qt[i], c.qt_natural[i], sizeof(f->qt[i]));
         if (c.has_grid[i]) {
-            wide |= c.grid[i].wide();
+            bits = std::max(bits, c.grid[i].bits());
             m = std::max<int64_t>(m, int64_t(c.grid[i].max_abs()) * c.max_q[i]);
         }
     }
-    f->coeff_bits = wide ? 32 : 16;
+    f->coeff_bits = bits;
     f->narrow = m <= 16384 ? 1 : 0;
     switch (jpeg_output_kind(c)) {
     case JpegOut::Gray: f->color = ZPX_JPEG_COLOR_GRAY; break;
@@ -536,7 +537,7 @@ void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_
     for (int i = 0; i < 4; i++) {
         const bool g = i < c.n_comp && c.has_grid[i];
         f->coeffs[i] = g ? c.grid[i].data() : nullptr;
-        if (coeff_bytes) coeff_bytes[i] = g ? c.grid[i].blocks() * 64 * (wide ? 4 : 2) : 0;
+        if (coeff_bytes) coeff_bytes[i] = g ? c.grid[i].blocks() * 64 * (bits / 8) : 0;
     }
 }
 
@@ -548,6 +549,14 @@ extern "C" int zpx_jpeg_coeffs_frame(const zpx_jpeg_coeffs *cc, zpx_jpeg_frame *
 }
 
 extern "C" void zpx_jpeg_coeffs_free(zpx_jpeg_coeffs *c) { delete c; }
+
+extern "C" int zpx_jpeg_coeffs_widen(zpx_jpeg_coeffs *cc, int bits)
+{
+    if (!cc || (bits != 8 && bits != 16 && bits != 32)) return ZPX_E_INVALID_ARGUMENT;
+    for (int i = 0; i < 4; i++)
+        if (cc->c.has_grid[i] && !cc->c.grid[i].widen_to(bits)) return ZPX_E_OUT_OF_MEMORY;
+    return ZPX_OK;
+}
 
 extern "C" int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out)
 {

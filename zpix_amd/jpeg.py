@@ -88,14 +88,22 @@ class Coefficients:
         self.coeff_bytes = [int(s) for s in sizes]
 
     def grid(self, comp: int) -> np.ndarray:
-        """Coefficient grid of a component as (blocks, 64) int16/int32 (host view)."""
+        """Coefficient grid of a component as (blocks, 64) int8/int16/int32 (host view; the
+        frame's `coeff_bits` is the narrowest width that holds every coefficient)."""
         ptr = self.frame.coeffs[comp]
         if not ptr:
             return None
-        dt = np.int16 if self.frame.coeff_bits == 16 else np.int32
-        n = self.coeff_bytes[comp] // np.dtype(dt).itemsize
-        return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int16 if dt == np.int16 else C.c_int32)),
-                                     shape=(n,)).reshape(-1, 64)
+        ct = {8: C.c_int8, 16: C.c_int16, 32: C.c_int32}[self.frame.coeff_bits]
+        n = self.coeff_bytes[comp] // C.sizeof(ct)
+        return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).reshape(-1, 64)
+
+    def widen(self, bits: int) -> "Coefficients":
+        """Widen every grid to at least `bits` (16 or 32) coefficient bits."""
+        _lib.check(_lib.lib().zpx_jpeg_coeffs_widen(self.handle, bits))
+        sizes = (C.c_size_t * 4)()
+        _lib.check(_lib.lib().zpx_jpeg_coeffs_frame(self.handle, C.byref(self.frame), sizes))
+        self.coeff_bytes = [int(s) for s in sizes]
+        return self
 
     def close(self):
         if self.handle:
