@@ -8,6 +8,7 @@ OUT=$ROOTDIR/gpurun_out/pmc
 ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --distinct 1 --no-cpu-baseline --no-config5 --no-e2e"}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
+export ZPX_BENCH_NO_INT16=1 # one kernel instance per pass (mean per dispatch)
 run() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $OUT/$name -o run -- \
