@@ -185,6 +185,33 @@ bool CoeffGrid::store(size_t blk, const int32_t *b)
     return true;
 }
 
+bool CoeffGrid::store_sparse(size_t blk, const int32_t *b, const uint8_t *pos, int n)
+{
+    int32_t m = max_abs_;
+    for (int i = 0; i < n; i++) {
+        const int32_t v = b[pos[i]];
+        int32_t a = v < 0 ? -v : v;
+        if (a > m || a < 0) m = (a < 0) ? INT32_MAX : a;
+    }
+    max_abs_ = m;
+    const int need = m > 32767 ? 32 : m > 127 ? 16 : 8;
+    if (need > bits_ && !widen_to(need)) return false;
+    if (bits_ == 8) {
+        int8_t *d = static_cast<int8_t *>(buf_.ptr) + blk * 64;
+        memset(d, 0, 64);
+        for (int i = 0; i < n; i++) d[pos[i]] = static_cast<int8_t>(b[pos[i]]);
+    } else if (bits_ == 16) {
+        int16_t *d = static_cast<int16_t *>(buf_.ptr) + blk * 64;
+        memset(d, 0, 128);
+        for (int i = 0; i < n; i++) d[pos[i]] = static_cast<int16_t>(b[pos[i]]);
+    } else {
+        int32_t *d = static_cast<int32_t *>(buf_.ptr) + blk * 64;
+        memset(d, 0, 256);
+        for (int i = 0; i < n; i++) d[pos[i]] = b[pos[i]];
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- decoder
 namespace {
 
@@ -327,6 +354,21 @@ class Decoder {
                 bm_ >>= nb;
                 out = static_cast<uint8_t>(lv >> 8);
                 return 0;
+            }
+            // a code longer than 8 bits: resolve it from the bits already
+            // buffered when they suffice -- exactly the bit loop below
+            // (code after i+1 bits = the top i+1 buffered bits), without
+            // reading a byte the loop would not have read
+            for (int i = 8; i < 16 && i < bn_; i++) {
+                const int32_t code = static_cast<int32_t>((ba_ >> (bn_ - (i + 1))) & ((1u << (i + 1)) - 1));
+                if (code <= h.max_codes[i]) {
+                    const int32_t idx = h.vals_indices[i] + code - h.min_codes[i];
+                    if (idx < 0 || idx > 255) return ZPX_E_PANIC;
+                    bn_ -= i + 1;
+                    bm_ >>= i + 1;
+                    out = h.vals[idx];
+                    return 0;
+                }
             }
         }
         int32_t code = 0;
@@ -668,6 +710,8 @@ int Decoder::sos(int32_t n)
     uint8_t expected_rst = 0xd0;
     int32_t dc[4] = {0, 0, 0, 0};
     int32_t b[64];
+    uint8_t nzpos[64];
+    memset(b, 0, sizeof(b));
     const bool prog = o_.progressive;
     for (int32_t my = 0; my < myy; my++) {
         for (int32_t mx = 0; mx < mxx; mx++) {
@@ -691,8 +735,10 @@ int Decoder::sos(int32_t n)
                             continue;
                     }
                     const size_t blk = size_t(by) * size_t(mxx * hi) + size_t(bx);
+                    // baseline: b stays all-zero between blocks; the positions a
+                    // block writes are recorded and cleared after its store
+                    int nnz = 0;
                     if (prog) g.load(blk, b);
-                    else memset(b, 0, sizeof(b));
                     if (ah != 0) {
                         ZTRY(refine(b, hac, zs, ze, int32_t(1) << al));
                     } else {
@@ -706,6 +752,7 @@ int Decoder::sos(int32_t n)
                             ZTRY(receive_extend(t, delta));
                             dc[ci] += delta;
                             b[0] = dc[ci] << al;
+                            nzpos[nnz++] = 0;
                         }
                         if (zig <= ze && eob_run_ > 0) {
                             eob_run_--;
@@ -720,6 +767,7 @@ int Decoder::sos(int32_t n)
                                     int32_t ac;
                                     ZTRY(receive_extend(v1, ac));
                                     b[kUnzig[zig]] = ac << al;
+                                    nzpos[nnz++] = kUnzig[zig];
                                 } else {
                                     if (v0r != 0x0f) {
                                         eob_run_ = static_cast<uint16_t>(1u << v0r);
@@ -736,7 +784,12 @@ int Decoder::sos(int32_t n)
                             }
                         }
                     }
-                    if (!g.store(blk, b)) return ZPX_E_OUT_OF_MEMORY;
+                    if (prog) {
+                        if (!g.store(blk, b)) return ZPX_E_OUT_OF_MEMORY;
+                    } else {
+                        if (!g.store_sparse(blk, b, nzpos, nnz)) return ZPX_E_OUT_OF_MEMORY;
+                        for (int i = 0; i < nnz; i++) b[nzpos[i]] = 0;
+                    }
                 }
             }
             mcu++;

@@ -52,6 +52,9 @@ class CoeffGrid {
     size_t bytes() const { return blocks_ * 64 * (bits_ / 8); }
     void load(size_t blk, int32_t *b) const;
     bool store(size_t blk, const int32_t *b); // false only on allocation failure
+    // Baseline fast path: the block is zero except at the n natural-order
+    // positions pos[] (all distinct).
+    bool store_sparse(size_t blk, const int32_t *b, const uint8_t *pos, int n);
     bool widen_to(int bits);                  // no-op when already that wide
     int32_t max_abs() const { return max_abs_; }
 
