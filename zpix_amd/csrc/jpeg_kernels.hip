@@ -534,28 +534,40 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
                     cb = ctile[0][ci];
                     cr = ctile[1][ci];
                 }
+                // colour.zig:95-106 chroma terms, once per chroma sample (RY rows)
+                const int32_t cb1 = cb - 128, cr1 = cr - 128;
+                const int32_t t_r = __mul24(91881, cr1);
+                const int32_t t_g = -(__mul24(22554, cb1) + __mul24(46802, cr1));
+                const int32_t t_b = __mul24(116130, cb1);
 #pragma unroll
                 for (int j = 0; j < RY; j++) {
                     const int i = i0 + j;
                     const int32_t Yv = yv[it][i];
                     uint32_t pix;
+#ifdef ZPX_JPEG_NO_COLOR // timing-only build: luma as gray, no colour math
+                    if constexpr (true) {
+#else
                     if constexpr (kGray) {
+#endif
                         pix = static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
                     } else if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
                         pix = static_cast<uint32_t>(Yv) | static_cast<uint32_t>(cb) << 8 |
                               static_cast<uint32_t>(cr) << 16 | 0xff000000u;
                     } else {
                         // color.zig:95-106; 8-bit result of (v>>8 or clamp)>>8 == clamp(v, 0, 2^24-1)>>16
-                        // (clamp before the shift: see ycc_rgba8 in color_kernels.hip)
-                        const int32_t yy1 = __mul24(Yv, 0x10101);
-                        const int32_t cb1 = cb - 128, cr1 = cr - 128;
-                        const int32_t r = yy1 + __mul24(91881, cr1);
-                        const int32_t g = yy1 - __mul24(22554, cb1) - __mul24(46802, cr1);
-                        const int32_t b = yy1 + __mul24(116130, cb1);
-                        const uint32_t R = static_cast<uint32_t>(min(max(r, 0), 0xffffff)) >> 16;
-                        const uint32_t G = static_cast<uint32_t>(min(max(g, 0), 0xffffff)) >> 16;
-                        const uint32_t B = static_cast<uint32_t>(min(max(b, 0), 0xffffff)) >> 16;
-                        pix = R | G << 8 | B << 16 | 0xff000000u;
+                        // (clamp before the shift: see ycc_rgba8 in color_kernels.hip).
+                        // Per pixel: 3 v_mad_i32_i24, 3 v_med3_i32, and two v_perm_b32
+                        // that take byte 2 of each clamped channel (= its >>16).
+                        const int32_t r = __mul24(Yv, 0x10101) + t_r;
+                        const int32_t g = __mul24(Yv, 0x10101) + t_g;
+                        const int32_t b = __mul24(Yv, 0x10101) + t_b;
+                        const uint32_t rc = static_cast<uint32_t>(min(max(r, 0), 0xffffff));
+                        const uint32_t gc = static_cast<uint32_t>(min(max(g, 0), 0xffffff));
+                        const uint32_t bc = static_cast<uint32_t>(min(max(b, 0), 0xffffff));
+                        // {R, G, 0x00, 0xff}: bytes rc.2, gc.2, zero, 0xff
+                        const uint32_t rg = __builtin_amdgcn_perm(gc, rc, 0x0d0c0602u);
+                        // {R, G, B, 0xff}
+                        pix = __builtin_amdgcn_perm(bc, rg, 0x03060100u);
                     }
                     o[i * PXW] = pix;
                 }
