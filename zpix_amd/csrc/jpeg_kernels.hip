@@ -253,7 +253,10 @@ typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 constexpr int kGroup = ZPX_JPEG_GROUP;
 static_assert(kGroup == 64 || kGroup == kThreads, "a strip group is one wave or the workgroup");
 // about 96 blocks per 256 threads (3 coefficient rows per lane)
-constexpr int kStripBlocks = 96 * kGroup / kThreads;
+#ifndef ZPX_JPEG_STRIP_BLOCKS
+#define ZPX_JPEG_STRIP_BLOCKS 96
+#endif
+constexpr int kStripBlocks = ZPX_JPEG_STRIP_BLOCKS * kGroup / kThreads;
 constexpr int strip_mcus(int blocks_per_mcu)
 {
     return blocks_per_mcu >= kStripBlocks ? 1 : kStripBlocks / blocks_per_mcu;
