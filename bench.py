@@ -330,7 +330,14 @@ def main():
             a16 = batch.bytes / (k16 * 1e-3) / 1e9
             int16 = {"kernel_ms_per_launch": round(k16, 4), "algorithmic_bytes_per_launch": batch.bytes,
                      "mpix_s_kernel_only": round(batch.pixels * ws / (k16 * 1e-3) / 1e6, 1),
-                     "achieved": round(a16, 1), "frac": round(a16 / PEAK_HBM_GBS, 4)}
+                     "achieved": round(a16, 1), "frac": round(a16 / PEAK_HBM_GBS, 4), "traffic": None}
+            t16 = os.path.join(os.path.dirname(args.traffic_json), "traffic_int16.json")
+            try:
+                tj16 = json.load(open(t16))
+                if tj16.get("images") == args.images and tj16.get("size") == args.size:
+                    int16["traffic"] = tj16.get("hbm_bytes_per_launch")
+            except Exception:
+                pass
         result = {
             "metric": "MPixels/sec decoded (4K baseline JPEG 4:2:0) at 1/8 GPU; % HBM roofline",
             "value": round(value, 1),
