@@ -52,7 +52,8 @@ def parse():
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end streaming line (host entropy threads + H2D + kernels)")
-    ap.add_argument("--e2e-images", type=int, default=16, help="encoded images in the end-to-end batch")
+    ap.add_argument("--e2e-images", type=int, default=64,
+                    help="encoded images per GPU in the end-to-end batch (configs[3]: 512 over 8 GPUs)")
     ap.add_argument("--host-threads", type=int, default=16, help="host entropy/inflate threads (end-to-end)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/)")
