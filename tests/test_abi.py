@@ -259,3 +259,68 @@ def test_png_decode_config():
     with pytest.raises(zpix_amd.ZpixError) as e:
         P.decode_config(b"\x89PNX\r\n\x1a\n" + b"\x00" * 30)
     assert e.value.name == "InvalidPngHeader"
+
+
+def _png_with_stream(w, h, z):
+    """A gray8 PNG whose IDAT is the given zlib stream (split in 3 chunks)."""
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    ihdr = struct.pack(">IIBBBBB", w, h, 8, 0, 0, 0, 0)
+    k = max(1, len(z) // 3)
+    idats = b"".join(chunk(b"IDAT", z[i:i + k]) for i in range(0, len(z), k))
+    return b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + idats + chunk(b"IEND", b"")
+
+
+@pytest.mark.parametrize("level,strategy", [(0, zlib.Z_DEFAULT_STRATEGY), (1, zlib.Z_DEFAULT_STRATEGY),
+                                            (6, zlib.Z_DEFAULT_STRATEGY), (9, zlib.Z_DEFAULT_STRATEGY),
+                                            (6, zlib.Z_FILTERED), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE),
+                                            (6, zlib.Z_FIXED)])
+def test_inflate_matches_zlib(level, strategy):
+    """The host inflate (fast decoder, zlib fallback) gives zlib's bytes for
+    stored, fixed and dynamic blocks, long matches and every strategy; and
+    truncated / corrupted streams keep zlib's error names."""
+    rng = np.random.default_rng(level * 10 + strategy)
+    w, h = 333, 97
+    rows = []
+    for y in range(h):  # filter-type byte 0 + mixed noise / runs / repeats
+        kind = y % 3
+        if kind == 0:
+            r = rng.integers(0, 256, w, dtype=np.uint8)
+        elif kind == 1:
+            r = np.repeat(rng.integers(0, 256, w // 37 + 1, dtype=np.uint8), 37)[:w]
+        else:
+            r = np.tile(rng.integers(0, 256, 7, dtype=np.uint8), w // 7 + 1)[:w]
+        rows.append(b"\x00" + r.tobytes())
+    raw = b"".join(rows)
+    co = zlib.compressobj(level, zlib.DEFLATED, 15, 8, strategy)
+    z = co.compress(raw) + co.flush()
+    st = P.Stream(_png_with_stream(w, h, z))
+    assert np.array_equal(st.filtered()[:st.filtered_len], np.frombuffer(raw, np.uint8))
+    # truncation and corruption: the same error name as the oracle (zlib)
+    for cut in (len(z) // 2, len(z) - 5):
+        bad = _png_with_stream(w, h, z[:cut])
+        try:
+            O.png_decode(bad)
+            want = "OK"
+        except O.OracleError as e:
+            want = e.name
+        try:
+            P.Stream(bad)
+            got = "OK"
+        except _lib.ZpixError as e:
+            got = e.name
+        assert got == want, (cut, got, want)
+    for k in range(6):
+        b = bytearray(z)
+        b[int(rng.integers(2, len(b)))] ^= int(rng.integers(1, 256))
+        bad = _png_with_stream(w, h, bytes(b))
+        try:
+            want = O.png_decode(bad).pixels.tobytes()[:0] or "OK"
+        except O.OracleError as e:
+            want = e.name
+        try:
+            P.Stream(bad)
+            got = "OK"
+        except _lib.ZpixError as e:
+            got = e.name
+        assert got == want, (k, got, want)

@@ -6,6 +6,8 @@
 // bytes are identical).
 #include "png_host.h"
 
+#include "inflate_fast.h"
+
 #include <zlib.h>
 
 #include <cstring>
@@ -38,6 +40,35 @@ int bits_of(int depth)
     return 0;
 }
 bool paletted(int d) { return d >= ZPX_PNG_P1 && d <= ZPX_PNG_P8; }
+
+// System zlib over the whole stream: `produced` bytes written before it
+// stopped; `data_error` when it stopped on corrupt data (vs. running out).
+int inflate_zlib(const std::vector<uint8_t> &z, uint8_t *dst, size_t total, size_t &produced, bool &data_error)
+{
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    if (inflateInit(&zs) != Z_OK) return ZPX_E_OUT_OF_MEMORY;
+    zs.next_in = const_cast<Bytef *>(z.data());
+    zs.avail_in = static_cast<uInt>(z.size());
+    produced = 0;
+    data_error = false;
+    while (produced < total) {
+        const size_t want = total - produced;
+        zs.next_out = dst + produced;
+        zs.avail_out = static_cast<uInt>(want > (1u << 30) ? (1u << 30) : want);
+        const uInt before = zs.avail_out;
+        const int r = inflate(&zs, Z_NO_FLUSH);
+        produced += before - zs.avail_out;
+        if (r == Z_STREAM_END) break;
+        if (r == Z_OK) continue;
+        if (r == Z_BUF_ERROR && zs.avail_in == 0) break; // truncated stream
+        if (r == Z_BUF_ERROR) continue;
+        data_error = true;
+        break;
+    }
+    inflateEnd(&zs);
+    return ZPX_OK;
+}
 
 class Parser {
   public:
@@ -224,30 +255,17 @@ int Parser::decode_image(const std::vector<uint8_t> &z)
     if (!o_.data.alloc(total + ZPX_PNG_INPUT_PAD, false)) return ZPX_E_OUT_OF_MEMORY;
     memset(static_cast<uint8_t *>(o_.data.ptr) + total, 0, ZPX_PNG_INPUT_PAD);
 
-    // inflate exactly the bytes the passes read (std.compress.flate .zlib)
-    z_stream zs;
-    memset(&zs, 0, sizeof(zs));
-    if (inflateInit(&zs) != Z_OK) return ZPX_E_OUT_OF_MEMORY;
-    zs.next_in = const_cast<Bytef *>(z.data());
-    zs.avail_in = static_cast<uInt>(z.size());
+    // inflate exactly the bytes the passes read (std.compress.flate .zlib):
+    // the fast decoder when the stream decodes cleanly, else system zlib from
+    // the start (whose error behaviour the rest of this function maps)
+    uint8_t *dst = static_cast<uint8_t *>(o_.data.ptr);
     size_t produced = 0;
     bool data_error = false;
-    uint8_t *dst = static_cast<uint8_t *>(o_.data.ptr);
-    while (produced < total) {
-        const size_t want = total - produced;
-        zs.next_out = dst + produced;
-        zs.avail_out = static_cast<uInt>(want > (1u << 30) ? (1u << 30) : want);
-        const uInt before = zs.avail_out;
-        const int r = inflate(&zs, Z_NO_FLUSH);
-        produced += before - zs.avail_out;
-        if (r == Z_STREAM_END) break;
-        if (r == Z_OK) continue;
-        if (r == Z_BUF_ERROR && zs.avail_in == 0) break; // truncated stream
-        if (r == Z_BUF_ERROR) continue;
-        data_error = true;
-        break;
+    if (!inflate_fast(z.data(), z.size(), dst, total, &produced)) {
+        produced = 0;
+        if (int e = inflate_zlib(z, dst, total, produced, data_error)) return e;
     }
-    inflateEnd(&zs);
+
 
     // rows in order: short data -> EndOfStream / ReadFailed, bad filter ->
     // InvalidFilterType (readImagePass :800, :839-841)
@@ -284,7 +302,16 @@ int Parser::decode_image(const std::vector<uint8_t> &z)
 int Parser::idat(uint32_t first_len)
 { // parseIdat :404-545
     std::vector<uint8_t> all;
-    all.reserve(first_len);
+    { // reserve the whole stream once: sum the run of IDAT chunk lengths
+      // ahead (a read-only scan; the loop below does the checks)
+        size_t total = first_len, p = pos_ + size_t(first_len) + 4;
+        while (p + 8 <= len_ && memcmp(src_ + p + 4, "IDAT", 4) == 0) {
+            const uint32_t n = be32(src_ + p);
+            total += n;
+            p += size_t(n) + 12;
+        }
+        all.reserve(total);
+    }
     auto take = [&](uint32_t n) -> int {
         if (len_ - pos_ < n) {
             pos_ = len_;
