@@ -6,6 +6,7 @@
 // bytes are identical).
 #include "png_host.h"
 
+#include "crc32_fast.h"
 #include "inflate_fast.h"
 
 #include <zlib.h>
@@ -89,7 +90,7 @@ class Parser {
     int read_crc(uint8_t *p, size_t n)
     {
         if (int e = read(p, n)) return e;
-        crc_ = static_cast<uint32_t>(crc32(crc_, p, static_cast<uInt>(n)));
+        crc_ = crc32_fast(crc_, p, n);
         return 0;
     }
     int verify()
@@ -104,7 +105,7 @@ class Parser {
             pos_ = len_;
             return ZPX_E_END_OF_STREAM;
         }
-        crc_ = static_cast<uint32_t>(crc32(crc_, src_ + pos_, static_cast<uInt>(n)));
+        crc_ = crc32_fast(crc_, src_ + pos_, n);
         pos_ += n;
         return 0;
     }
@@ -317,7 +318,7 @@ int Parser::idat(uint32_t first_len)
             pos_ = len_;
             return ZPX_E_END_OF_STREAM;
         }
-        crc_ = static_cast<uint32_t>(crc32(crc_, src_ + pos_, static_cast<uInt>(n)));
+        crc_ = crc32_fast(crc_, src_ + pos_, n);
         all.insert(all.end(), src_ + pos_, src_ + pos_ + n);
         pos_ += n;
         return 0;
