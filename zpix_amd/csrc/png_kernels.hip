@@ -389,13 +389,16 @@ template <int DEPTH, int CW>
 __device__ __forceinline__ void pack_chunk16(const DevPngPass &ps, const uint32_t (&ob)[CW], uint32_t (&w)[4])
 {
     if constexpr (DEPTH == ZPX_PNG_TC8) { // RGBA (or NRGBA with the colour key)
-        const bool trns = ps.use_trns != 0;
+        // 12 RGB bytes -> 4 RGBA words by byte selects (v_perm_b32), alpha 0xff
+        w[0] = __builtin_amdgcn_perm(ob[0], ob[0], 0x0c020100u) | 0xff000000u;
+        w[1] = __builtin_amdgcn_perm(ob[1], ob[0], 0x0c050403u) | 0xff000000u;
+        w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x0c040302u) | 0xff000000u;
+        w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0c030201u) | 0xff000000u;
+        if (ps.use_trns) { // wave-uniform: the colour key is per image
+            const uint32_t key = uint32_t(ps.trns[1]) | uint32_t(ps.trns[3]) << 8 | uint32_t(ps.trns[5]) << 16;
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t r = byte_of(ob, 3 * u), g = byte_of(ob, 3 * u + 1), b = byte_of(ob, 3 * u + 2);
-            uint32_t a = 0xff;
-            if (trns && r == ps.trns[1] && g == ps.trns[3] && b == ps.trns[5]) a = 0;
-            w[u] = r | g << 8 | b << 16 | a << 24;
+            for (int u = 0; u < 4; u++)
+                if ((w[u] & 0xffffffu) == key) w[u] &= 0xffffffu;
         }
     } else if constexpr (DEPTH == ZPX_PNG_TC16) { // RGBA64 / NRGBA64, big-endian channels
         const bool trns = ps.use_trns != 0;
