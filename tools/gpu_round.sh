@@ -27,5 +27,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 "$ROOTDIR/bench.py" --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" \
     || { echo "rocprof failed rc=$?"; tail -30 "$OUT/prof_bench.err"; exit 1; }
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
-cut -c1-200 "$OUT/kernel_stats.csv" | head -8
+find "$OUT/prof" -name '*kernel_trace.csv' -exec python3 "$ROOTDIR/tools/trace_stats.py" {} \; > "$OUT/kernel_by_launch.csv"
+cut -c1-200 "$OUT/kernel_by_launch.csv" | head -8
 echo gpu_round done
