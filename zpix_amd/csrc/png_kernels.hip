@@ -33,11 +33,19 @@
 namespace zpx {
 namespace {
 
-constexpr int kRegionChunks = 16;
+#ifndef ZPX_PNG_WIN
+#define ZPX_PNG_WIN 16
+#endif
+constexpr int kRegionChunks = ZPX_PNG_WIN;
 #ifndef ZPX_PNG_GROUP
 #define ZPX_PNG_GROUP 8
 #endif
 constexpr int kGroup = ZPX_PNG_GROUP; // steps per input/output burst
+#ifndef ZPX_PNG_LDS_OUT
+#define ZPX_PNG_LDS_OUT 1
+#endif
+constexpr bool kLdsOut = ZPX_PNG_LDS_OUT != 0; // output chunks staged in an LDS ring, flushed as aligned lines
+constexpr int kOutSlots = 17;                  // 16 ring slots + 1 of padding per lane
 #ifndef ZPX_PNG_SPIN_LIMIT
 #define ZPX_PNG_SPIN_LIMIT (1u << 20)
 #endif
@@ -85,6 +93,18 @@ typedef uint32_t gv2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gcast(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
 // Store n bytes held in dwords w[] to dst, using 16-byte stores when aligned.
+// Output stores: the image is written once and never re-read by this kernel,
+// so ZPX_PNG_NT_STORE marks them non-temporal (the L2 keeps the input lines
+// a row's next group re-reads).
+#ifndef ZPX_PNG_NT_STORE
+#define ZPX_PNG_NT_STORE 0
+#endif
+__device__ __forceinline__ void store16(ZPX_GLOBAL gv4 *p, gv4 v)
+{
+    if constexpr (ZPX_PNG_NT_STORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 template <int NB>
 __device__ __forceinline__ void store_bytes(gu8 *dst, const uint32_t (&w)[(NB + 3) / 4])
 {
@@ -93,7 +113,7 @@ __device__ __forceinline__ void store_bytes(gu8 *dst, const uint32_t (&w)[(NB + 
         if ((a & 15) == 0) {
 #pragma unroll
             for (int i = 0; i < NB / 16; i++)
-                gcast<gv4>(dst)[i] = gv4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+                store16(gcast<gv4>(dst) + i, gv4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]});
             return;
         }
     }
@@ -437,7 +457,10 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     constexpr bool kGroupStore = group_store_depth<DEPTH>();
     static_assert(!kGroupStore || CW == 4 || DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TC16, "16-byte output chunks");
     static_assert(WG <= 128, "a window is two 8-byte granules per lane");
+    static_assert(!kLdsOut || G == 8, "the output ring flushes 8-chunk blocks, 16 slots");
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
+    // output ring (kLdsOut): 16 chunks of 16 bytes per lane, +1 slot of padding
+    __shared__ gv4 out_lds[kLdsOut && kGroupStore ? 64 * kOutSlots : 1];
 
     const int lane = threadIdx.x;
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
@@ -521,11 +544,13 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
 #pragma unroll
         for (int i = 0; i < CW; i++) outp[i] = 0;
         int maxidx = 0;
+        int flushed = 0;                                     // chunks [0, flushed) of my row are in HBM
+        const int nfull = static_cast<int>(ps.width / C);    // chunks whose pixels are all inside the row
 
         // One group: G steps from step0 over this lane's chunks k0 .. k0+G-1
         // (k0 = step0 - skew), input dwords in `in`.
         auto run_group = [&](const uint32_t (&in)[GD], int step0) {
-            uint32_t gw[kGroupStore ? G : 1][4];
+            uint32_t gw[kGroupStore && !kLdsOut ? G : 1][4];
 #pragma unroll
             for (int r = 0; r < G; r++) {
                 const int step = step0 + r;
@@ -603,9 +628,17 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
 #pragma unroll
                 for (int i = 0; i < CW; i++) outp[i] = ob[i];
 
-                if constexpr (kGroupStore) pack_chunk16<DEPTH, CW>(ps, ob, gw[r]);
+                const bool full = k < nfull;
+                if constexpr (kGroupStore && kLdsOut) {
+                    if (gstore && act && full) {
+                        uint32_t w[4];
+                        pack_chunk16<DEPTH, CW>(ps, ob, w);
+                        out_lds[lane * kOutSlots + (k & 15)] = gv4{w[0], w[1], w[2], w[3]};
+                    }
+                } else if constexpr (kGroupStore) {
+                    pack_chunk16<DEPTH, CW>(ps, ob, gw[r]);
+                }
                 if (act) {
-                    const bool full = static_cast<uint32_t>(k + 1) * C <= ps.width;
                     if (!(gstore && full)) {
                         store_chunk<DEPTH>(ps, y, static_cast<uint32_t>(k * C), ob, maxidx);
                     } else if constexpr (DEPTH == ZPX_PNG_P8) { // palette growth (:1079-1134)
@@ -619,14 +652,31 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     }
                 }
             }
-            if constexpr (kGroupStore) {
+            if constexpr (kGroupStore && kLdsOut) {
+                // Flush whole aligned 8-chunk blocks (one 128-byte line of RGBA8)
+                // as soon as they are complete, and the row's tail at its end: a
+                // line is written whole by one lane in one burst, never in two
+                // halves a group apart.
+                if (gstore && row_ok) {
+                    const int done = min(step0 + G - skew, nchunks); // chunks [0, done) reconstructed
+                    const int upto = done == nchunks ? done : (done & ~7);
+                    const int hi = min(upto, nfull);
+                    int kf = flushed;
+#pragma unroll
+                    for (int i = 0; i < 8; i++, kf++)
+                        if (kf < hi) store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                    for (; kf < hi; kf++)
+                        store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                    flushed = max(flushed, upto);
+                }
+            } else if constexpr (kGroupStore) {
                 if (gstore) { // the group's full chunks, one contiguous burst per lane
 #pragma unroll
                     for (int r = 0; r < G; r++) {
                         const int k = step0 + r - skew;
                         if (step0 + r < nsteps_of(nchunks, max_skew) && row_ok && k >= 0 && k < nchunks &&
                             static_cast<uint32_t>(k + 1) * C <= ps.width)
-                            gcast<gv4>(out_row + static_cast<size_t>(k) * 16)[0] = gv4{gw[r][0], gw[r][1], gw[r][2], gw[r][3]};
+                            store16(gcast<gv4>(out_row + static_cast<size_t>(k) * 16), gv4{gw[r][0], gw[r][1], gw[r][2], gw[r][3]});
                     }
                 }
             }
