@@ -46,6 +46,14 @@ constexpr int kGroup = ZPX_PNG_GROUP; // steps per input/output burst
 #endif
 constexpr bool kLdsOut = ZPX_PNG_LDS_OUT != 0; // output chunks staged in an LDS ring, flushed as aligned lines
 constexpr int kOutSlots = 17;                  // 16 ring slots + 1 of padding per lane
+#ifndef ZPX_PNG_PAIR_LOADS
+#define ZPX_PNG_PAIR_LOADS 0
+#endif
+constexpr bool kPairLoads = ZPX_PNG_PAIR_LOADS != 0; // input bursts issued two groups at a time
+#ifndef ZPX_PNG_COOP_STORE
+#define ZPX_PNG_COOP_STORE 1
+#endif
+constexpr bool kCoopStore = ZPX_PNG_COOP_STORE != 0; // ring flush: 8 lanes per row, whole lines per store
 #ifndef ZPX_PNG_SPIN_LIMIT
 #define ZPX_PNG_SPIN_LIMIT (1u << 20)
 #endif
@@ -457,7 +465,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     constexpr bool kGroupStore = group_store_depth<DEPTH>();
     static_assert(!kGroupStore || CW == 4 || DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TC16, "16-byte output chunks");
     static_assert(WG <= 128, "a window is two 8-byte granules per lane");
-    static_assert(!kLdsOut || G == 8, "the output ring flushes 8-chunk blocks, 16 slots");
+    static_assert(!kLdsOut || G % 8 == 0, "the output ring flushes every 8 steps, 16 slots");
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
     // output ring (kLdsOut): 16 chunks of 16 bytes per lane, +1 slot of padding
     __shared__ gv4 out_lds[kLdsOut && kGroupStore ? 64 * kOutSlots : 1];
@@ -547,6 +555,48 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         int flushed = 0;                                     // chunks [0, flushed) of my row are in HBM
         const int nfull = static_cast<int>(ps.width / C);    // chunks whose pixels are all inside the row
 
+        // Output ring flush after `steps` steps: whole aligned 8-chunk blocks
+        // (one 128-byte line of RGBA8) as soon as they are complete, and the
+        // row's tail at its end. A line is written whole by one lane in one
+        // burst, never in two halves a group apart. Called every 8 steps, so
+        // at most 15 chunks are pending and 16 slots never collide.
+        auto flush_out = [&](int steps) {
+            if constexpr (kGroupStore && kLdsOut) {
+                if (!gstore) return; // wave-uniform
+                const int done = min(steps - skew, nchunks); // chunks [0, done) reconstructed
+                const int upto = done == nchunks ? done : (done & ~7);
+                const int lo = row_ok ? flushed : 0;
+                const int hi = row_ok ? max(lo, min(upto, nfull)) : 0;
+                if (row_ok) flushed = max(flushed, upto);
+                if constexpr (kCoopStore) {
+                    // Eight lanes write one row's aligned 8-chunk block: each
+                    // store instruction covers 8 whole lines instead of 16 bytes
+                    // of 64 lines. The block is read from the row's ring slots.
+                    const int span = lo | (hi - lo) << 16;
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const int r = 8 * i + (lane >> 3);
+                        const int sp = __shfl(span, r);
+                        const int k = (sp & 0xffff) + (lane & 7);
+                        if ((lane & 7) < (sp >> 16)) {
+                            const uint32_t yr = bd.band * 64 + static_cast<uint32_t>(r);
+                            gu8 *orow = (gu8 *)(ps.out + static_cast<size_t>(yr * ps.yf + ps.yo) * ps.out_stride);
+                            store16(gcast<gv4>(orow + static_cast<size_t>(k) * 16), out_lds[r * kOutSlots + (k & 15)]);
+                        }
+                    }
+                    for (int kf = lo + 8; kf < hi; kf++) // a row's tail past its last whole block (end of row only)
+                        store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                } else {
+                    int kf = lo;
+#pragma unroll
+                    for (int i = 0; i < 8; i++, kf++)
+                        if (kf < hi) store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                    for (; kf < hi; kf++)
+                        store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                }
+            }
+        };
+
         // One group: G steps from step0 over this lane's chunks k0 .. k0+G-1
         // (k0 = step0 - skew), input dwords in `in`.
         auto run_group = [&](const uint32_t (&in)[GD], int step0) {
@@ -554,7 +604,10 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
 #pragma unroll
             for (int r = 0; r < G; r++) {
                 const int step = step0 + r;
-                if (step >= nsteps_of(nchunks, max_skew)) break;
+                if (step >= nsteps_of(nchunks, max_skew)) {
+                    if ((r & 7) != 0) flush_out(step);
+                    break;
+                }
                 const int k = step - skew;
                 const bool act = row_ok && k >= 0 && k < nchunks;
 
@@ -651,25 +704,9 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                         for (int i = 0; i < CW; i++) st_sc1_64(d + i, static_cast<uint64_t>(epoch) << 32 | ob[i]);
                     }
                 }
+                if ((r & 7) == 7) flush_out(step + 1);
             }
-            if constexpr (kGroupStore && kLdsOut) {
-                // Flush whole aligned 8-chunk blocks (one 128-byte line of RGBA8)
-                // as soon as they are complete, and the row's tail at its end: a
-                // line is written whole by one lane in one burst, never in two
-                // halves a group apart.
-                if (gstore && row_ok) {
-                    const int done = min(step0 + G - skew, nchunks); // chunks [0, done) reconstructed
-                    const int upto = done == nchunks ? done : (done & ~7);
-                    const int hi = min(upto, nfull);
-                    int kf = flushed;
-#pragma unroll
-                    for (int i = 0; i < 8; i++, kf++)
-                        if (kf < hi) store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
-                    for (; kf < hi; kf++)
-                        store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
-                    flushed = max(flushed, upto);
-                }
-            } else if constexpr (kGroupStore) {
+            if constexpr (kGroupStore && !kLdsOut) {
                 if (gstore) { // the group's full chunks, one contiguous burst per lane
 #pragma unroll
                     for (int r = 0; r < G; r++) {
@@ -703,14 +740,35 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 load_dwords<GD>(b, rsrc, off);
             }
         };
-        uint32_t bufA[GD], bufB[GD];
-        load_group(bufA, 0);
-        for (int step0 = 0; step0 < nsteps; step0 += 2 * G) {
-            load_group(bufB, step0 + G);
-            run_group(bufA, step0);
-            if (step0 + G >= nsteps) break;
-            load_group(bufA, step0 + 2 * G);
-            run_group(bufB, step0 + G);
+        if constexpr (kPairLoads) {
+            // two groups' bursts back to back: the line they share is requested
+            // twice within a few cycles and fetched from HBM once
+            uint32_t b0[GD], b1[GD], b2[GD], b3[GD];
+            load_group(b0, 0);
+            load_group(b1, G);
+            for (int step0 = 0; step0 < nsteps; step0 += 4 * G) {
+                load_group(b2, step0 + 2 * G);
+                load_group(b3, step0 + 3 * G);
+                run_group(b0, step0);
+                if (step0 + G >= nsteps) break;
+                run_group(b1, step0 + G);
+                if (step0 + 2 * G >= nsteps) break;
+                load_group(b0, step0 + 4 * G);
+                load_group(b1, step0 + 5 * G);
+                run_group(b2, step0 + 2 * G);
+                if (step0 + 3 * G >= nsteps) break;
+                run_group(b3, step0 + 3 * G);
+            }
+        } else {
+            uint32_t bufA[GD], bufB[GD];
+            load_group(bufA, 0);
+            for (int step0 = 0; step0 < nsteps; step0 += 2 * G) {
+                load_group(bufB, step0 + G);
+                run_group(bufA, step0);
+                if (step0 + G >= nsteps) break;
+                load_group(bufA, step0 + 2 * G);
+                run_group(bufB, step0 + G);
+            }
         }
         if constexpr (DEPTH >= ZPX_PNG_P1 && DEPTH <= ZPX_PNG_P8) {
             for (int off = 32; off > 0; off >>= 1) maxidx = max(maxidx, __shfl_xor(maxidx, off));
