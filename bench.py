@@ -394,11 +394,18 @@ def main():
         steps = max(3, args.steps // 2)
         pv = pb.pixels * ws * steps / wall / 1e6
         ach = pb.bytes / (kern_ms * 1e-3) / 1e9
+        ptraffic = None
+        try:
+            tp = json.load(open(args.traffic_json)).get("png_unfilter", {})
+            if tp.get("images") == args.images and tp.get("size") == args.size:
+                ptraffic = tp.get("hbm_bytes_per_launch")
+        except Exception:
+            ptraffic = None
         pres = {"metric": "MPixels/sec decoded (4K truecolor-8 PNG, mixed Sub/Up/Avg/Paeth)", "value": round(pv, 1),
                 "unit": "MPixels/sec", "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
                 "config": {"workload": f"{args.images}x {W}x{H} tc8 PNG unfilter -> RGBA, configs[2]"},
                 "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "png_unfilter_kernel",
+                             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": ptraffic, "kernel": "png_unfilter_kernel",
                              "kernel_ms_per_launch": round(kern_ms, 3), "algorithmic_bytes_per_launch": pb.bytes},
                 "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1)}
         if result:

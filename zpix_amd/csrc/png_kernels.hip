@@ -54,6 +54,14 @@ constexpr bool kPairLoads = ZPX_PNG_PAIR_LOADS != 0; // input bursts issued two 
 #define ZPX_PNG_COOP_STORE 1
 #endif
 constexpr bool kCoopStore = ZPX_PNG_COOP_STORE != 0; // ring flush: 8 lanes per row, whole lines per store
+#ifndef ZPX_PNG_COOP_LOAD
+#define ZPX_PNG_COOP_LOAD 0
+#endif
+constexpr bool kCoopLoad = ZPX_PNG_COOP_LOAD != 0; // group input: 8 lanes per row load its 128-byte window
+// LDS dwords per row of the input stage: the row's window of NP 16-byte
+// pieces plus one piece of padding (4-way bank spread for the per-lane reads)
+constexpr int stage_pieces(int gd) { return (12 + 4 * gd + 15) / 16; } // window start is 16-aligned, <= 12 B early
+constexpr int stage_dw(int gd) { return stage_pieces(gd) <= 8 ? 36 : 44; }
 #ifndef ZPX_PNG_SPIN_LIMIT
 #define ZPX_PNG_SPIN_LIMIT (1u << 20)
 #endif
@@ -469,6 +477,10 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
     // output ring (kLdsOut): 16 chunks of 16 bytes per lane, +1 slot of padding
     __shared__ gv4 out_lds[kLdsOut && kGroupStore ? 64 * kOutSlots : 1];
+    // input stage (kCoopLoad): each row's 128-byte window of the next group
+    constexpr int NP = stage_pieces(GD), kStageDw = stage_dw(GD);
+    static_assert(NP <= 9 && (NP <= 8 || kStageDw >= 40), "input window: 8 pieces by 8-lane groups, +1 by one round");
+    __shared__ __attribute__((aligned(16))) uint32_t in_lds[kCoopLoad ? 64 * kStageDw : 1];
 
     const int lane = threadIdx.x;
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
@@ -512,7 +524,9 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         // them), so a 16-byte load holding a row's last bytes is never cut by
         // the range check; loads wholly past it read zeros
         const uint8_t *band0 = ps.filtered + static_cast<size_t>(bd.band) * 64 * (rb + 1);
-        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
+        // (line-aligned for the cooperative loads, so a row's window is its lines)
+        const uintptr_t base_mask = kCoopLoad ? ~uintptr_t(127) : ~uintptr_t(3);
+        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & base_mask);
         const uint32_t delta = static_cast<uint32_t>(band0 - base4);
         const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
         const uint32_t nrec = extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent);
@@ -740,7 +754,63 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 load_dwords<GD>(b, rsrc, off);
             }
         };
-        if constexpr (kPairLoads) {
+        if constexpr (kCoopLoad) {
+            // Cooperative group loads: in round i, lanes 8j..8j+7 load row
+            // 8i+j's 128-byte window (16 bytes each), so a load instruction
+            // covers 8 rows' contiguous lines instead of 16 bytes of 64 rows.
+            // The windows go through LDS to the lane that owns the row.
+            // Row r's group starts at dword-aligned offset base_r + step0*CB.
+            int wbase[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int r = 8 * i + (lane >> 3);
+                const int ro = static_cast<int>(delta) + r * static_cast<int>(rb + 1); // filter byte of row r
+                const int dof = ro + 1 - ((ro + 1) & 3);
+                wbase[i] = dof - __shfl(skew, r) * CB;
+            }
+            const int wmine = data_off - skew * CB; // my row's group start at step 0
+            u32x4 R[8], R8;
+            auto coop_load = [&](int step0) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    // a negative offset (a row still in its skew) must not reach
+                    // the instruction's immediate: select it out of range instead
+                    const int o = ((wbase[i] + step0 * CB) & ~15) + 16 * (lane & 7);
+                    R[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
+                }
+                if constexpr (NP > 8) { // 16-byte chunks: a ninth piece, my own row's
+                    const int o = ((wmine + step0 * CB) & ~15) + 16 * 8;
+                    R8 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
+                }
+            };
+            auto stage_in = [&](uint32_t (&b)[GD], int step0) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int r = 8 * i + (lane >> 3);
+                    *reinterpret_cast<u32x4 *>(&in_lds[r * kStageDw + 4 * (lane & 7)]) = R[i];
+                }
+                if constexpr (NP > 8) *reinterpret_cast<u32x4 *>(&in_lds[lane * kStageDw + 32]) = R8;
+                const int w = ((data_off + (step0 - skew) * CB) & 15) >> 2; // my first dword in my window
+#pragma unroll
+                for (int j = 0; j < GD; j++) b[j] = in_lds[lane * kStageDw + w + j];
+            };
+            // pipeline: group g+1's window is staged and read back into
+            // registers before group g runs (its LDS latency hides behind g),
+            // and group g+2's loads are in flight meanwhile
+            uint32_t inA[GD], inB[GD];
+            coop_load(0);
+            stage_in(inA, 0);
+            coop_load(G);
+            for (int step0 = 0; step0 < nsteps; step0 += 2 * G) {
+                stage_in(inB, step0 + G);
+                coop_load(step0 + 2 * G);
+                run_group(inA, step0);
+                if (step0 + G >= nsteps) break;
+                stage_in(inA, step0 + 2 * G);
+                coop_load(step0 + 3 * G);
+                run_group(inB, step0 + G);
+            }
+        } else if constexpr (kPairLoads) {
             // two groups' bursts back to back: the line they share is requested
             // twice within a few cycles and fetched from HBM once
             uint32_t b0[GD], b1[GD], b2[GD], b3[GD];
