@@ -555,8 +555,26 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         // group stores: contiguous rows (xf == 1), 16-byte aligned, and an
         // output type a colour key does not change (Gray8/16 + tRNS -> NRGBA)
         constexpr bool kKeyWidens = DEPTH == ZPX_PNG_G8 || DEPTH == ZPX_PNG_G16;
-        const bool gstore = kGroupStore && ps.xf == 1 && !(kKeyWidens && ps.use_trns) &&
+        // Adam7 passes (xf > 1) of the 4- and 8-byte-pixel depths also go
+        // through the ring: a chunk's pixels are scattered xf apart at flush
+        constexpr bool kStrided = kLdsOut && (DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TCA8 ||
+                                              DEPTH == ZPX_PNG_TC16 || DEPTH == ZPX_PNG_TCA16);
+        const bool gstore = kGroupStore && (ps.xf == 1 || kStrided) && !(kKeyWidens && ps.use_trns) &&
                             ((reinterpret_cast<uintptr_t>(ps.out) | ps.out_stride) & 15) == 0;
+        // chunk k's 16 output bytes (pack_chunk16) into output row orow
+        auto put_chunk = [&](gu8 *orow, int k, gv4 v) {
+            if (ps.xf == 1) { // wave-uniform
+                store16(gcast<gv4>(orow + static_cast<size_t>(k) * 16), v);
+            } else if constexpr (kStrided) {
+                constexpr int OBPX = 16 / C; // output bytes per pixel: 4 or 8
+#pragma unroll
+                for (int u = 0; u < C; u++) {
+                    gu8 *d = orow + static_cast<size_t>((static_cast<uint32_t>(k * C + u)) * ps.xf + ps.xo) * OBPX;
+                    if constexpr (OBPX == 8) *gcast<gv2>(d) = gv2{v[2 * u], v[2 * u + 1]};
+                    else *gcast<uint32_t>(d) = v[u];
+                }
+            }
+        };
         gu8 *out_row = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
 
         uint32_t left[BPP], ul[BPP];
@@ -595,18 +613,18 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                         if ((lane & 7) < (sp >> 16)) {
                             const uint32_t yr = bd.band * 64 + static_cast<uint32_t>(r);
                             gu8 *orow = (gu8 *)(ps.out + static_cast<size_t>(yr * ps.yf + ps.yo) * ps.out_stride);
-                            store16(gcast<gv4>(orow + static_cast<size_t>(k) * 16), out_lds[r * kOutSlots + (k & 15)]);
+                            put_chunk(orow, k, out_lds[r * kOutSlots + (k & 15)]);
                         }
                     }
                     for (int kf = lo + 8; kf < hi; kf++) // a row's tail past its last whole block (end of row only)
-                        store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                        put_chunk(out_row, kf, out_lds[lane * kOutSlots + (kf & 15)]);
                 } else {
                     int kf = lo;
 #pragma unroll
                     for (int i = 0; i < 8; i++, kf++)
-                        if (kf < hi) store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                        if (kf < hi) put_chunk(out_row, kf, out_lds[lane * kOutSlots + (kf & 15)]);
                     for (; kf < hi; kf++)
-                        store16(gcast<gv4>(out_row + static_cast<size_t>(kf) * 16), out_lds[lane * kOutSlots + (kf & 15)]);
+                        put_chunk(out_row, kf, out_lds[lane * kOutSlots + (kf & 15)]);
                 }
             }
         };
