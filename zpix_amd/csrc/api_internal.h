@@ -6,10 +6,12 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "zpix_amd.h"
+#include "device_types.h"
 
 struct zpx_ctx {
     int device = 0;
@@ -93,5 +95,28 @@ int launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_frame,
 void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
                       uint64_t &bytes);
 DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette);
+
+// PNG band schedule (the ticket order of png_unfilter_kernel). Bands are
+// ordered by the first output row they write, then by pass: band b of a pass
+// still precedes band b+1 of it (the kernel's no-deadlock rule), and for
+// Adam7 the passes that fill the same output lines run close together, so a
+// line's partial writes from passes 1/2/4/6 meet in L2 instead of reaching
+// HBM one pass at a time. Without interlacing this is band-major order.
+inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passes)
+{
+    std::vector<DevPngBand> sched;
+    std::vector<uint64_t> key;
+    for (size_t i = 0; i < passes.size(); i++)
+        for (uint32_t b = 0; b < passes[i].nbands; b++) {
+            sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
+            key.push_back(static_cast<uint64_t>(b) * 64 * passes[i].yf + passes[i].yo);
+        }
+    std::vector<size_t> idx(sched.size());
+    for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return key[a] < key[b]; });
+    std::vector<DevPngBand> out(sched.size());
+    for (size_t i = 0; i < idx.size(); i++) out[i] = sched[idx[i]];
+    return out;
+}
 
 } // namespace zpx

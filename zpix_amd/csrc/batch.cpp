@@ -363,10 +363,7 @@ int Pipeline::issue_png(Slot &s)
         max_bands = std::max(max_bands, p.nbands);
         max_rb = std::max(max_rb, rowbytes[i]);
     }
-    std::vector<DevPngBand> sched; // band-major over the passes (as zpx_png_plan_create)
-    for (uint32_t b = 0; b < max_bands; b++)
-        for (size_t i = 0; i < passes.size(); i++)
-            if (b < passes[i].nbands) sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
+    const std::vector<DevPngBand> sched = png_schedule(passes); // output-row order (api_internal.h)
     const uint32_t granules = static_cast<uint32_t>(png_band_granules(ps.depth, max_rb));
     // descriptor staging: passes | sched | palette (256 zpx_color)
     const size_t pass_b = align_up(passes.size() * sizeof(DevPngPass));

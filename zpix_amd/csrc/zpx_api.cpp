@@ -319,11 +319,7 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
         max_bands = std::max(max_bands, p.nbands);
         max_rb = std::max(max_rb, pass_rowbytes[i]);
     }
-    // band-major order: band b of every pass before band b+1 of any pass
-    std::vector<DevPngBand> sched;
-    for (uint32_t b = 0; b < max_bands; b++)
-        for (size_t i = 0; i < passes.size(); i++)
-            if (b < passes[i].nbands) sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
+    const std::vector<DevPngBand> sched = png_schedule(passes); // output-row order (api_internal.h)
     g.nsched = static_cast<uint32_t>(sched.size());
     g.nbands = base;
     g.band_bytes = static_cast<uint32_t>(png_band_granules(g.depth, max_rb)); // granules per band
