@@ -479,7 +479,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     __shared__ gv4 out_lds[kLdsOut && kGroupStore ? 64 * kOutSlots : 1];
     // input stage (kCoopLoad): each row's 128-byte window of the next group
     constexpr int NP = stage_pieces(GD), kStageDw = stage_dw(GD);
-    static_assert(NP <= 9 && (NP <= 8 || kStageDw >= 40), "input window: 8 pieces by 8-lane groups, +1 by one round");
+    static_assert(!kCoopLoad || (NP <= 9 && (NP <= 8 || kStageDw >= 40)), "input window: 8 pieces by 8-lane groups, +1 by one round");
     __shared__ __attribute__((aligned(16))) uint32_t in_lds[kCoopLoad ? 64 * kStageDw : 1];
 
     const int lane = threadIdx.x;
