@@ -476,7 +476,16 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     static_assert(!kLdsOut || G % 8 == 0, "the output ring flushes every 8 steps, 16 slots");
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
     // output ring (kLdsOut): 16 chunks of 16 bytes per lane, +1 slot of padding
-    __shared__ gv4 out_lds[kLdsOut && kGroupStore ? 64 * kOutSlots : 1];
+    // ZPX_PNG_RAW_RING=1: TC8/TC16 (12-byte chunks) keep the chunk's reconstructed bytes (3
+    // dwords) and pack them to 16 output bytes at the flush: 12.3 KB per wave
+    // instead of 17.4 KB, 12 resident waves per CU. Measured: 3.61 ms at 12
+    // waves/CU, the same as the default ring, so it stays off.
+#ifndef ZPX_PNG_RAW_RING
+#define ZPX_PNG_RAW_RING 0
+#endif
+    constexpr bool kRawRing = ZPX_PNG_RAW_RING && kLdsOut && kGroupStore && CW == 3;
+    constexpr int kRingDw = kRawRing ? 16 * CW + 1 : 4 * kOutSlots; // dwords per lane (odd stride when raw)
+    __shared__ __attribute__((aligned(16))) uint32_t out_lds[kLdsOut && kGroupStore ? 64 * kRingDw : 1];
     // input stage (kCoopLoad): each row's 128-byte window of the next group
     constexpr int NP = stage_pieces(GD), kStageDw = stage_dw(GD);
     static_assert(!kCoopLoad || (NP <= 9 && (NP <= 8 || kStageDw >= 40)), "input window: 8 pieces by 8-lane groups, +1 by one round");
@@ -576,6 +585,28 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
             }
         };
         gu8 *out_row = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
+        // output ring slot (k & 15) of row r: write my chunk, read any row's
+        auto ring_put = [&](int k, const uint32_t (&ob)[CW]) __attribute__((always_inline)) {
+            if constexpr (kRawRing) {
+#pragma unroll
+                for (int i = 0; i < CW; i++) out_lds[lane * kRingDw + (k & 15) * CW + i] = ob[i];
+            } else {
+                uint32_t w[4];
+                pack_chunk16<DEPTH, CW>(ps, ob, w);
+                *reinterpret_cast<gv4 *>(&out_lds[lane * kRingDw + (k & 15) * 4]) = gv4{w[0], w[1], w[2], w[3]};
+            }
+        };
+        auto ring_get = [&](int r, int k) __attribute__((always_inline)) -> gv4 {
+            if constexpr (kRawRing) {
+                uint32_t ob[CW], w[4];
+#pragma unroll
+                for (int i = 0; i < CW; i++) ob[i] = out_lds[r * kRingDw + (k & 15) * CW + i];
+                pack_chunk16<DEPTH, CW>(ps, ob, w);
+                return gv4{w[0], w[1], w[2], w[3]};
+            } else {
+                return *reinterpret_cast<const gv4 *>(&out_lds[r * kRingDw + (k & 15) * 4]);
+            }
+        };
 
         uint32_t left[BPP], ul[BPP];
 #pragma unroll
@@ -592,7 +623,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         // row's tail at its end. A line is written whole by one lane in one
         // burst, never in two halves a group apart. Called every 8 steps, so
         // at most 15 chunks are pending and 16 slots never collide.
-        auto flush_out = [&](int steps) {
+        auto flush_out = [&](int steps) __attribute__((always_inline)) {
             if constexpr (kGroupStore && kLdsOut) {
                 if (!gstore) return; // wave-uniform
                 const int done = min(steps - skew, nchunks); // chunks [0, done) reconstructed
@@ -613,18 +644,18 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                         if ((lane & 7) < (sp >> 16)) {
                             const uint32_t yr = bd.band * 64 + static_cast<uint32_t>(r);
                             gu8 *orow = (gu8 *)(ps.out + static_cast<size_t>(yr * ps.yf + ps.yo) * ps.out_stride);
-                            put_chunk(orow, k, out_lds[r * kOutSlots + (k & 15)]);
+                            put_chunk(orow, k, ring_get(r, k));
                         }
                     }
                     for (int kf = lo + 8; kf < hi; kf++) // a row's tail past its last whole block (end of row only)
-                        put_chunk(out_row, kf, out_lds[lane * kOutSlots + (kf & 15)]);
+                        put_chunk(out_row, kf, ring_get(lane, kf));
                 } else {
                     int kf = lo;
 #pragma unroll
                     for (int i = 0; i < 8; i++, kf++)
-                        if (kf < hi) put_chunk(out_row, kf, out_lds[lane * kOutSlots + (kf & 15)]);
+                        if (kf < hi) put_chunk(out_row, kf, ring_get(lane, kf));
                     for (; kf < hi; kf++)
-                        put_chunk(out_row, kf, out_lds[lane * kOutSlots + (kf & 15)]);
+                        put_chunk(out_row, kf, ring_get(lane, kf));
                 }
             }
         };
@@ -716,9 +747,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 const bool full = k < nfull;
                 if constexpr (kGroupStore && kLdsOut) {
                     if (gstore && act && full) {
-                        uint32_t w[4];
-                        pack_chunk16<DEPTH, CW>(ps, ob, w);
-                        out_lds[lane * kOutSlots + (k & 15)] = gv4{w[0], w[1], w[2], w[3]};
+                        ring_put(k, ob);
                     }
                 } else if constexpr (kGroupStore) {
                     pack_chunk16<DEPTH, CW>(ps, ob, gw[r]);
