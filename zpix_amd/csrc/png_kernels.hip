@@ -66,6 +66,9 @@ constexpr int stage_dw(int gd) { return stage_pieces(gd) <= 8 ? 36 : 44; }
 #define ZPX_PNG_SPIN_LIMIT (1u << 20)
 #endif
 constexpr uint32_t kSpinLimit = ZPX_PNG_SPIN_LIMIT;
+#ifndef ZPX_PNG_SLEEP
+#define ZPX_PNG_SLEEP 2 // s_sleep between boundary polls (units of 64 cycles)
+#endif
 
 template <int DEPTH>
 struct Traits;
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                             timed_out = true;
                             break;
                         }
-                        __builtin_amdgcn_s_sleep(2);
+                        __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
                         fill_window(step - wi);
                     }
                     uint32_t gv[CW];
