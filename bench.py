@@ -6,8 +6,13 @@ q75 4:2:0 frames per GPU, coefficient grids resident in HBM, RGBA written to
 HBM).  Host entropy decoding happens before the timed region (it is reported
 separately as host_entropy_mpix_s).  Multi-GPU: one process per GPU
 (torch.distributed over RCCL), each rank decodes its own 64 frames (weak
-scaling, no data-path collective); `--gather` adds an RCCL gather of every
-rank's RGBA to rank 0, timed separately.
+scaling, no data-path collective).
+
+configs[3] is the "end_to_end" line: this rank's shard of the mixed
+JPEG+PNG batch (image i -> rank i mod N) from encoded bytes in host memory
+to RGBA8 in HBM, then (N > 1) ONE RCCL gather of every rank's RGBA arena to
+rank 0, timed and reported apart ("gather"); zpix_amd/shard.py holds the
+placement, shared with tests/test_distributed.py.
 
 The PNG workload (configs[2]: 64 x 4096^2 tc8, mixed Sub/Up/Avg/Paeth rows)
 is measured in the same run and reported under "png" (disable: --no-png).
@@ -46,15 +51,17 @@ def parse():
     ap.add_argument("--no-png", action="store_true")
     ap.add_argument("--png-only", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
-    ap.add_argument("--gather", action="store_true", help="RCCL-gather all RGBA outputs to rank 0 (timed apart)")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="bound on the CPU baseline samples (JPEG + PNG)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the RCCL gather of the end-to-end batch's RGBA to rank 0")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end streaming line (host entropy threads + H2D + kernels)")
     ap.add_argument("--e2e-images", type=int, default=64,
                     help="encoded images per GPU in the end-to-end batch (configs[3]: 512 over 8 GPUs)")
-    ap.add_argument("--host-threads", type=int, default=16, help="host entropy/inflate threads (end-to-end)")
+    ap.add_argument("--host-threads", type=int, default=0,
+                    help="host entropy/inflate threads per rank (end-to-end); 0 = this rank's share of the host")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/)")
     return ap.parse_args()
@@ -68,9 +75,18 @@ def dist_env():
 
 
 def shard_images(total: int, rank: int, ws: int) -> list[int]:
-    """Global image ids owned by `rank`: image i -> GPU i mod N.
-    Images are independent, so the shards share nothing."""
-    return [i for i in range(total) if i % ws == rank]
+    """Global image ids owned by `rank`: image i -> GPU i mod N."""
+    from zpix_amd.shard import shard_images as f
+
+    return f(total, rank, ws)
+
+
+def e2e_is_jpeg(i: int, ws: int) -> bool:
+    """configs[3]'s mix: image i is a 4K JPEG 4:2:0 when its index within its
+    rank's shard (i // N) is even, else a 4K tc8 PNG -- every shard is half
+    and half at every N (an even/odd split by global index would hand all
+    JPEGs to even ranks and all PNGs to odd ones)."""
+    return (i // ws) % 2 == 0
 
 
 def max_over_ranks(dist, value: float, device) -> float:
@@ -113,45 +129,116 @@ def timed_steps(torch, dist, launch, steps, warmup, ws):
     return max_over_ranks(dist, wall, "cuda"), kern_ms
 
 
-def cpu_baseline_jpeg(data: bytes, seconds: float):
-    """The oracle (C restatement of the reference algorithm, -O2, scalar) on a
-    bounded sample: full jpeg.decode + Image.rgbaPixels of the same 4K frame,
-    on all host cores (one frame per thread) and on one core."""
-    import numpy as np  # noqa: F401
-    import oracle_py as O
+def cpu_info() -> dict:
+    from zpix_amd.shard import host_cpu_budget
 
-    O.lib()
-    cores = min(16, os.cpu_count() or 1)
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "budget": host_cpu_budget(),
+            "cpu_model": model}
 
-    def one():
-        img = O.jpeg_decode(data)
-        img.rgba_pixels()
-        return img.width * img.height
 
-    t0 = time.perf_counter()
-    px1 = one()
-    t1 = time.perf_counter() - t0
-    single = px1 / t1 / 1e6
-    # all cores: threads (ctypes releases the GIL inside the oracle)
-    budget = max(seconds - t1, 1.0)
-    per_thread = max(1, int(budget / t1 / 1.5))
-    done = [0] * cores
+def _all_cores(fn, threads: int, seconds: float, t_one: float):
+    """fn() on `threads` threads (ctypes drops the GIL inside the oracle), each
+    repeating it to fill about `seconds`; returns (pixels, wall)."""
+    per_thread = max(1, int(seconds / max(t_one, 1e-3) / 1.5))
+    done = [0] * threads
 
     def worker(i):
         for _ in range(per_thread):
-            done[i] += one()
+            done[i] += fn()
 
-    ths = [threading.Thread(target=worker, args=(i,)) for i in range(cores)]
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
     t0 = time.perf_counter()
     for t in ths:
         t.start()
     for t in ths:
         t.join()
-    tm = time.perf_counter() - t0
-    multi = sum(done) / tm / 1e6
-    return {"value": round(multi, 2), "unit": "MPixels/sec", "cores": cores, "kind": "port",
-            "sample": f"{cores * per_thread + 1} x oracle jpeg.decode+rgbaPixels of one 4096x4096 q75 4:2:0 frame "
-                      f"({tm + t1:.1f}s)", "single_core_mpix_s": round(single, 2)}
+    return sum(done), time.perf_counter() - t0, per_thread
+
+
+def cpu_baseline(jpeg_data: bytes, png_data: bytes | None, seconds: float) -> dict:
+    """The oracle (C restatement of the reference algorithm, gcc -O2, scalar,
+    one image per thread) timed on this box's host cores on bounded samples
+    of the bench's own 4K inputs:
+
+    - JPEG (the headline's metric): jpeg.decode + Image.rgbaPixels of one
+      4096^2 q75 4:2:0 frame, on 1 core with the stage split entropy
+      (processSos, decoder.zig:1148-1455) / reconstruct (reconstructBlock,
+      :1553-1634) / rgbaPixels (image.zig:103-130), then on every usable core;
+    - PNG: png.decode of one 4096^2 tc8 mixed-filter image, on 1 core split
+      into inflate+chunks (png/decoder.zig:404-545) / unfilter+store
+      (:649-1149), then on every usable core."""
+    import numpy as np
+    import oracle_py as O
+
+    O.lib()
+    info = cpu_info()
+    cores = info["budget"]
+    out = {"unit": "MPixels/sec", "cores": cores, "kind": "port", **info}
+    # ---- JPEG, 1 core, stage split
+    t0 = time.perf_counter()
+    co = O.jpeg_coefficients(jpeg_data)
+    t_ent = time.perf_counter() - t0
+    from zpix_amd.device import jpeg_layout as _lay  # makeImg geometry (host arithmetic only)
+
+    class _F:  # the frame fields jpeg_layout reads
+        n_comp, mxx, myy, h, v = co.n_comp, co.mxx, co.myy, co.h, co.v
+
+    lay = _lay(_F)
+    planes_buf = np.zeros(lay.total, np.uint8)
+    planes = [planes_buf[0:], planes_buf[lay.cb_off:], planes_buf[lay.cr_off:]][:co.n_comp]
+    strides = [lay.y_stride] + [lay.c_stride] * (co.n_comp - 1)
+    qts = [co.quant_zigzag[co.tq[c]] for c in range(co.n_comp)]
+    tr = []
+    O.reconstruct_grids(co.n_comp, co.width, co.height, co.h, co.v, co.mxx, co.myy, co.grids, qts,
+                        co.progressive, planes, strides, timing=tr)
+    t_rec = tr[0]
+    img = O.jpeg_decode(jpeg_data)
+    t0 = time.perf_counter()
+    img.rgba_pixels()
+    t_rgba = time.perf_counter() - t0
+    px = img.width * img.height
+    t1 = t_ent + t_rec + t_rgba
+
+    def jpeg_one():
+        im = O.jpeg_decode(jpeg_data)
+        im.rgba_pixels()
+        return im.width * im.height
+
+    share = seconds / 2 if png_data is not None else seconds
+    pix, wall, per = _all_cores(jpeg_one, cores, share, t1)
+    out["value"] = round(pix / wall / 1e6, 2)
+    out["sample"] = (f"JPEG: {cores} threads x {per} oracle jpeg.decode+rgbaPixels of one 4096x4096 q75 4:2:0 frame "
+                     f"({wall:.1f}s); 1-core stage split on the same frame")
+    out["jpeg"] = {"all_cores_mpix_s": out["value"], "single_core_mpix_s": round(px / t1 / 1e6, 2),
+                   "stages_ms_1core": {"entropy": round(t_ent * 1e3, 1), "reconstruct": round(t_rec * 1e3, 1),
+                                       "rgba_pixels": round(t_rgba * 1e3, 1)}}
+    # ---- PNG, 1 core, stage split
+    if png_data is not None:
+        O.png_unfilter_seconds()
+        t0 = time.perf_counter()
+        pim = O.png_decode(png_data)
+        t_all = time.perf_counter() - t0
+        t_unf = O.png_unfilter_seconds()
+        ppx = pim.width * pim.height
+
+        def png_one():
+            return O.png_decode(png_data).width * pim.height
+
+        pix, wall, per = _all_cores(png_one, cores, share, t_all)
+        out["png"] = {"all_cores_mpix_s": round(pix / wall / 1e6, 2), "single_core_mpix_s": round(ppx / t_all / 1e6, 2),
+                      "stages_ms_1core": {"inflate_and_chunks": round((t_all - t_unf) * 1e3, 1),
+                                          "unfilter_and_store": round(t_unf * 1e3, 1)},
+                      "sample": f"{cores} threads x {per} oracle png.decode of one 4096x4096 tc8 mixed-filter PNG "
+                                f"({wall:.1f}s)"}
+    return out
 
 
 def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
@@ -198,6 +285,7 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         if not np.array_equal(got.reshape(-1)[:want.size], want.reshape(-1)):
             raise SystemExit("parity failure: Adam7 RGBA16 PNG != oracle")
     wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, 1, ws)
+    pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
     out["png_adam7_rgba16"] = {
         "value": round(pb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
         "kernel_ms_per_launch": round(kern_ms, 3),
@@ -211,34 +299,63 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
     return out
 
 
-def bench_e2e(args, torch, dist, ws, rank, ctx, S):
-    """End to end, from encoded bytes in host memory: zpx_batch_decode_rgba
-    with a pool of host entropy/inflate threads overlapped with pinned H2D
-    copies and the kernels, RGBA8 into device memory (configs[3]'s per-GPU
-    shard: alternating 4096^2 JPEG 4:2:0 and tc8 PNG).  Never `value`."""
-    from zpix_amd import batch
+def bench_e2e(args, torch, dist, ws, rank, ctx, S, threads):
+    """configs[3], end to end from encoded bytes in host memory: this rank's
+    shard of the mixed JPEG+PNG batch (image i -> rank i mod N) through
+    zpx_batch_decode_rgba -- host entropy/inflate workers overlapped with
+    pinned H2D copies and the kernels -- into this rank's RGBA8 arena in HBM,
+    then one RCCL gather of every arena to rank 0 (N > 1), timed apart.
+    The placement is zpix_amd.shard's (shared with the gloo test).  Never
+    `value`: it is bound by the host's serial Huffman/inflate work."""
+    from zpix_amd import batch, shard
 
     W = H = args.size
-    mine = shard_images(args.e2e_images * ws, rank, ws)
-    uniq = {0: S.jpeg_420(0, W, H, args.quality), 1: S.png_tc8_mixed(1, W, H)}
-    bufs = [uniq[i % 2] for i in mine]
-    batch.decode_rgba(bufs[:2], host_threads=args.host_threads, ctx=ctx)  # warm-up (pools, code objects)
-    torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    res, st = batch.decode_rgba(bufs, host_threads=args.host_threads, ctx=ctx, with_stats=True)
-    torch.cuda.synchronize()
-    wall = max_over_ranks(dist, time.perf_counter() - t0, "cuda")
-    bad = [r.status for r in res if r.status != "Ok"]
+    total = args.e2e_images * ws
+    uniq = {True: S.jpeg_420(0, W, H, args.quality), False: S.png_tc8_mixed(1, W, H)}
+    bufs = [uniq[e2e_is_jpeg(i, ws)] for i in range(total)]
+    plan = shard.ShardPlan([(W, H)] * total, ws)
+
+    def decode_fn(my_bufs, dsts):
+        res, st = batch.decode_rgba(my_bufs, host_threads=threads, ctx=ctx, dst=dsts, with_stats=True)
+        return [r.status for r in res], st
+
+    # warm-up (pinned pools, code objects) on two images of the shard
+    warm = torch.empty(2 * W * H * 4, dtype=torch.uint8, device="cuda")
+    decode_fn([uniq[True], uniq[False]], [warm[:W * H * 4].view(H, W, 4), warm[W * H * 4:].view(H, W, 4)])
+    del warm
+    gather = ws > 1 and not args.no_gather
+    r = shard.decode_and_gather(bufs, plan, rank, dist if ws > 1 else None, decode_fn, "cuda", gather=gather,
+                                sync=torch.cuda.synchronize)
+    wall = max_over_ranks(dist, r.decode_s, "cuda")
+    bad = sorted({s for s in r.statuses.values() if s != "Ok"})
     if bad:
         raise SystemExit(f"end-to-end batch failed: {bad[:3]}")
-    return {"value": round(len(bufs) * ws * W * H / wall / 1e6, 1), "unit": "MPixels/sec",
-            "images_per_gpu": len(bufs), "host_threads": st.host_threads, "depth": st.depth,
-            "wall_s": round(wall, 3), "host_cpu_s": round(st.host_s, 3),
-            "h2d_gb": round(st.h2d_bytes / 1e9, 3),
-            "config": {"workload": f"{len(bufs)}x {W}x{H} alternating JPEG 4:2:0 / tc8 PNG, encoded bytes in host "
-                                   "memory -> RGBA8 in HBM (zpx_batch_decode_rgba), configs[3] shard"}}
+    st = r.stats
+    out = {"value": round(total * W * H / wall / 1e6, 1), "unit": "MPixels/sec",
+           "per_gpu_mpix_s": round(total * W * H / wall / 1e6 / ws, 1),
+           "images": total, "images_per_gpu": len(plan.owned[rank]), "host_threads_per_rank": st.host_threads,
+           "depth": st.depth, "decode_wall_s": round(wall, 3), "host_cpu_s_rank0": round(st.host_s, 3),
+           "h2d_gb_rank0": round(st.h2d_bytes / 1e9, 3),
+           "config": {"workload": f"{total}x {W}x{H} JPEG 4:2:0 / tc8 PNG (half each per shard), encoded bytes in "
+                                  f"host memory -> RGBA8 in HBM (zpx_batch_decode_rgba), image i -> GPU i mod {ws}"
+                                  + (", RCCL gather to rank 0" if gather else ""), "configs": "configs[3]"}}
+    if gather:
+        gs = max_over_ranks(dist, r.gather_s, "cuda")
+        out["gather"] = {"bytes": plan.gather_bytes, "seconds": round(gs, 4),
+                         "GB_s": round(plan.gather_bytes / gs / 1e9, 1), "collective": "torch.distributed.gather (RCCL)"}
+        if rank == 0:  # spot-check the gathered placement: one image of every rank against its source
+            import numpy as np
+            import oracle_py as O
+
+            want = {k: O.decode(uniq[k]).rgba_pixels() for k in (True, False)}
+            for q in range(ws):
+                i = plan.owned[q][-1]
+                got = r.image(plan, i).reshape(-1).cpu().numpy()
+                if not np.array_equal(got, want[e2e_is_jpeg(i, ws)]):
+                    raise SystemExit(f"gather parity failure: image {i} from rank {q}")
+    del r
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -256,6 +373,15 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
+    # this rank's share of the host (entropy threads + the CPUs they run on)
+    from zpix_amd.shard import rank_cpus
+
+    local_ws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+    threads, cpus = rank_cpus(local, local_ws)
+    if args.host_threads:
+        threads = args.host_threads
+    if ws > 1:
+        os.sched_setaffinity(0, cpus)
 
     from tools import synthetic as S
 
@@ -265,6 +391,7 @@ def main():
     ctx = zpix_amd.context.default(dev)
     W = H = args.size
     result = {}
+    pdatas = []
     # ------------------------------------------------------------ JPEG (headline)
     if not args.png_only:
         t0 = time.perf_counter()
@@ -303,18 +430,6 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        gather = None
-        if args.gather and ws > 1:
-            out = batch.out_arena
-            bufs = [torch.empty_like(out) for _ in range(ws)] if rank == 0 else None
-            torch.cuda.synchronize()
-            dist.barrier()
-            g0 = time.perf_counter()
-            dist.gather(out, gather_list=bufs, dst=0)
-            torch.cuda.synchronize()
-            gt = time.perf_counter() - g0
-            gather = {"bytes": int(out.numel() * (ws - 1)), "seconds": round(gt, 4),
-                      "GB_s": round(out.numel() * (ws - 1) / gt / 1e9, 1)}
         coeff_bits = int(coeffs[0].frame.coeff_bits)
         if traffic is not None and tj.get("coeff_bits", 16) != coeff_bits:
             traffic = None  # measured on the other coefficient transport
@@ -365,8 +480,6 @@ def main():
                          "algorithmic_bytes_per_launch": launch_bytes},
             "host_entropy_mpix_s": round(host_entropy, 1),
         }
-        if gather:
-            result["gather"] = gather
         if int16:
             result["int16_transport"] = int16
         del batch
@@ -391,6 +504,7 @@ def main():
             if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
                 raise SystemExit("parity failure: GPU PNG unfilter != source pixels")
         wall, kern_ms = timed_steps(torch, dist, pb.launch, max(3, args.steps // 2), 1, ws)
+        pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
         steps = max(3, args.steps // 2)
         pv = pb.pixels * ws * steps / wall / 1e6
         ach = pb.bytes / (kern_ms * 1e-3) / 1e9
@@ -418,10 +532,10 @@ def main():
     if not args.no_config5 and not args.png_only:
         result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)
     if not args.no_e2e and not args.png_only:
-        result["end_to_end"] = bench_e2e(args, torch, dist, ws, rank, ctx, S)
+        result["end_to_end"] = bench_e2e(args, torch, dist, ws, rank, ctx, S, threads)
     # ------------------------------------------------------------ CPU baseline (rank 0, N=1)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.png_only:
-        result["cpu_baseline"] = cpu_baseline_jpeg(datas[0], args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(datas[0], pdatas[0] if pdatas else None, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if ws > 1:

@@ -330,6 +330,15 @@ int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames,
 
 /* Enqueue the plan's kernels on `stream` (NULL = the context's stream). */
 int zpx_plan_launch(zpx_plan *plan, void *stream);
+/* Error status of the plan's launches since the last call: ZPX_OK, or
+ * ZPX_E_HIP ("Hip", with zpx_last_error "png wavefront hand-off timed out")
+ * when any PNG wavefront hand-off gave up waiting, i.e. that launch's output
+ * is invalid.  The reference's contract is that every decode step returns an
+ * error union (src/png/decoder.zig:143-221); zpx_plan_launch only enqueues,
+ * so this is where an asynchronous launch reports.  Waits for `stream` (NULL
+ * = the context's stream), then clears the status.  JPEG plans always report
+ * ZPX_OK (their kernels have no wait that can time out). */
+int zpx_plan_status(zpx_plan *plan, void *stream);
 /* Algorithmic bytes (read + written) one launch of the plan moves. */
 uint64_t zpx_plan_bytes(const zpx_plan *plan);
 /* Number of kernel launches one zpx_plan_launch enqueues. */
@@ -422,6 +431,40 @@ typedef struct zpx_batch zpx_batch;
 int zpx_batch_start(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
                     zpx_batch **out);
 int zpx_batch_wait(zpx_batch *b, zpx_batch_stats *stats /* may be NULL */);
+
+/* configs[3] in one process: image i of `items` is
+ * decoded on ctxs[i % ndev] -- one streaming pipeline (zpx_batch_decode_rgba,
+ * `opts` per device) per device, each on its own host thread -- and every
+ * result is gathered into items[i].dst on ctxs[0]'s device: grouped
+ * ncclSend/ncclRecv over RCCL (xGMI) between distinct devices, a device copy
+ * when a context shares device 0's GPU.  items[i].dst are DEVICE pointers on
+ * ctxs[0]'s device (dst_capacity bytes each); every other device decodes into
+ * staging of that capacity first.  Statuses, widths and heights come back in
+ * items as from zpx_batch_decode_rgba.  `stats` sums over the devices (wall_s
+ * = the whole job, gather included); `gather` (may be NULL) splits the wall
+ * time into decode and gather.  The reference has no counterpart (it is
+ * single-threaded, src/root.zig:24-40); per image the result is
+ * zpix.fromBuffer + Image.rgbaPixels (image.zig:103-130). */
+typedef struct zpx_gather_stats {
+    double decode_s;      /* until every device's pipeline finished */
+    double gather_s;      /* the gather to device 0 */
+    double gather_bytes;  /* bytes moved to device 0 */
+    int32_t ndev, pad;
+} zpx_gather_stats;
+int zpx_batch_decode_sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n_items,
+                             const zpx_batch_opts *opts, zpx_batch_stats *stats /* may be NULL */,
+                             zpx_gather_stats *gather /* may be NULL */);
+
+/* ---------------------------------------------------------------------- */
+/* fault injection (tests)                                                 */
+/* ---------------------------------------------------------------------- */
+/* Launches the PNG unfilter kernel on a 2-band image whose second band waits
+ * for a first band that is never scheduled (a producer that never
+ * publishes), with `spin_limit` polls per wait, and returns what
+ * zpx_plan_status reports for it: ZPX_E_HIP when the bounded wait gave up
+ * (the expected outcome).  `seconds` (may be NULL) receives the launch's wall
+ * time, which must stay about one spin limit, not one per step. */
+int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds);
 
 #ifdef __cplusplus
 }

@@ -17,11 +17,31 @@
  *   - the 4-component YCbCrK branch (decoder.zig:811-846, which goes through
  *     the off-by-one image/util.zig drawYCbCr) is reported as Unsupported.
  */
+#define _POSIX_C_SOURCE 200809L
 #include "zpix_oracle.h"
 
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <zlib.h>
+
+/* CPU-baseline stage clock (bench.py cpu_baseline): seconds this thread
+ * spent in PNG filter reconstruction + pixel store (readImagePass and
+ * mergePassInto), so the caller can split png.decode into inflate+parse vs
+ * unfilter+store.  Timing only; no decode result depends on it. */
+static __thread double zo_png_unfilter_s;
+static double zo_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+double zo_png_unfilter_seconds(void)
+{
+    double t = zo_png_unfilter_s;
+    zo_png_unfilter_s = 0;
+    return t;
+}
 
 /* ------------------------------------------------------------------------ */
 /* Error names: the Zig error-set names the path can raise.                 */
@@ -1986,6 +2006,7 @@ static int pd_idat(zo_pdec *d, uint32_t first_len)
         size_t dlen = 0;
         int derr = 0;
         if ((e = inflate_all(all, len, &data, &dlen, &derr))) goto out;
+        const double t_pass = zo_now();
         size_t pos = 0;
         if (d->have_img) zo_image_free(&d->img);
         if ((e = pd_alloc_image(d, &d->img, d->width, d->height))) {
@@ -2027,6 +2048,7 @@ static int pd_idat(zo_pdec *d, uint32_t first_len)
             }
         }
         free(data);
+        zo_png_unfilter_s += zo_now() - t_pass;
     }
 out:
     free(all);

@@ -129,6 +129,10 @@ void zo_jpeg_coeffs_free(zo_jpeg_coeffs *c);
 int zo_png_unfilter(const uint8_t *filtered, uint32_t rows, uint32_t row_bytes,
                     uint32_t bytes_per_pixel, uint8_t *out);
 
+/* CPU-baseline stage clock: seconds the calling thread spent in PNG filter
+ * reconstruction + pixel store (+ Adam7 merge) since the last call; resets. */
+double zo_png_unfilter_seconds(void);
+
 #ifdef __cplusplus
 }
 #endif

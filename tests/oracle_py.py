@@ -93,6 +93,8 @@ def lib():
             C.c_int32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
             C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
         ]
+        L.zo_png_unfilter_seconds.restype = C.c_double
+        L.zo_png_unfilter_seconds.argtypes = []
         _lib = L
     return _lib
 
@@ -250,8 +252,11 @@ def jpeg_coefficients(data: bytes) -> JpegCoeffs:
 
 
 def reconstruct_grids(n_comp, width, height, h, v, mxx, myy, grids, qts_zigzag, progressive,
-                      planes, strides):
-    """zo_jpeg_reconstruct_grids: grids are int32 (nblocks,64) arrays (copied; mutated in C)."""
+                      planes, strides, timing: list | None = None):
+    """zo_jpeg_reconstruct_grids: grids are int32 (nblocks,64) arrays (copied; mutated in C).
+    timing: if given, the C call's wall seconds are appended (CPU-baseline stage split)."""
+    import time
+
     gcopies = [np.ascontiguousarray(g, np.int32).copy() if g is not None else None for g in grids]
     gptrs = (C.c_void_p * 4)(*[g.ctypes.data if g is not None else None for g in gcopies] + [None] * (4 - len(gcopies)))
     qcopies = [np.ascontiguousarray(q, np.int32) for q in qts_zigzag]
@@ -260,9 +265,12 @@ def reconstruct_grids(n_comp, width, height, h, v, mxx, myy, grids, qts_zigzag, 
     harr = (C.c_int32 * 4)(*h[:4])
     varr = (C.c_int32 * 4)(*v[:4])
     sarr = (C.c_size_t * 4)(*list(strides) + [0] * (4 - len(strides)))
+    t0 = time.perf_counter()
     lib().zo_jpeg_reconstruct_grids(n_comp, width, height, C.addressof(harr), C.addressof(varr),
                                     mxx, myy, C.addressof(gptrs), C.addressof(qptrs),
                                     int(progressive), C.addressof(pptrs), C.addressof(sarr))
+    if timing is not None:
+        timing.append(time.perf_counter() - t0)
 
 
 def png_unfilter(filtered: np.ndarray, rows: int, row_bytes: int, bpp: int) -> np.ndarray:
@@ -272,3 +280,8 @@ def png_unfilter(filtered: np.ndarray, rows: int, row_bytes: int, bpp: int) -> n
     if e:
         raise OracleError(error_name(e))
     return out
+
+
+def png_unfilter_seconds() -> float:
+    """Seconds this thread spent in PNG unfilter + pixel store since the last call (CPU-baseline stage split)."""
+    return float(lib().zo_png_unfilter_seconds())

@@ -1,18 +1,21 @@
 """The N>1 path of bench.py on CPU: world_size-2 `gloo` ranks.
 
-Images shard one-per-rank (image i -> rank i mod N) with no
-data-path collective; each rank decodes its shard independently; the only
-collectives are the max-over-ranks wall time and the optional gather of
-results to rank 0.  Here each rank decodes a small sharded batch with the
-oracle (CPU test infrastructure, the GPU path is covered by -m gpu) and rank 0
-checks that the gathered per-image checksums equal an unsharded decode — a
-checksum of checksums, independent of N.
+configs[3]: images shard one-per-rank (image i -> rank i mod N)
+with no data-path collective; each rank decodes its shard into its RGBA arena,
+then one gather moves every arena to rank 0.  These tests drive the SAME
+functions bench.py's end-to-end line uses -- zpix_amd.shard.ShardPlan (the
+placement every rank derives from the header sizes), decode_and_gather (the
+shard decode + arena gather + status gather) and bench.max_over_ranks -- with
+a CPU decode function in place of the GPU pipeline: here each rank decodes
+its images with the oracle (test infrastructure: the device decode itself is
+covered by -m gpu), and rank 0 checks every gathered image, byte for byte,
+against an unsharded decode, plus the error status of a corrupt image.
 """
 import ast
 import os
 import socket
-import zlib
 
+import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -20,8 +23,10 @@ import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
 import bench  # noqa: E402
+from zpix_amd import shard  # noqa: E402
 
-N_IMAGES = 6
+N_IMAGES = 7
+CORRUPT = 5  # a truncated JPEG: its rank reports the reference's error name
 
 
 def _free_port():
@@ -30,32 +35,58 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _decode_checksum(i: int) -> int:
-    import oracle_py as O
+def _image(i: int, ws: int) -> bytes:
     from tools import synthetic as S
 
-    data = S.jpeg_420(i, 48 + 8 * i, 40) if i % 2 == 0 else S.png_tc8_mixed(i, 40 + 8 * i, 24)
-    return zlib.crc32(O.decode(data).rgba_pixels().tobytes())
+    if bench.e2e_is_jpeg(i, ws):
+        d = S.jpeg_420(i, 48 + 8 * i, 40)
+        return d[: len(d) // 2] if i == CORRUPT else d
+    return S.png_tc8_mixed(i, 40 + 8 * i, 24)
+
+
+def _dims(data: bytes):
+    import oracle_py as O
+
+    try:
+        im = O.decode(data)
+        return (im.width, im.height)
+    except O.OracleError:
+        # header-only size, as the GPU path gets it (decodeConfig, host-only):
+        # a truncated scan still has its SOF
+        from zpix_amd.batch import _probe_dims
+
+        return _probe_dims(data)
+
+
+def _oracle_decode_fn(bufs, dsts):
+    """decode_fn for decode_and_gather: the oracle into the (H, W, 4) views."""
+    import oracle_py as O
+
+    statuses = []
+    for b, d in zip(bufs, dsts):
+        try:
+            px = O.decode(b).rgba_pixels()
+        except O.OracleError as e:
+            statuses.append(e.name)
+            continue
+        d.copy_(torch.from_numpy(px).view(d.shape))
+        statuses.append("Ok")
+    return statuses, None
 
 
 def _worker(rank, ws, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
-        mine = bench.shard_images(N_IMAGES, rank, ws)
-        sums = torch.tensor([[i, _decode_checksum(i)] for i in mine], dtype=torch.int64)
-        # ranks may own different counts: pad to the max shard size
-        n = torch.tensor([len(mine)])
-        dist.all_reduce(n, op=dist.ReduceOp.MAX)
-        pad = torch.full((int(n.item()) - len(mine), 2), -1, dtype=torch.int64)
-        sums = torch.cat([sums, pad])
-        bufs = [torch.empty_like(sums) for _ in range(ws)] if rank == 0 else None
-        dist.gather(sums, gather_list=bufs, dst=0)
+        bufs = [_image(i, ws) for i in range(N_IMAGES)]
+        plan = shard.ShardPlan([_dims(b) for b in bufs], ws)
+        r = shard.decode_and_gather(bufs, plan, rank, dist, _oracle_decode_fn, "cpu", gather=True)
         slowest = bench.max_over_ranks(dist, float(rank + 1), "cpu")
         if rank == 0:
-            got = {int(i): int(c) for b in bufs for i, c in b.tolist() if i >= 0}
+            got = {i: (r.statuses[i], r.image(plan, i).reshape(-1).numpy().tobytes().hex()
+                       if r.statuses[i] == "Ok" else None) for i in range(N_IMAGES)}
             with open(os.path.join(out_dir, "result.txt"), "w") as f:
-                f.write(repr((got, slowest)))
+                f.write(repr((got, slowest, r.gather_s is not None, plan.slot_bytes)))
     finally:
         dist.destroy_process_group()
 
@@ -68,15 +99,59 @@ def test_shard_images_partition():
         assert all(len(s) == 512 // ws for s in shards)  # weak scaling: 64 per GPU at N=8
 
 
+def test_e2e_mix_is_half_and_half_on_every_rank():
+    for ws in (1, 2, 4, 8):
+        for r in range(ws):
+            mine = bench.shard_images(64 * ws, r, ws)
+            kinds = [bench.e2e_is_jpeg(i, ws) for i in mine]
+            assert sum(kinds) == len(mine) // 2, (ws, r)
+
+
+def test_shard_plan_placement():
+    dims = [(16, 8), None, (4, 4), (100, 3), (7, 9)]
+    p = shard.ShardPlan(dims, 2)
+    assert p.owned == [[0, 2, 4], [1, 3]]
+    # arena offsets are 256-aligned, non-overlapping, and fit the padded slot
+    for r in range(2):
+        spans = sorted((p.offset[i], p.offset[i] + p.nbytes(i)) for i in p.owned[r])
+        assert all(a % 256 == 0 for a, _ in spans)
+        assert all(spans[k][1] <= spans[k + 1][0] for k in range(len(spans) - 1))
+        assert spans[-1][1] <= p.slot_bytes
+    assert p.slot_bytes == max(p.arena_bytes)
+    assert p.gathered_offset(3) == p.slot_bytes + p.offset[3]
+    assert p.gather_bytes == p.slot_bytes
+
+
+def test_rank_cpus_split():
+    threads, cpus = shard.rank_cpus(0, 1)
+    assert threads == shard.host_cpu_budget() and set(cpus) == set(os.sched_getaffinity(0))
+    n = len(os.sched_getaffinity(0))
+    if n >= 2:
+        t0, c0 = shard.rank_cpus(0, 2)
+        t1, c1 = shard.rank_cpus(1, 2)
+        assert not set(c0) & set(c1) and len(c0) == len(c1) == n // 2
+        assert t0 == t1 == max(1, shard.host_cpu_budget() // 2)
+
+
 def test_max_over_ranks_single_process():
     assert bench.max_over_ranks(None, 1.5, "cpu") == 1.5
 
 
-def test_gloo_world2_sharded_decode(tmp_path):
+def test_gloo_world2_sharded_decode_and_gather(tmp_path):
+    import oracle_py as O
+
     ws = 2
     mp.spawn(_worker, args=(ws, _free_port(), str(tmp_path)), nprocs=ws, join=True)
-    got, slowest = ast.literal_eval(open(tmp_path / "result.txt").read())
-    assert slowest == float(ws)
+    got, slowest, gathered, slot = ast.literal_eval(open(tmp_path / "result.txt").read())
+    assert slowest == float(ws) and gathered and slot % 256 == 0
     assert sorted(got) == list(range(N_IMAGES))
     for i in range(N_IMAGES):
-        assert got[i] == _decode_checksum(i), i
+        data = _image(i, ws)
+        if i == CORRUPT:
+            with pytest.raises(O.OracleError) as e:
+                O.decode(data)
+            assert got[i] == (e.value.name, None)
+            continue
+        want = O.decode(data).rgba_pixels()
+        assert got[i][0] == "Ok", i
+        assert np.array_equal(np.frombuffer(bytes.fromhex(got[i][1]), np.uint8), want), i

@@ -226,3 +226,17 @@ def test_jpeg_batch_planes_matches_oracle():
     want = O.jpeg_decode(data)
     got = batch.output_tensor(0).cpu().numpy()
     assert np.array_equal(got, want.pixels)
+
+
+def test_jpeg_progressive_444_4k_matches_oracle():
+    """configs[4] JPEG at its bench size: a 4096^2 progressive 4:4:4 frame
+    (786,432 blocks, reconstructProgressiveImage's block rule) through the
+    fused kernel, bit-exact against the oracle's jpeg.decode + rgbaPixels."""
+    data = S.jpeg_progressive_444(1000, 4096, 4096)
+    co = J.Coefficients(data)
+    batch = device.JpegBatch([co], slots=[0, 0], output="rgba")
+    batch.launch(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = torch.from_numpy(O.jpeg_decode(data).rgba_pixels().reshape(4096, 4096, 4))
+    for s in range(2):
+        assert torch.equal(batch.output_tensor(s).cpu(), want)

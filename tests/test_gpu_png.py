@@ -153,3 +153,19 @@ def test_rgba_pixels_every_kind(where, name):
     got = zpix_amd.from_buffer(data)
     assert got.kind == want.kind
     assert np.array_equal(got.rgba_pixels(), want.rgba_pixels())
+
+
+def test_png_adam7_rgba16_4k_matches_oracle():
+    """configs[4] PNG at its bench size: 4096^2 Adam7 RGBA16 -> NRGBA64 (7
+    passes scattered by mergePassInto), bit-exact against the oracle, twice
+    through one plan (relaunch), plus zpx_plan_status."""
+    data = S.png_rgba16_adam7(2000, 4096, 4096)
+    want = O.png_decode(data).pixels
+    st = P.Stream(data)
+    batch = device.PngBatch([st], slots=[0, 0])
+    for _ in range(2):
+        batch.launch(torch.cuda.current_stream().cuda_stream)
+    batch.status(torch.cuda.current_stream().cuda_stream)
+    for s in range(2):
+        got = batch.output_tensor(s).cpu().numpy()
+        assert np.array_equal(got.reshape(-1)[:want.size], want.reshape(-1))

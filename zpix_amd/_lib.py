@@ -127,6 +127,11 @@ class zpx_batch_stats(C.Structure):
     ]
 
 
+class zpx_gather_stats(C.Structure):
+    _fields_ = [("decode_s", C.c_double), ("gather_s", C.c_double), ("gather_bytes", C.c_double),
+                ("ndev", C.c_int32), ("pad", C.c_int32)]
+
+
 # every symbol include/zpix_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "zpx_error_name", "zpx_last_error", "zpx_ctx_create", "zpx_ctx_destroy", "zpx_ctx_stream",
@@ -137,7 +142,8 @@ EXPORTS = [
     "zpx_plan_kernel_count", "zpx_plan_destroy", "zpx_dev_rgba_pixels", "zpx_jpeg_entropy_decode",
     "zpx_jpeg_coeffs_frame", "zpx_jpeg_coeffs_free", "zpx_jpeg_coeffs_widen", "zpx_png_inflate", "zpx_png_stream_frame",
     "zpx_png_stream_data", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
-    "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config",
+    "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config", "zpx_plan_status",
+    "zpx_batch_decode_sharded", "zpx_debug_png_stall",
 ]
 
 _lib = None
@@ -194,6 +200,11 @@ def lib():
         "zpx_jpeg_decode_config": (i32, [C.c_char_p, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                          C.POINTER(C.c_int32)]),
         "zpx_png_decode_config": (i32, [C.c_char_p, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "zpx_plan_status": (i32, [vp, vp]),
+        "zpx_batch_decode_sharded": (i32, [C.POINTER(vp), i32, C.POINTER(zpx_batch_item), i32,
+                                           C.POINTER(zpx_batch_opts), C.POINTER(zpx_batch_stats),
+                                           C.POINTER(zpx_gather_stats)]),
+        "zpx_debug_png_stall": (i32, [vp, C.c_uint32, C.POINTER(C.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -83,6 +83,7 @@ struct CtxScope { // make ctx->device current for this call
 };
 
 struct JpegCoeffs;
+struct HostBuf;
 struct DevJpegFrame;
 struct DevPngPass;
 struct DevImage;
@@ -95,6 +96,18 @@ int launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_frame,
 void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
                       uint64_t &bytes);
 DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette);
+// planes + colour pass for frames the fused kernel does not take (async on st)
+int jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, DevBuf &planes, DevBuf &desc,
+                        HostBuf &hdesc, uint8_t *out, hipStream_t st);
+
+// The unfilter kernel addresses one band (64 filtered rows + the input pad)
+// through a buffer descriptor with a 31-bit byte range, and row offsets in
+// 32-bit registers: a pass whose band would exceed it is rejected
+// (ZPX_E_UNSUPPORTED) instead of silently reading zeros past 2 GiB.
+inline bool png_band_fits(uint32_t max_row_bytes)
+{
+    return 64ull * (uint64_t(max_row_bytes) + 1) + ZPX_PNG_INPUT_PAD + 4 < 0x7ffffff0ull;
+}
 
 // PNG band schedule (the ticket order of png_unfilter_kernel). Bands are
 // ordered by the first output row they write, then by pass: band b of a pass

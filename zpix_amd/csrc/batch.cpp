@@ -79,6 +79,7 @@ struct Slot {
     std::unique_ptr<Decoded> dec;
     bool busy = false;
     bool check_png = false;
+    bool failed = false; // the image failed after its slot was bound (status already set)
 };
 
 bool host_reserve(HostBuf &b, size_t n) { return b.bytes >= n || b.alloc(n, false); }
@@ -120,6 +121,7 @@ class Pipeline {
     std::mutex mu_;
     std::condition_variable cv_ready_, cv_token_;
     std::deque<std::unique_ptr<Decoded>> ready_;
+    std::vector<int> oom_items_; // items a worker could not even allocate for
     int tokens_ = 0;
     bool stop_ = false;
     std::atomic<int> next_{0};
@@ -160,7 +162,13 @@ void Pipeline::worker()
             if (stop_) return;
             tokens_--;
         }
-        std::unique_ptr<Decoded> d(new Decoded);
+        std::unique_ptr<Decoded> d(new (std::nothrow) Decoded);
+        if (!d) { // out of memory: report on the item, keep the pipeline going
+            std::lock_guard<std::mutex> lk(mu_);
+            oom_items_.push_back(i);
+            cv_ready_.notify_one();
+            continue;
+        }
         d->item = i;
         const zpx_batch_item &it = items_[i];
         const double t0 = now_s();
@@ -246,25 +254,11 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
     const uint32_t W = f.width, H = f.height;
     const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
     const JpegOut kind = jpeg_output_kind(d.jc);
-    if (kind == JpegOut::CMYK || kind == JpegOut::YCCK || !jpeg_fusable(f)) {
-        // planes + colour pass through the per-image entry point (synchronous)
-        uint8_t *rgba = nullptr;
-        size_t rlen = 0;
-        uint32_t w = 0, h = 0;
-        int e = zpx_jpeg_decode_rgba(ctx_, nullptr, it.buf, it.len, &rgba, &rlen, &w, &h);
-        if (!e) {
-            if (on_host_) {
-                for (uint32_t y = 0; y < h; y++) memcpy(it.dst + y * stride, rgba + size_t(y) * w * 4, size_t(w) * 4);
-                d2h_bytes_ += double(w) * h * 4; // came back over PCIe inside zpx_jpeg_decode_rgba
-            } else {
-                hipError_t he = hipMemcpy2D(it.dst, stride, rgba, size_t(w) * 4, size_t(w) * 4, h, hipMemcpyHostToDevice);
-                if (he != hipSuccess) e = hip_fail(ctx_, he, "batch: rgba upload");
-            }
-            free(rgba);
-        }
-        it.status = e;
+    const bool fused = kind != JpegOut::CMYK && kind != JpegOut::YCCK && jpeg_fusable(f);
+    if (kind == JpegOut::YCCK || (d.jc.n_comp == 4 && !d.jc.adobe_valid)) { // jpeg.decode's own errors
+        it.status = kind == JpegOut::YCCK ? ZPX_E_UNSUPPORTED : ZPX_E_UNSUPPORTED_COLOR_MODEL;
         sync_done = true;
-        return e == ZPX_E_HIP ? e : ZPX_OK;
+        return ZPX_OK;
     }
     // fused dequant + IDCT + upsample + colour straight into the destination
     size_t total = 0;
@@ -281,6 +275,29 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
     }
     HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
     HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
+    if (!fused) {
+        // planes + colour pass from the coefficients this worker already
+        // decoded (no second entropy decode, no host sync): CMYK, Adobe RGB
+        // with non-interleaved scans, ...; the colour kernels write 4W rows
+        const bool direct = !on_host_ && stride == size_t(W) * 4;
+        uint8_t *out = it.dst;
+        if (!direct) {
+            HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+            out = s.dout.as<uint8_t>();
+        }
+        if (int e = jpeg_planes_to_rgba(ctx_, d.jc, f, s.dimg, s.ddesc, s.hdesc, out, ctx_->stream)) {
+            if (e == ZPX_E_HIP) return e;
+            it.status = e; // the image's own error; the slot's queued copy is harmless
+            HIPCHK(ctx_, hipEventRecord(s.ev_done, ctx_->stream));
+            s.failed = true;
+            return ZPX_OK;
+        }
+        if (direct) {
+            HIPCHK(ctx_, hipEventRecord(s.ev_done, ctx_->stream));
+            return ZPX_OK;
+        }
+        return finish_copy(s, out, size_t(W) * 4, W, H, ctx_->stream);
+    }
     const bool direct = !on_host_;
     uint8_t *out;
     if (direct) {
@@ -439,15 +456,25 @@ int Pipeline::issue(Slot &s, bool &sync_done)
         sync_done = true;
         return ZPX_OK;
     }
+    if (d.fmt == 2)
+        for (int p = 0; p < d.ps.npasses; p++)
+            if (!png_band_fits(d.ps.pass[p].row_bytes)) { // beyond the kernel's band range
+                it.status = ZPX_E_UNSUPPORTED;
+                sync_done = true;
+                return ZPX_OK;
+            }
     sync_done = false;
     s.check_png = false;
+    s.failed = false;
     return d.fmt == 1 ? issue_jpeg(s, sync_done) : issue_png(s);
 }
 
 void Pipeline::retire(Slot &s)
 {
     zpx_batch_item &it = items_[s.dec->item];
-    if (s.check_png && *static_cast<volatile uint32_t *>(s.hstatus.ptr) != 0) {
+    if (s.failed) {
+        // it.status holds the image's error
+    } else if (s.check_png && *static_cast<volatile uint32_t *>(s.hstatus.ptr) != 0) {
         ctx_->last_error = "png wavefront hand-off timed out";
         it.status = ZPX_E_HIP;
     } else {
@@ -479,16 +506,23 @@ int Pipeline::run(zpx_batch_stats *stats)
         std::unique_ptr<Decoded> d;
         bool any_busy = false;
         for (auto &s : slots_) any_busy |= s->busy;
+        std::vector<int> oom;
         {
             std::unique_lock<std::mutex> lk(mu_);
-            if (ready_.empty()) {
+            if (ready_.empty() && oom_items_.empty()) {
                 if (any_busy) cv_ready_.wait_for(lk, std::chrono::microseconds(100));
-                else cv_ready_.wait(lk, [&] { return !ready_.empty(); });
+                else cv_ready_.wait(lk, [&] { return !ready_.empty() || !oom_items_.empty(); });
             }
             if (!ready_.empty()) {
                 d = std::move(ready_.front());
                 ready_.pop_front();
             }
+            oom.swap(oom_items_);
+        }
+        for (int i : oom) {
+            items_[i].status = ZPX_E_OUT_OF_MEMORY;
+            done++;
+            give_token();
         }
         if (d) {
             if (d->status != ZPX_OK) {

@@ -32,13 +32,14 @@ HostBuf &HostBuf::operator=(HostBuf &&o) noexcept
 
 static bool pinned_allowed()
 {
-    static int ok = -1;
-    if (ok < 0) {
+    // function-local static: initialised once, thread-safe (batch workers
+    // allocate concurrently)
+    static const bool ok = [] {
         const char *env = getenv("ZPX_NO_PINNED");
         int n = 0;
-        ok = (!(env && env[0] == '1') && hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
-    }
-    return ok == 1;
+        return !(env && env[0] == '1') && hipGetDeviceCount(&n) == hipSuccess && n > 0;
+    }();
+    return ok;
 }
 
 namespace {
@@ -905,15 +906,19 @@ int Decoder::run()
 
 int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out)
 {
-    Decoder d(buf, len, out);
-    if (int e = d.run()) return e;
-    // one width per frame (the kernels take one coefficient type per frame)
-    int bits = 8;
-    for (int i = 0; i < 4; i++)
-        if (out.has_grid[i]) bits = std::max(bits, out.grid[i].bits());
-    for (int i = 0; i < 4; i++)
-        if (out.has_grid[i] && !out.grid[i].widen_to(bits)) return ZPX_E_OUT_OF_MEMORY;
-    return ZPX_OK;
+    try { // no exception crosses the ABI
+        Decoder d(buf, len, out);
+        if (int e = d.run()) return e;
+        // one width per frame (the kernels take one coefficient type per frame)
+        int bits = 8;
+        for (int i = 0; i < 4; i++)
+            if (out.has_grid[i]) bits = std::max(bits, out.grid[i].bits());
+        for (int i = 0; i < 4; i++)
+            if (out.has_grid[i] && !out.grid[i].widen_to(bits)) return ZPX_E_OUT_OF_MEMORY;
+        return ZPX_OK;
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
 }
 
 int jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h, int &model)

@@ -22,9 +22,12 @@ int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int 
 int png_chunk_bytes(int depth);
 // uint64 granules of boundary buffer per band for rows of up to max_row_bytes
 int png_band_granules(int depth, uint32_t max_row_bytes);
-// ctl: 4 device words {epoch, ticket, status, pad}; boundary: nbands * band_granules
+// ctl: 4 device words {epoch, ticket, status, pad}; boundary: nbands * band_granules.
+// spin_limit: polls per boundary wait before the launch gives up and sets
+// the status word (0 = the default, env ZPX_PNG_SPIN_LIMIT or 2^20).
 int launch_png_unfilter(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                        uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s);
+                        uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s,
+                        uint32_t spin_limit = 0);
 
 // color_kernels.hip
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);

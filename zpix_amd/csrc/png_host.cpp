@@ -311,7 +311,8 @@ int Parser::idat(uint32_t first_len)
             total += n;
             p += size_t(n) + 12;
         }
-        all.reserve(total);
+        // the lengths are untrusted: never reserve more than the input holds
+        all.reserve(std::min(total, len_ - pos_));
     }
     auto take = [&](uint32_t n) -> int {
         if (len_ - pos_ < n) {
@@ -410,8 +411,12 @@ int Parser::run(bool header_only)
 
 int png_parse(const uint8_t *buf, size_t len, PngStream &out)
 {
-    Parser p(buf, len, out);
-    return p.run();
+    try { // no exception crosses the ABI (std::bad_alloc on a huge stream)
+        Parser p(buf, len, out);
+        return p.run();
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
 }
 
 int png_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h)

@@ -63,9 +63,8 @@ constexpr bool kCoopLoad = ZPX_PNG_COOP_LOAD != 0; // group input: 8 lanes per r
 constexpr int stage_pieces(int gd) { return (12 + 4 * gd + 15) / 16; } // window start is 16-aligned, <= 12 B early
 constexpr int stage_dw(int gd) { return stage_pieces(gd) <= 8 ? 36 : 44; }
 #ifndef ZPX_PNG_SPIN_LIMIT
-#define ZPX_PNG_SPIN_LIMIT (1u << 20)
+#define ZPX_PNG_SPIN_LIMIT (1u << 20) // default polls per wait (ZPX_PNG_SPIN_LIMIT env overrides at launch)
 #endif
-constexpr uint32_t kSpinLimit = ZPX_PNG_SPIN_LIMIT;
 #ifndef ZPX_PNG_SLEEP
 #define ZPX_PNG_SLEEP 2 // s_sleep between boundary polls (units of 64 cycles)
 #endif
@@ -464,7 +463,8 @@ __device__ __forceinline__ void pack_chunk16(const DevPngPass &ps, const uint32_
 template <int DEPTH>
 __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__restrict__ passes,
                                                           const DevPngBand *__restrict__ sched, uint32_t nsched,
-                                                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules)
+                                                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules,
+                                                          uint32_t spin_limit)
 {
     using Tr = Traits<DEPTH>;
     constexpr int BPP = Tr::kBpp, C = Tr::kC, CW = Tr::kCW;
@@ -701,8 +701,17 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                         // this chunk's granules (publication order is not visibility
                         // order), and at a window's start also its last chunk
                         if (chunk_ready(wi) && (wi != 0 || chunk_ready(last))) break;
-                        if (++spins > kSpinLimit) {
+                        // after a timeout (this wave's, or any wave's: the status
+                        // word, checked every 256 polls) never spin again: the
+                        // launch's result is already an error, and a stalled
+                        // producer must cost one spin limit, not one per step
+                        if (timed_out) break;
+                        ++spins;
+                        if (spins > spin_limit ||
+                            ((spins & 255) == 0 &&
+                             __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
                             timed_out = true;
+                            if (lane == 0) atomicOr(status, 1u);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
@@ -895,15 +904,16 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
             if (lane == 0 && ps.max_index) atomicMax(ps.max_index, maxidx);
         }
     }
-    if (timed_out && lane == 0) atomicOr(status, 1u);
 }
 
 // Per-launch control block: epoch++ (fresh granule tags, so the boundary
-// buffer never needs clearing), ticket = 0, status = 0.
+// buffer never needs clearing), ticket = 0, the previous launch's status
+// folded into the sticky word (read and cleared by zpx_plan_status), status = 0.
 __global__ void png_ctl_kernel(uint32_t *ctl)
 {
     ctl[0] += 1;
     ctl[1] = 0;
+    ctl[3] |= ctl[2];
     ctl[2] = 0;
 }
 
@@ -930,9 +940,19 @@ int cus()
     return n;
 }
 
+uint32_t default_spin_limit()
+{
+    static const uint32_t n = [] {
+        const char *e = getenv("ZPX_PNG_SPIN_LIMIT");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? static_cast<uint32_t>(v) : static_cast<uint32_t>(ZPX_PNG_SPIN_LIMIT);
+    }();
+    return n;
+}
+
 template <int DEPTH>
 void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl, uint64_t *boundary,
-              uint32_t band_granules, hipStream_t s)
+              uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
 {
     static const bool trace = getenv("ZPX_BATCH_TRACE") != nullptr;
     if (trace) fprintf(stderr, "[zpx png] launch depth %d nsched %u\n", DEPTH, nsched);
@@ -942,7 +962,7 @@ void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched
     hipLaunchKernelGGL(png_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
     if (trace) fprintf(stderr, "[zpx png] unfilter kernel\n");
     hipLaunchKernelGGL((png_unfilter_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
-                       band_granules);
+                       band_granules, spin_limit ? spin_limit : default_spin_limit());
     if (trace) fprintf(stderr, "[zpx png] launched\n");
 }
 
@@ -965,10 +985,11 @@ int png_band_granules(int depth, uint32_t max_row_bytes)
 }
 
 int launch_png_unfilter(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                        uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s)
+                        uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s,
+                        uint32_t spin_limit)
 {
     switch (depth) {
-#define ZPX_CASE(D) case D: launch_t<D>(passes, sched, nsched, ctl, boundary, band_granules, s); break;
+#define ZPX_CASE(D) case D: launch_t<D>(passes, sched, nsched, ctl, boundary, band_granules, spin_limit, s); break;
         ZPX_CASE(ZPX_PNG_G1) ZPX_CASE(ZPX_PNG_G2) ZPX_CASE(ZPX_PNG_G4) ZPX_CASE(ZPX_PNG_G8)
         ZPX_CASE(ZPX_PNG_GA8) ZPX_CASE(ZPX_PNG_TC8) ZPX_CASE(ZPX_PNG_P1) ZPX_CASE(ZPX_PNG_P2)
         ZPX_CASE(ZPX_PNG_P4) ZPX_CASE(ZPX_PNG_P8) ZPX_CASE(ZPX_PNG_TCA8) ZPX_CASE(ZPX_PNG_G16)

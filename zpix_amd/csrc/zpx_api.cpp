@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -41,6 +42,17 @@ extern "C" const char *zpx_last_error(const zpx_ctx *ctx) { return ctx ? ctx->la
 
 namespace {
 
+// Runs an entry point's body so that no C++ exception crosses the C-ABI
+// (include/zpix_amd.h: "No exception or abort crosses the ABI").
+template <typename F> int guarded(F &&f) noexcept
+{
+    try {
+        return f();
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+}
+
 int read_file(const char *path, std::vector<uint8_t> &out)
 {
     FILE *f = fopen(path, "rb");
@@ -61,7 +73,7 @@ int read_file(const char *path, std::vector<uint8_t> &out)
 } // namespace
 
 // ------------------------------------------------------------------ context
-extern "C" int zpx_ctx_create(int device, zpx_ctx **out)
+static int zpx_ctx_create_impl(int device, zpx_ctx **out)
 {
     if (!out) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
@@ -74,6 +86,11 @@ extern "C" int zpx_ctx_create(int device, zpx_ctx **out)
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return ZPX_E_HIP;
     *out = c.release();
     return ZPX_OK;
+}
+
+extern "C" int zpx_ctx_create(int device, zpx_ctx **out)
+{
+    return guarded([&] { return zpx_ctx_create_impl(device, out); });
 }
 
 extern "C" void zpx_ctx_destroy(zpx_ctx *ctx)
@@ -135,7 +152,7 @@ extern "C" int zpx_dev_rgba_pixels(zpx_ctx *ctx, const zpx_image *img, uint8_t *
     return ZPX_OK;
 }
 
-extern "C" int zpx_image_rgba_pixels(zpx_ctx *ctx, const zpx_allocator *al, const zpx_image *img, uint8_t **out,
+static int zpx_image_rgba_pixels_impl(zpx_ctx *ctx, const zpx_allocator *al, const zpx_image *img, uint8_t **out,
                                      size_t *out_len)
 {
     if (!ctx || !img || !out || !out_len) return ZPX_E_INVALID_ARGUMENT;
@@ -167,6 +184,12 @@ extern "C" int zpx_image_rgba_pixels(zpx_ctx *ctx, const zpx_allocator *al, cons
     *out = host;
     *out_len = n;
     return ZPX_OK;
+}
+
+extern "C" int zpx_image_rgba_pixels(zpx_ctx *ctx, const zpx_allocator *al, const zpx_image *img, uint8_t **out,
+                                     size_t *out_len)
+{
+    return guarded([&] { return zpx_image_rgba_pixels_impl(ctx, al, img, out, out_len); });
 }
 
 // ------------------------------------------------------------------ plans
@@ -210,6 +233,77 @@ int zpx::launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_f
     const int hc = f.n_comp == 3 ? f.h[1] : 1, vc = f.n_comp == 3 ? f.v[1] : 1;
     return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits, f.narrow != 0, st);
 }
+// jpeg.decode's planes (reconstructBlock into makeImg's layout) followed by
+// the colour pass of Image.rgbaPixels, for the frames the fused kernel does
+// not take: Adobe RGB (convertToRGB, decoder.zig:751-783), CMYK (applyBlack,
+// :792-902), Gray/YCbCr from non-interleaved scans.  `f` carries DEVICE
+// coefficient pointers; everything is enqueued on `st` (no host sync): the
+// planes go to `planes`, the descriptor through pinned `hdesc` to `desc`, and
+// RGBA8 (stride 4W) to `out`.
+int zpx::jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, DevBuf &planes, DevBuf &desc,
+                             HostBuf &hdesc, uint8_t *out, hipStream_t st)
+{
+    const JpegOut kind = jpeg_output_kind(c);
+    if (c.n_comp == 4 && !c.adobe_valid) return ZPX_E_UNSUPPORTED_COLOR_MODEL; // applyBlack :793-795
+    if (kind == JpegOut::YCCK) {
+        ctx->last_error = "YCbCrK (Adobe transform 2) goes through image/util.zig drawYCbCr: out of scope";
+        return ZPX_E_UNSUPPORTED;
+    }
+    JpegLayout L;
+    if (int e = jpeg_layout(c, L)) return e;
+    const size_t kofs = (L.total + 255) & ~size_t(255);
+    HIPCHK(ctx, planes.reserve(kofs + L.k_total));
+    HIPCHK(ctx, hipMemsetAsync(planes.ptr, 0, kofs + L.k_total, st)); // makeImg zeroes (image.zig:505-507)
+    uint8_t *pb = planes.as<uint8_t>();
+    f.planes[0] = pb;
+    f.strides[0] = L.y_stride;
+    if (c.n_comp >= 3) {
+        f.planes[1] = pb + L.cb_off;
+        f.planes[2] = pb + L.cr_off;
+        f.strides[1] = f.strides[2] = L.c_stride;
+    }
+    if (c.n_comp == 4) {
+        f.planes[3] = pb + kofs;
+        f.strides[3] = L.k_stride;
+    }
+    const DevJpegFrame df = dev_jpeg_frame(f);
+    if (hdesc.bytes < sizeof(df) && !hdesc.alloc(sizeof(df), false)) return ZPX_E_OUT_OF_MEMORY;
+    memcpy(hdesc.ptr, &df, sizeof(df));
+    HIPCHK(ctx, desc.reserve(sizeof(df)));
+    HIPCHK(ctx, hipMemcpyAsync(desc.ptr, hdesc.ptr, sizeof(df), hipMemcpyHostToDevice, st));
+    int gw = 0, gh = 0;
+    for (int i = 0; i < f.n_comp; i++) {
+        gw = std::max(gw, f.mxx * df.h[i]);
+        gh = std::max(gh, f.myy * df.v[i]);
+    }
+    if (launch_jpeg_planar(desc.as<DevJpegFrame>(), 1, gw, gh, f.coeff_bits, f.narrow != 0, st))
+        return hip_fail(ctx, hipGetLastError(), "jpeg planar kernel");
+    zpx_image planar{};
+    planar.kind = c.n_comp == 1 ? ZPX_GRAY : ZPX_YCBCR;
+    planar.max_x = static_cast<int32_t>(c.width);
+    planar.max_y = static_cast<int32_t>(c.height);
+    planar.stride = L.y_stride;
+    planar.y_stride = L.y_stride;
+    planar.c_stride = L.c_stride;
+    planar.cb_off = L.cb_off;
+    planar.cr_off = L.cr_off;
+    planar.subsample = L.subsample;
+    const DevImage m = dev_image_of(&planar, pb, nullptr);
+    int rc;
+    if (kind == JpegOut::RGB) {
+        rc = launch_jpeg_rgb(m, c.comp[0].h / c.comp[1].h, out, st);
+    } else if (kind == JpegOut::CMYK) {
+        uint32_t sub = 0;
+        for (int t = 0; t < 4; t++)
+            if (c.comp[t].h != c.comp[0].h || c.comp[t].v != c.comp[0].v) sub |= 1u << t;
+        rc = launch_jpeg_cmyk(m, pb + kofs, L.k_stride, sub, out, st);
+    } else {
+        rc = launch_rgba_pixels(m, out, st); // Gray / YCbCr: Color.toRGBA (color.zig:90-126)
+    }
+    if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg colour kernel");
+    return ZPX_OK;
+}
+
 struct JpegGroup {
     DevBuf frames;
     int n = 0;
@@ -230,10 +324,11 @@ struct zpx_plan {
     int kind = 0; // 0 jpeg planes, 1 jpeg rgba, 2 png
     std::vector<std::unique_ptr<JpegGroup>> jpeg;
     std::vector<std::unique_ptr<PngGroup>> png;
+    HostBuf status_host; // pinned: per PNG group {status, sticky status}
     uint64_t bytes = 0;
 };
 
-extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, int n_frames, int output,
+static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames, int n_frames, int output,
                                     zpx_plan **out)
 {
     if (!ctx || !frames || n_frames <= 0 || !out) return ZPX_E_INVALID_ARGUMENT;
@@ -306,6 +401,12 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
     return ZPX_OK;
 }
 
+extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, int n_frames, int output,
+                                    zpx_plan **out)
+{
+    return guarded([&] { return zpx_jpeg_plan_create_impl(ctx, frames, n_frames, output, out); });
+}
+
 static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPass> &passes_in,
                            const std::vector<uint32_t> &pass_rowbytes)
 {
@@ -318,6 +419,10 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
         base += p.nbands;
         max_bands = std::max(max_bands, p.nbands);
         max_rb = std::max(max_rb, pass_rowbytes[i]);
+    }
+    if (!png_band_fits(max_rb)) {
+        ctx->last_error = "png: a 64-row band of this image exceeds the kernel's 2 GiB band range";
+        return ZPX_E_UNSUPPORTED;
     }
     const std::vector<DevPngBand> sched = png_schedule(passes); // output-row order (api_internal.h)
     g.nsched = static_cast<uint32_t>(sched.size());
@@ -403,7 +508,7 @@ static int png_out_bpp(int depth, bool trns)
     }
 }
 
-extern "C" int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames, zpx_plan **out)
+static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames, zpx_plan **out)
 {
     if (!ctx || !frames || n_frames <= 0 || !out) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
@@ -435,6 +540,11 @@ extern "C" int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, in
     return ZPX_OK;
 }
 
+extern "C" int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames, zpx_plan **out)
+{
+    return guarded([&] { return zpx_png_plan_create_impl(ctx, frames, n_frames, out); });
+}
+
 extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
 {
     if (!plan) return ZPX_E_INVALID_ARGUMENT;
@@ -459,18 +569,40 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
     return ZPX_OK;
 }
 
-// Reads the status word of a finished PNG plan (wavefront spin timeout).
-static int png_plan_status(zpx_plan *plan)
+// zpx_plan_status: control words {epoch, ticket, status, sticky}. The
+// kernel sets `status` for its own launch; png_ctl_kernel folds it into
+// `sticky` at the next launch's start, so a timeout in any launch since the
+// last call is reported, not only the last launch's.
+static int zpx_plan_status_impl(zpx_plan *plan, void *stream)
 {
-    for (auto &g : plan->png) {
-        uint32_t st = 0;
-        HIPCHK(plan->ctx, hipMemcpy(&st, g->scratch.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost));
-        if (st) {
-            plan->ctx->last_error = "png wavefront hand-off timed out";
+    if (!plan) return ZPX_E_INVALID_ARGUMENT;
+    zpx_ctx *ctx = plan->ctx;
+    CtxScope s(ctx);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (plan->png.empty()) {
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        return ZPX_OK;
+    }
+    const size_t n = plan->png.size();
+    if (plan->status_host.bytes < n * 8 && !plan->status_host.alloc(n * 8, true)) return ZPX_E_OUT_OF_MEMORY;
+    uint32_t *h = static_cast<uint32_t *>(plan->status_host.ptr);
+    for (size_t i = 0; i < n; i++) {
+        uint32_t *ctl = plan->png[i]->scratch.as<uint32_t>();
+        HIPCHK(ctx, hipMemcpyAsync(h + 2 * i, ctl + 2, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemsetAsync(ctl + 2, 0, 8, st));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (size_t i = 0; i < n; i++)
+        if (h[2 * i] | h[2 * i + 1]) {
+            ctx->last_error = "png wavefront hand-off timed out";
             return ZPX_E_HIP;
         }
-    }
     return ZPX_OK;
+}
+
+extern "C" int zpx_plan_status(zpx_plan *plan, void *stream)
+{
+    return guarded([&] { return zpx_plan_status_impl(plan, stream); });
 }
 
 extern "C" uint64_t zpx_plan_bytes(const zpx_plan *plan) { return plan ? plan->bytes : 0; }
@@ -493,7 +625,7 @@ struct zpx_png_stream {
     PngStream s;
 };
 
-extern "C" int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
+static int zpx_jpeg_entropy_decode_impl(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
 {
     if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
@@ -501,6 +633,11 @@ extern "C" int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_
     if (int e = jpeg_entropy_decode(buf, len, c->c)) return e;
     *out = c.release();
     return ZPX_OK;
+}
+
+extern "C" int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
+{
+    return guarded([&] { return zpx_jpeg_entropy_decode_impl(buf, len, out); });
 }
 
 void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes)
@@ -554,7 +691,7 @@ extern "C" int zpx_jpeg_coeffs_widen(zpx_jpeg_coeffs *cc, int bits)
     return ZPX_OK;
 }
 
-extern "C" int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out)
+static int zpx_png_inflate_impl(const uint8_t *buf, size_t len, zpx_png_stream **out)
 {
     if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
@@ -562,6 +699,11 @@ extern "C" int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **
     if (int e = png_parse(buf, len, s->s)) return e;
     *out = s.release();
     return ZPX_OK;
+}
+
+extern "C" int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out)
+{
+    return guarded([&] { return zpx_png_inflate_impl(buf, len, out); });
 }
 
 extern "C" int zpx_png_stream_frame(const zpx_png_stream *ss, zpx_png_frame *f, size_t *filtered_len)
@@ -623,7 +765,7 @@ int run_plan_once(zpx_ctx *ctx, const zpx_jpeg_frame &f, int output)
 
 } // namespace
 
-extern "C" int zpx_jpeg_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+static int zpx_jpeg_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
 {
     if (!ctx || !out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     memset(out, 0, sizeof(*out));
@@ -723,7 +865,12 @@ extern "C" int zpx_jpeg_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint
     return ZPX_OK;
 }
 
-extern "C" int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+extern "C" int zpx_jpeg_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+{
+    return guarded([&] { return zpx_jpeg_decode_impl(ctx, al, buf, len, out); });
+}
+
+static int zpx_jpeg_decode_rgba_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
                                     uint8_t **rgba, size_t *rgba_len, uint32_t *width, uint32_t *height)
 {
     if (!ctx || !rgba || !rgba_len || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
@@ -738,27 +885,20 @@ extern "C" int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const
     if (fused && c.n_comp == 3)
         fused = jpeg_rgba_supported(kind == JpegOut::RGB ? ZPX_JPEG_COLOR_RGB : ZPX_JPEG_COLOR_YCBCR, c.comp[0].h,
                                     c.comp[0].v, c.comp[1].h, c.comp[1].v);
-    if (!fused) { // planes + rgbaPixels
-        zpx_image img;
-        if (int e = zpx_jpeg_decode(ctx, nullptr, buf, len, &img)) return e;
-        uint8_t *p = nullptr;
-        size_t pl = 0;
-        int e = zpx_image_rgba_pixels(ctx, al, &img, &p, &pl);
-        zpx_image_free(nullptr, &img);
-        if (e) return e;
-        *rgba = p;
-        *rgba_len = pl;
-        if (width) *width = c.width;
-        if (height) *height = c.height;
-        return ZPX_OK;
-    }
     JpegDeviceFrame d;
     if (int e = upload_jpeg(ctx, c, d)) return e;
     DevBuf dout;
     HIPCHK(ctx, dout.alloc(n));
-    d.f.rgba = dout.as<uint8_t>();
-    d.f.rgba_stride = size_t(c.width) * 4;
-    if (int e = run_plan_once(ctx, d.f, ZPX_JPEG_RGBA)) return e;
+    if (!fused) { // planes + the colour pass of rgbaPixels, one entropy decode
+        DevBuf planes, desc;
+        HostBuf hdesc;
+        if (int e = jpeg_planes_to_rgba(ctx, c, d.f, planes, desc, hdesc, dout.as<uint8_t>(), ctx->stream)) return e;
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    } else {
+        d.f.rgba = dout.as<uint8_t>();
+        d.f.rgba_stride = size_t(c.width) * 4;
+        if (int e = run_plan_once(ctx, d.f, ZPX_JPEG_RGBA)) return e;
+    }
     uint8_t *host = static_cast<uint8_t *>(al_alloc(al, n));
     if (!host) return ZPX_E_OUT_OF_MEMORY;
     hipError_t e = hipMemcpy(host, dout.ptr, n, hipMemcpyDeviceToHost);
@@ -773,8 +913,14 @@ extern "C" int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const
     return ZPX_OK;
 }
 
+extern "C" int zpx_jpeg_decode_rgba(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                                    uint8_t **rgba, size_t *rgba_len, uint32_t *width, uint32_t *height)
+{
+    return guarded([&] { return zpx_jpeg_decode_rgba_impl(ctx, al, buf, len, rgba, rgba_len, width, height); });
+}
+
 // ------------------------------------------------------------------ png.decode
-extern "C" int zpx_png_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
 {
     if (!ctx || !out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     memset(out, 0, sizeof(*out));
@@ -807,7 +953,7 @@ extern "C" int zpx_png_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8
         hipError_t he = hipStreamSynchronize(ctx->stream);
         if (he != hipSuccess) e = hip_fail(ctx, he, "png kernel");
     }
-    if (!e) e = png_plan_status(plan);
+    if (!e) e = zpx_plan_status(plan, ctx->stream);
     zpx_plan_destroy(plan);
     if (e) return e;
     zpx_image img{};
@@ -843,6 +989,11 @@ extern "C" int zpx_png_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8
     return ZPX_OK;
 }
 
+extern "C" int zpx_png_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
+{
+    return guarded([&] { return zpx_png_decode_impl(ctx, al, buf, len, out); });
+}
+
 // ------------------------------------------------------------------ probes / facade
 extern "C" int zpx_jpeg_probe_buffer(const uint8_t *buf, size_t len)
 {
@@ -854,7 +1005,7 @@ extern "C" int zpx_png_probe_buffer(const uint8_t *buf, size_t len)
     return buf && len >= 8 && memcmp(buf, sig, 8) == 0;
 }
 
-extern "C" int zpx_jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height,
+static int zpx_jpeg_decode_config_impl(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height,
                                       int32_t *color_model)
 {
     if (!width || !height || !color_model || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
@@ -867,7 +1018,13 @@ extern "C" int zpx_jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t *
     return ZPX_OK;
 }
 
-extern "C" int zpx_png_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height)
+extern "C" int zpx_jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height,
+                                      int32_t *color_model)
+{
+    return guarded([&] { return zpx_jpeg_decode_config_impl(buf, len, width, height, color_model); });
+}
+
+static int zpx_png_decode_config_impl(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height)
 {
     if (!width || !height || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     uint32_t w = 0, h = 0;
@@ -877,7 +1034,12 @@ extern "C" int zpx_png_decode_config(const uint8_t *buf, size_t len, uint32_t *w
     return ZPX_OK;
 }
 
-extern "C" int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+extern "C" int zpx_png_decode_config(const uint8_t *buf, size_t len, uint32_t *width, uint32_t *height)
+{
+    return guarded([&] { return zpx_png_decode_config_impl(buf, len, width, height); });
+}
+
+static int zpx_jpeg_load_impl(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
 {
     std::vector<uint8_t> data;
     if (!path) return ZPX_E_INVALID_ARGUMENT;
@@ -885,12 +1047,22 @@ extern "C" int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *
     return zpx_jpeg_decode(ctx, al, data.data(), data.size(), out);
 }
 
-extern "C" int zpx_png_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+extern "C" int zpx_jpeg_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+{
+    return guarded([&] { return zpx_jpeg_load_impl(ctx, al, path, out); });
+}
+
+static int zpx_png_load_impl(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
 {
     std::vector<uint8_t> data;
     if (!path) return ZPX_E_INVALID_ARGUMENT;
     if (int e = read_file(path, data)) return e;
     return zpx_png_decode(ctx, al, data.data(), data.size(), out);
+}
+
+extern "C" int zpx_png_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+{
+    return guarded([&] { return zpx_png_load_impl(ctx, al, path, out); });
 }
 
 extern "C" int zpx_from_buffer(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len, zpx_image *out)
@@ -902,10 +1074,74 @@ extern "C" int zpx_from_buffer(zpx_ctx *ctx, const zpx_allocator *al, const uint
     return ZPX_E_UNKNOWN_IMAGE_FORMAT;
 }
 
-extern "C" int zpx_from_file_path(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+static int zpx_from_file_path_impl(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
 {
     std::vector<uint8_t> data;
     if (!path) return ZPX_E_INVALID_ARGUMENT;
     if (int e = read_file(path, data)) return e;
     return zpx_from_buffer(ctx, al, data.data(), data.size(), out);
+}
+
+extern "C" int zpx_from_file_path(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out)
+{
+    return guarded([&] { return zpx_from_file_path_impl(ctx, al, path, out); });
+}
+
+// ------------------------------------------------------------------ fault injection
+static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *seconds)
+{
+    if (!ctx || spin_limit == 0) return ZPX_E_INVALID_ARGUMENT;
+    CtxScope s(ctx);
+    // a 64 x 128 RGB8 image, every row Up-filtered: band 1's first row reads
+    // band 0's last row through the boundary granules
+    const uint32_t W = 64, H = 128, rb = W * 3;
+    std::vector<uint8_t> filt(size_t(H) * (rb + 1) + ZPX_PNG_INPUT_PAD, 0);
+    for (uint32_t y = 0; y < H; y++) filt[size_t(y) * (rb + 1)] = 2;
+    DevBuf din, dout, ctl, bound, dpass, dsched;
+    HIPCHK(ctx, din.alloc(filt.size()));
+    HIPCHK(ctx, hipMemcpy(din.ptr, filt.data(), filt.size(), hipMemcpyHostToDevice));
+    HIPCHK(ctx, dout.alloc(size_t(W) * H * 4));
+    zpx_png_frame f;
+    memset(&f, 0, sizeof(f));
+    f.width = W;
+    f.height = H;
+    f.depth = ZPX_PNG_TC8;
+    f.filtered = din.as<uint8_t>();
+    f.out = dout.as<uint8_t>();
+    f.out_stride = size_t(W) * 4;
+    std::vector<DevPngPass> passes;
+    std::vector<uint32_t> rbs;
+    uint64_t bytes = 0;
+    png_frame_passes(f, passes, rbs, bytes);
+    passes[0].nbands = 2;
+    passes[0].band_base = 0;
+    const DevPngBand only{0, 1}; // band 1 alone: band 0 never runs, so never publishes
+    const uint32_t granules = static_cast<uint32_t>(png_band_granules(ZPX_PNG_TC8, rb));
+    HIPCHK(ctx, ctl.alloc(16));
+    HIPCHK(ctx, hipMemset(ctl.ptr, 0, 16));
+    HIPCHK(ctx, bound.alloc(size_t(2) * granules * sizeof(uint64_t)));
+    HIPCHK(ctx, hipMemset(bound.ptr, 0, size_t(2) * granules * sizeof(uint64_t)));
+    HIPCHK(ctx, dpass.alloc(sizeof(DevPngPass)));
+    HIPCHK(ctx, hipMemcpy(dpass.ptr, passes.data(), sizeof(DevPngPass), hipMemcpyHostToDevice));
+    HIPCHK(ctx, dsched.alloc(sizeof(DevPngBand)));
+    HIPCHK(ctx, hipMemcpy(dsched.ptr, &only, sizeof(DevPngBand), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipDeviceSynchronize());
+    const auto t0 = std::chrono::steady_clock::now();
+    if (launch_png_unfilter(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1, ctl.as<uint32_t>(),
+                            bound.as<uint64_t>(), granules, ctx->stream, spin_limit))
+        return hip_fail(ctx, hipGetLastError(), "png stall kernel launch");
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    uint32_t st[2] = {0, 0};
+    HIPCHK(ctx, hipMemcpy(st, ctl.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost));
+    if (st[0] | st[1]) {
+        ctx->last_error = "png wavefront hand-off timed out";
+        return ZPX_E_HIP;
+    }
+    return ZPX_OK;
+}
+
+extern "C" int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds)
+{
+    return guarded([&] { return zpx_debug_png_stall_impl(ctx, spin_limit, seconds); });
 }

@@ -72,6 +72,11 @@ class _Plan:
     def launch(self, stream: int | None = None) -> None:
         _lib.check(_lib.lib().zpx_plan_launch(self.handle, stream or None), self.ctx.handle)
 
+    def status(self, stream: int | None = None) -> None:
+        """zpx_plan_status: waits for `stream` and raises ZpixError('Hip') if
+        any launch since the last call timed out in a PNG wavefront hand-off."""
+        _lib.check(_lib.lib().zpx_plan_status(self.handle, stream or None), self.ctx.handle)
+
     def close(self):
         if self.handle:
             _lib.lib().zpx_plan_destroy(self.handle)
@@ -209,6 +214,9 @@ class PngBatch:
 
     def launch(self, stream: int | None = None) -> None:
         self.plan.launch(stream)
+
+    def status(self, stream: int | None = None) -> None:
+        self.plan.status(stream)
 
     def output_tensor(self, slot: int):
         f = self.frames[slot]
