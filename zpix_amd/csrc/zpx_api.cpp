@@ -252,7 +252,9 @@ int zpx::jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f
     JpegLayout L;
     if (int e = jpeg_layout(c, L)) return e;
     const size_t kofs = (L.total + 255) & ~size_t(255);
-    HIPCHK(ctx, planes.reserve(kofs + L.k_total));
+    const size_t cmyk_ofs = (kofs + L.k_total + 255) & ~size_t(255); // CMYK image (kind CMYK, 4 B/px)
+    const size_t cmyk_bytes = kind == JpegOut::CMYK ? size_t(c.width) * c.height * 4 : 0;
+    HIPCHK(ctx, planes.reserve(cmyk_ofs + cmyk_bytes));
     HIPCHK(ctx, hipMemsetAsync(planes.ptr, 0, kofs + L.k_total, st)); // makeImg zeroes (image.zig:505-507)
     uint8_t *pb = planes.as<uint8_t>();
     f.planes[0] = pb;
@@ -296,7 +298,16 @@ int zpx::jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f
         uint32_t sub = 0;
         for (int t = 0; t < 4; t++)
             if (c.comp[t].h != c.comp[0].h || c.comp[t].v != c.comp[0].v) sub |= 1u << t;
-        rc = launch_jpeg_cmyk(m, pb + kofs, L.k_stride, sub, out, st);
+        // applyBlack builds the CMYK image; rgbaPixels converts it (color.zig:115-121)
+        rc = launch_jpeg_cmyk(m, pb + kofs, L.k_stride, sub, pb + cmyk_ofs, st);
+        if (!rc) {
+            zpx_image cm{};
+            cm.kind = ZPX_CMYK;
+            cm.max_x = static_cast<int32_t>(c.width);
+            cm.max_y = static_cast<int32_t>(c.height);
+            cm.stride = size_t(c.width) * 4;
+            rc = launch_rgba_pixels(dev_image_of(&cm, pb + cmyk_ofs, nullptr), out, st);
+        }
     } else {
         rc = launch_rgba_pixels(m, out, st); // Gray / YCbCr: Color.toRGBA (color.zig:90-126)
     }
