@@ -104,9 +104,9 @@ int jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, Dev
 // through a buffer descriptor with a 31-bit byte range, and row offsets in
 // 32-bit registers: a pass whose band would exceed it is rejected
 // (ZPX_E_UNSUPPORTED) instead of silently reading zeros past 2 GiB.
-inline bool png_band_fits(uint32_t max_row_bytes)
+inline bool png_band_fits(uint32_t max_row_bytes, uint32_t band_rows = 128)
 {
-    return 64ull * (uint64_t(max_row_bytes) + 1) + ZPX_PNG_INPUT_PAD + 4 < 0x7ffffff0ull;
+    return uint64_t(band_rows) * (uint64_t(max_row_bytes) + 1) + ZPX_PNG_INPUT_PAD + 4 < 0x7ffffff0ull;
 }
 
 // PNG band schedule (the ticket order of png_unfilter_kernel). Bands are
@@ -115,14 +115,14 @@ inline bool png_band_fits(uint32_t max_row_bytes)
 // Adam7 the passes that fill the same output lines run close together, so a
 // line's partial writes from passes 1/2/4/6 meet in L2 instead of reaching
 // HBM one pass at a time. Without interlacing this is band-major order.
-inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passes)
+inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passes, uint32_t band_rows)
 {
     std::vector<DevPngBand> sched;
     std::vector<uint64_t> key;
     for (size_t i = 0; i < passes.size(); i++)
         for (uint32_t b = 0; b < passes[i].nbands; b++) {
             sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
-            key.push_back(static_cast<uint64_t>(b) * 64 * passes[i].yf + passes[i].yo);
+            key.push_back(static_cast<uint64_t>(b) * band_rows * passes[i].yf + passes[i].yo);
         }
     std::vector<size_t> idx(sched.size());
     for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
@@ -131,5 +131,46 @@ inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passe
     for (size_t i = 0; i < idx.size(); i++) out[i] = sched[idx[i]];
     return out;
 }
+
+// The device-side band layout of a group of PNG passes of one depth: the
+// kernel that takes them (the paired-row kernel with 128-row bands, or the
+// one-row-per-lane kernel with 64-row bands), each pass's band count and
+// first band, the ticket schedule, and the boundary granules per band.
+struct PngBandPlan {
+    bool pair = false;
+    uint32_t band_rows = 64, nbands = 0, granules = 0, max_rb = 0;
+    std::vector<DevPngBand> sched;
+};
+int png_band_granules(int depth, uint32_t max_row_bytes);      // kernels.h
+bool png_pair_supported(int depth, int interlace, bool use_trns); // kernels.h
+// Which kernel takes a PNG image: the paired-row kernel wherever it
+// supports the depth (ZPX_PNG_PAIR=0 forces the one-row-per-lane kernel, for
+// A/B runs).
+inline bool png_use_pair(int depth, int interlace, bool use_trns)
+{
+    static const bool off = [] {
+        const char *e = getenv("ZPX_PNG_PAIR");
+        return e && e[0] == '0';
+    }();
+    return !off && png_pair_supported(depth, interlace, use_trns);
+}
+inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> &passes,
+                                  const std::vector<uint32_t> &rowbytes)
+{
+    PngBandPlan b;
+    b.pair = pair;
+    b.band_rows = pair ? 128 : 64;
+    for (size_t i = 0; i < passes.size(); i++) {
+        DevPngPass &p = passes[i];
+        p.nbands = (p.rows + b.band_rows - 1) / b.band_rows;
+        p.band_base = b.nbands;
+        b.nbands += p.nbands;
+        b.max_rb = std::max(b.max_rb, rowbytes[i]);
+    }
+    b.sched = png_schedule(passes, b.band_rows);
+    b.granules = static_cast<uint32_t>(png_band_granules(depth, b.max_rb));
+    return b;
+}
+
 
 } // namespace zpx

@@ -371,17 +371,11 @@ int Pipeline::issue_png(Slot &s)
     std::vector<uint32_t> rowbytes;
     uint64_t bytes = 0;
     png_frame_passes(f, passes, rowbytes, bytes);
-    uint32_t base = 0, max_bands = 0, max_rb = 0;
-    for (size_t i = 0; i < passes.size(); i++) {
-        DevPngPass &p = passes[i];
-        p.nbands = (p.rows + 63) / 64;
-        p.band_base = base;
-        base += p.nbands;
-        max_bands = std::max(max_bands, p.nbands);
-        max_rb = std::max(max_rb, rowbytes[i]);
-    }
-    const std::vector<DevPngBand> sched = png_schedule(passes); // output-row order (api_internal.h)
-    const uint32_t granules = static_cast<uint32_t>(png_band_granules(ps.depth, max_rb));
+    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent);
+    const PngBandPlan bp = png_plan_bands(ps.depth, pair, passes, rowbytes);
+    const std::vector<DevPngBand> &sched = bp.sched; // output-row order (api_internal.h)
+    const uint32_t granules = bp.granules;
+    const uint32_t base = bp.nbands;
     // descriptor staging: passes | sched | palette (256 zpx_color)
     const size_t pass_b = align_up(passes.size() * sizeof(DevPngPass));
     const size_t sched_b = align_up(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand));
@@ -402,9 +396,10 @@ int Pipeline::issue_png(Slot &s)
     uint8_t *dd = s.ddesc.as<uint8_t>();
     ZPX_TRACE("png: item %d %ux%u depth %d interlace %d passes %zu bands %zu granules %u", d.item, W, H, ps.depth,
               ps.interlace, passes.size(), sched.size(), granules);
-    if (launch_png_unfilter(ps.depth, reinterpret_cast<const DevPngPass *>(dd),
-                            reinterpret_cast<const DevPngBand *>(dd + pass_b), static_cast<uint32_t>(sched.size()),
-                            s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(), granules, ctx_->stream))
+    if ((pair ? launch_png_pair : launch_png_unfilter)(ps.depth, reinterpret_cast<const DevPngPass *>(dd),
+                                                       reinterpret_cast<const DevPngBand *>(dd + pass_b),
+                                                       static_cast<uint32_t>(sched.size()), s.dctl.as<uint32_t>(),
+                                                       s.dbound.as<uint64_t>(), granules, ctx_->stream, 0))
         return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
     HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, ctx_->stream));
     s.check_png = true;
@@ -458,7 +453,8 @@ int Pipeline::issue(Slot &s, bool &sync_done)
     }
     if (d.fmt == 2)
         for (int p = 0; p < d.ps.npasses; p++)
-            if (!png_band_fits(d.ps.pass[p].row_bytes)) { // beyond the kernel's band range
+            if (!png_band_fits(d.ps.pass[p].row_bytes,
+                               png_use_pair(d.ps.depth, d.ps.interlace, d.ps.use_transparent) ? 128 : 64)) {
                 it.status = ZPX_E_UNSUPPORTED;
                 sync_done = true;
                 return ZPX_OK;

@@ -940,7 +940,9 @@ int cus()
     return n;
 }
 
-uint32_t default_spin_limit()
+} // namespace
+
+uint32_t png_default_spin_limit()
 {
     static const uint32_t n = [] {
         const char *e = getenv("ZPX_PNG_SPIN_LIMIT");
@@ -949,6 +951,8 @@ uint32_t default_spin_limit()
     }();
     return n;
 }
+
+namespace {
 
 template <int DEPTH>
 void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl, uint64_t *boundary,
@@ -962,7 +966,7 @@ void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched
     hipLaunchKernelGGL(png_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
     if (trace) fprintf(stderr, "[zpx png] unfilter kernel\n");
     hipLaunchKernelGGL((png_unfilter_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
-                       band_granules, spin_limit ? spin_limit : default_spin_limit());
+                       band_granules, spin_limit ? spin_limit : png_default_spin_limit());
     if (trace) fprintf(stderr, "[zpx png] launched\n");
 }
 

@@ -1,0 +1,628 @@
+// gfx950 PNG filter reconstruction, two rows per lane in packed 16-bit halves
+// (the unfilter loop of readImagePass, src/png/decoder.zig:806-842, filterPaeth
+// :1152-1182, fused with the pixel store :845-1140 and the Adam7 scatter of
+// mergePassInto :1289-1373) for the byte-aligned depths whose chunk is 16
+// output bytes: RGB8 (RGBA / NRGBA with a colour key), RGBA8, Gray8, Gray16,
+// RGB16 (RGBA64 / NRGBA64 with a colour key), RGBA16.
+//
+// Work layout.  A wave owns a band of 128 rows of one pass: lane j holds rows
+// 2j (low 16-bit half of every register) and 2j+1 (high half), so one VALU
+// instruction reconstructs a byte of each.  Rows are cut into chunks of CB
+// bytes (12 for 3/6-byte pixels, else 16); at step t row r reconstructs chunk
+// t - skew(r), where skew(r) = r - (last row <= r that restarts the chain:
+// None/Sub filter, or the band's first row).  The row above arrives one step
+// late from the previous step's outputs:
+//   - row 2j+1 (high half) reads row 2j = the low half of its own lane,
+//   - row 2j (low half) reads row 2j-1 = the high half of lane j-1, through a
+//     DPP wave_shr:1 of the output registers; lane 0 takes the value the DPP
+//     leaves in its `old` operand: the previous band's last row (boundary
+//     granules, see png_kernels.hip) or zero (the first row of a pass).
+// so up = alignbit(out, dpp_shr1(out), 16) = [lane j-1 hi, own lo].
+//
+// Per byte pair the whole filter set is one path: the Paeth keys
+// dist * 128 + code (code = the byte position of a / b / c in a v_perm
+// source pair; a and b tie harmlessly, c loses every tie -- the reference's
+// a < b < c rule), the smallest key's code picks the predictor byte, and a
+// per-half (KEEP, FORCE) pair overrides the code for None / Sub / Up / Avg
+// (Avg's (a + b) >> 1 is a fourth byte of the same v_perm source):
+//   pa = |b-c|, pb = |a-c|, pc = |a+b-2c|  (packed max - min)
+//   sel = (min(ka, kb, kc) & KEEP) | FORCE;  t = perm(c | avg << 8, a | b << 8, sel)
+//   out = (f + t) & 0x00ff00ff
+// about 23 instructions per byte PAIR, against ~21 per byte one row per lane.
+//
+// Memory: every lane burst-loads its two rows' next group of 4 chunks one
+// group ahead; reconstructed chunks go to a per-row LDS ring of 12 slots
+// (raw filtered-order bytes), and every 4 steps the rows that completed an
+// aligned 8-chunk block (one 128-byte line of output) are listed, and 8 lanes
+// per listed row store its block as whole lines (cooperative flush).  The
+// hot loop is one 4-step group, so the loop body stays a few KB of code (the
+// one-row-per-lane kernel's 94 KB loop missed the instruction cache).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#include "device_types.h"
+#include "kernels.h"
+
+namespace zpx {
+namespace {
+
+#define ZPX_GLOBAL __attribute__((address_space(1)))
+typedef ZPX_GLOBAL uint8_t gu8;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gptr(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
+
+constexpr int kG = 4;       // steps per group (input burst, flush period)
+constexpr int kSlots = 12;  // ring slots per row: an 8-chunk block + one group's chunks fit
+#ifndef ZPX_PNG_SLEEP
+#define ZPX_PNG_SLEEP 2
+#endif
+
+template <int DEPTH> struct PairTraits;
+#define ZPX_PAIR_TRAITS(D, BPP_, OBPX_)                                        \
+    template <> struct PairTraits<D> {                                         \
+        static constexpr int BPP = BPP_;                 /* filter bytes/px */ \
+        static constexpr int CB = (BPP_ == 3 || BPP_ == 6) ? 12 : 16;          \
+        static constexpr int CW = CB / 4;                                      \
+        static constexpr int C = CB / BPP_;              /* pixels/chunk */    \
+        static constexpr int OBPX = OBPX_;               /* out bytes/px */    \
+    };
+ZPX_PAIR_TRAITS(ZPX_PNG_G8, 1, 1)
+ZPX_PAIR_TRAITS(ZPX_PNG_G16, 2, 2)
+ZPX_PAIR_TRAITS(ZPX_PNG_TC8, 3, 4)
+ZPX_PAIR_TRAITS(ZPX_PNG_TCA8, 4, 4)
+ZPX_PAIR_TRAITS(ZPX_PNG_TC16, 6, 8)
+ZPX_PAIR_TRAITS(ZPX_PNG_TCA16, 8, 8)
+#undef ZPX_PAIR_TRAITS
+
+// ---- packed 16-bit helpers (v_pk_*_u16)
+__device__ __forceinline__ u16x2 as16(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t pk_absdiff(uint32_t x, uint32_t y)
+{
+    const u16x2 a = as16(x), b = as16(y);
+    return as32(__builtin_elementwise_max(a, b) - __builtin_elementwise_min(a, b));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t x, uint32_t y)
+{
+    return as32(__builtin_elementwise_min(as16(x), as16(y)));
+}
+__device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) { return as32(as16(x) + as16(y)); }
+__device__ __forceinline__ uint32_t pk_shr1(uint32_t x) { return as32(as16(x) >> (unsigned short)1); }
+
+// Paeth key codes: the byte position of each candidate in perm(cav, ab):
+// ab = [a.lo, b.lo, a.hi, b.hi] (bytes 0-3), cav = [c.lo, avg.lo, c.hi, avg.hi]
+// (bytes 4-7); low half codes a 0, b 1, c 4, avg 5; high half 2, 3, 6, 7.
+constexpr uint32_t kKA = 0x00020000u, kKB = 0x00030001u, kKC = 0x00060004u;
+
+struct PairFilter {
+    uint32_t keep, force; // sel = (key & keep) | force, per 16-bit half
+};
+// filter type -> (keep, force) of one half (h = 0 low, 1 high)
+__device__ __forceinline__ PairFilter half_filter(int ft, int h)
+{
+    const uint32_t sh = h ? 16u : 0u, base = h ? 2u : 0u;
+    uint32_t keep = 0, force = 0x0c00u;
+    switch (ft) {
+    case 1: force |= base + 0; break;     // Sub: a
+    case 2: force |= base + 1; break;     // Up: b
+    case 3: force |= base + 5; break;     // Avg: (a + b) >> 1
+    case 4: keep = 0x0007u; break;        // Paeth: the smallest key's code
+    default: force = 0x0c0cu; break;      // None: zero
+    }
+    return PairFilter{keep << sh, force << sh};
+}
+
+// One byte pair: out = (f + predictor) mod 256 per half.
+__device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, uint32_t ka,
+                                               uint32_t c2, PairFilter pf)
+{
+    const uint32_t pb = pk_absdiff(a, c);
+    const uint32_t s = pk_add(a, b);
+    const uint32_t pc = pk_absdiff(s, c2);
+    const uint32_t kb = (pb << 7) | kKB;
+    const uint32_t kc = (pc << 7) | kKC;
+    const uint32_t m = pk_min(pk_min(ka, kb), kc);
+    const uint32_t sel = (m & pf.keep) | pf.force;
+    const uint32_t ab = a | (b << 8);
+    const uint32_t cav = c | (pk_shr1(s) << 8);
+    const uint32_t t = __builtin_amdgcn_perm(cav, ab, sel);
+    return (f + t) & 0x00ff00ffu;
+}
+
+// ---- output of one chunk: the 16 bytes store_chunk writes (readImagePass
+// :947-950, :963-968, :994-1015, :1033-1039, :1062-1078), from CW raw dwords
+template <int DEPTH>
+__device__ __forceinline__ v4u expand_chunk(const DevPngPass &ps, const uint32_t *ob)
+{
+    if constexpr (DEPTH == ZPX_PNG_TC8) { // RGBA, alpha 0xff (NRGBA with the colour key)
+        v4u w;
+        w[0] = __builtin_amdgcn_perm(ob[0], ob[0], 0x0c020100u) | 0xff000000u;
+        w[1] = __builtin_amdgcn_perm(ob[1], ob[0], 0x0c050403u) | 0xff000000u;
+        w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x0c040302u) | 0xff000000u;
+        w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0c030201u) | 0xff000000u;
+        if (ps.use_trns) {
+            const uint32_t key = uint32_t(ps.trns[1]) | uint32_t(ps.trns[3]) << 8 | uint32_t(ps.trns[5]) << 16;
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if ((w[u] & 0xffffffu) == key) w[u] &= 0xffffffu;
+        }
+        return w;
+    } else if constexpr (DEPTH == ZPX_PNG_TC16) { // RGBA64 (NRGBA64 with the key), big-endian channels
+        // bytes r0 r1 g0 g1 b0 b1 | r0 r1 g0 g1 b0 b1 in ob[0..2]
+        v4u w;
+        w[0] = ob[0];                                             // r, g of pixel 0
+        w[1] = __builtin_amdgcn_perm(ob[1], ob[1], 0x0d0d0100u);  // b, alpha ffff
+        w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x05040302u);  // r, g of pixel 1
+        w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0d0d0302u);  // b, alpha ffff
+        if (ps.use_trns) {
+            const uint32_t k01 = uint32_t(ps.trns[0]) | uint32_t(ps.trns[1]) << 8 | uint32_t(ps.trns[2]) << 16 |
+                                 uint32_t(ps.trns[3]) << 24;
+            const uint32_t k2 = uint32_t(ps.trns[4]) | uint32_t(ps.trns[5]) << 8;
+            if (w[0] == k01 && (w[1] & 0xffffu) == k2) w[1] &= 0xffffu;
+            if (w[2] == k01 && (w[3] & 0xffffu) == k2) w[3] &= 0xffffu;
+        }
+        return w;
+    } else { // the chunk's bytes are the output bytes (Gray8, Gray16 BE, RGBA8, RGBA16)
+        return v4u{ob[0], ob[1], ob[2], ob[3]};
+    }
+}
+
+// chunk k's 16 output bytes into output row `orow` of the pass (pixels xf apart)
+template <int DEPTH>
+__device__ __forceinline__ void put_chunk(const DevPngPass &ps, gu8 *orow, int k, v4u v)
+{
+    using T = PairTraits<DEPTH>;
+    if (ps.xf == 1) {
+        *gptr<v4u>(orow + static_cast<size_t>(k) * 16) = v;
+    } else {
+#pragma unroll
+        for (int u = 0; u < T::C; u++) {
+            gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u) * ps.xf + ps.xo) * T::OBPX;
+            if constexpr (T::OBPX == 8) *gptr<v2u>(d) = v2u{v[2 * u], v[2 * u + 1]};
+            else *gptr<uint32_t>(d) = v[u];
+        }
+    }
+}
+
+// the pixels [x0, x0 + n) of a partial last chunk (n < C), byte stores
+template <int DEPTH>
+__device__ __forceinline__ void put_partial(const DevPngPass &ps, gu8 *orow, int k, v4u v, int n)
+{
+    using T = PairTraits<DEPTH>;
+    for (int u = 0; u < n; u++) {
+        gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u) * ps.xf + ps.xo) * T::OBPX;
+        for (int i = 0; i < T::OBPX; i++) {
+            const int byte = u * T::OBPX + i;
+            d[i] = static_cast<uint8_t>(v[byte >> 2] >> ((byte & 3) * 8));
+        }
+    }
+}
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void *base, uint32_t bytes)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base);
+    const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a)));
+    const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32)));
+    void *ua = reinterpret_cast<void *>(static_cast<uintptr_t>(hi << 32 | lo));
+    return __builtin_amdgcn_make_buffer_rsrc(ua, 0, static_cast<int>(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
+}
+
+// N dwords from byte offset `off` (dword aligned, >= 0) into d[]
+template <int N>
+__device__ __forceinline__ void load_dwords(uint32_t (&d)[N], Rsrc rsrc, int off)
+{
+#pragma unroll
+    for (int i = 0; i + 4 <= N; i += 4) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 4 * i, 0, 0);
+        d[i] = v[0];
+        d[i + 1] = v[1];
+        d[i + 2] = v[2];
+        d[i + 3] = v[3];
+    }
+    constexpr int T = N & ~3;
+    if constexpr (N - T == 1) {
+        d[T] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4 * T, 0, 0);
+    } else if constexpr (N - T == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off + 4 * T, 0, 0);
+        d[T] = v[0];
+        d[T + 1] = v[1];
+    } else if constexpr (N - T == 3) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, off + 4 * T, 0, 0);
+        d[T] = v[0];
+        d[T + 1] = v[1];
+        d[T + 2] = v[2];
+    }
+}
+// the same, dword by dword, for a lane whose group may start before its row
+// (any offset < 0 is selected out of range: the range check does not wrap
+// voffset + the instruction's immediate)
+template <int N>
+__device__ __forceinline__ void load_dwords_neg(uint32_t (&d)[N], Rsrc rsrc, int off)
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const int o = off + 4 * i;
+        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
+    }
+}
+
+__device__ __forceinline__ uint64_t ld_sc1_64(const uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_64(uint64_t *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int DEPTH>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__restrict__ sched, uint32_t nsched,
+                     uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit)
+{
+    using T = PairTraits<DEPTH>;
+    constexpr int BPP = T::BPP, CB = T::CB, CW = T::CW, C = T::C;
+    constexpr int GD = kG * CW + 1;         // input dwords per row per group (+1: alignbyte carry)
+    constexpr int RS = kSlots * CW + 1;     // ring dwords per row (odd: spreads the banks)
+    constexpr int WINP = kG * CB;           // boundary window: packed pairs of kG chunks
+    __shared__ __attribute__((aligned(16))) uint32_t ring[128 * RS + 4]; // + a trash slot
+    __shared__ __attribute__((aligned(16))) uint32_t win[WINP];
+    __shared__ uint32_t list[128];
+    constexpr int kTrash = 128 * RS;
+
+    const int lane = threadIdx.x;
+    const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
+    uint32_t *ticket = ctl + 1, *status = ctl + 2;
+    bool timed_out = false;
+
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(ticket, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+        if (t >= nsched) break;
+        const DevPngBand bd = sched[t];
+        const DevPngPass ps = passes[bd.pass];
+        const uint32_t rb = ps.row_bytes;
+        const int nchunks = static_cast<int>(((rb + BPP - 1) / BPP + C - 1) / C);
+        const int nfull = static_cast<int>(ps.width / C); // chunks whose pixels are all inside the row
+        const uint32_t base = bd.band * 128;
+        const uint32_t band_rows = min(128u, ps.rows - base);
+        const uint32_t y0 = base + 2 * lane, y1 = y0 + 1;
+        const bool ok0 = 2u * lane < band_rows, ok1 = 2u * lane + 1 < band_rows;
+        const int ft0 = ok0 ? ps.filtered[static_cast<size_t>(y0) * (rb + 1)] : 0;
+        const int ft1 = ok1 ? ps.filtered[static_cast<size_t>(y1) * (rb + 1)] : 0;
+
+        // skew over the band's 128 rows (row 2j = low half of lane j, 2j+1 high)
+        const uint64_t R0 = __ballot(!(ft0 >= 2) || lane == 0 || !ok0);
+        const uint64_t R1 = __ballot(!(ft1 >= 2) || !ok1);
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1), below = (1ull << lane) - 1;
+        const int i0 = 63 - __builtin_clzll(R0 & upto); // R0 bit 0 is always set
+        const int last0 = max(2 * i0, (R1 & below) ? 2 * (63 - __builtin_clzll(R1 & below)) + 1 : -1);
+        const int last1 = max(2 * i0, (R1 & upto) ? 2 * (63 - __builtin_clzll(R1 & upto)) + 1 : -1);
+        const int skew0 = 2 * lane - last0, skew1 = 2 * lane + 1 - last1;
+        int max_skew = max(ok0 ? skew0 : 0, ok1 ? skew1 : 0);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) max_skew = max(max_skew, __shfl_xor(max_skew, off));
+        max_skew = __builtin_amdgcn_readfirstlane(max_skew);
+        const int nsteps = nchunks + max_skew;
+
+        PairFilter pf;
+        {
+            const PairFilter a = half_filter(ft0, 0), b = half_filter(ft1, 1);
+            pf = PairFilter{a.keep | b.keep, a.force | b.force};
+        }
+
+        // band input: one descriptor from the dword below the band's first
+        // byte over its rows + ZPX_PNG_INPUT_PAD
+        const uint8_t *band0 = ps.filtered + static_cast<size_t>(base) * (rb + 1);
+        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
+        const uint32_t delta = static_cast<uint32_t>(band0 - base4);
+        const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
+        const Rsrc rsrc = make_rsrc(base4, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
+        const uint32_t roff0 = delta + static_cast<uint32_t>(2 * lane) * (rb + 1); // filter byte of row 2j
+        const uint32_t roff1 = roff0 + rb + 1;
+        const uint32_t mis0 = (roff0 + 1) & 3, mis1 = (roff1 + 1) & 3;
+        const int doff0 = static_cast<int>(roff0 + 1 - mis0) - skew0 * CB; // group 0's first dword, row 2j
+        const int doff1 = static_cast<int>(roff1 + 1 - mis1) - skew1 * CB;
+
+        const bool has_prev = bd.band > 0, has_next = bd.band + 1 < ps.nbands;
+        const bool dep_first = (__ballot(ft0 >= 2) & 1ull) != 0; // row 0 of the band reads the row above
+        const bool wait_prev = has_prev && dep_first;
+        const uint64_t *prev_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) * band_granules;
+        uint64_t *my_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band) * band_granules;
+        const uint64_t ep64 = static_cast<uint64_t>(epoch) << 32;
+
+        gu8 *out0 = (gu8 *)(ps.out + static_cast<size_t>(y0 * ps.yf + ps.yo) * ps.out_stride);
+        gu8 *out1 = (gu8 *)(ps.out + static_cast<size_t>(y1 * ps.yf + ps.yo) * ps.out_stride);
+
+        // per-row state
+        uint32_t outp[CB], left[BPP], ul[BPP];
+#pragma unroll
+        for (int i = 0; i < CB; i++) outp[i] = 0;
+#pragma unroll
+        for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
+        int k0 = -skew0, k1 = -skew1;                                   // chunk of the current step
+        int s0 = ((k0 % kSlots) + kSlots) % kSlots, s1 = ((k1 % kSlots) + kSlots) % kSlots; // k mod 12
+        int fl0 = 0, fl1 = 0;                                           // blocks of 8 chunks flushed
+        const int ring0 = (2 * lane) * RS, ring1 = ring0 + RS;
+
+        // input double buffer: A = the group being reconstructed, B = the next
+        uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
+        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
+            const int o0 = doff0 + g0 * CB, o1 = doff1 + g0 * CB;
+            if (__ballot(o0 < 0 || o1 < 0) != 0) {
+                load_dwords_neg<GD>(d0, rsrc, o0);
+                load_dwords_neg<GD>(d1, rsrc, o1);
+            } else {
+                load_dwords<GD>(d0, rsrc, o0);
+                load_dwords<GD>(d1, rsrc, o1);
+            }
+        };
+
+        // the previous band's last row, chunks [g0, g0 + kG): wait until
+        // every granule of the window carries this launch's epoch, then stage
+        // it in LDS as packed "old" operands (byte << 16) for lane 0's DPP
+        auto wait_window = [&](int g0) {
+            const int nwc = min(kG, nchunks - g0);
+            if (nwc <= 0) return;
+            const int ng = nwc * CW; // granules (<= 16): lanes 0..7 take 2 each
+            const bool mine = 2 * lane < ng;
+            const uint64_t *src = prev_bnd + static_cast<size_t>(g0) * CW + (mine ? 2 * lane : 0);
+            uint64_t ga = 0, gb = 0;
+            uint32_t spins = 0;
+            for (;;) {
+                ga = ld_sc1_64(src);
+                gb = ld_sc1_64(src + 1);
+                const bool ready = !mine || ((ga >> 32) == epoch && (2 * lane + 1 >= ng || (gb >> 32) == epoch));
+                if (__ballot(!ready) == 0) break;
+                if (timed_out) break;
+                ++spins;
+                if (spins > spin_limit ||
+                    ((spins & 255) == 0 && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+                    timed_out = true;
+                    if (lane == 0) atomicOr(status, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
+            }
+            if (mine) {
+                const uint32_t da = static_cast<uint32_t>(ga), db = static_cast<uint32_t>(gb);
+                v4u p, q;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    p[b] = ((da >> (8 * b)) & 0xffu) << 16;
+                    q[b] = ((db >> (8 * b)) & 0xffu) << 16;
+                }
+                *reinterpret_cast<v4u *>(&win[8 * lane]) = p;
+                *reinterpret_cast<v4u *>(&win[8 * lane + 4]) = q;
+            }
+            wave_lds_sync();
+        };
+
+        // every kG steps: rows that completed an aligned block of 8 full
+        // chunks are listed, 8 lanes per listed row store it from the ring
+        auto flush = [&](int t_end) {
+            const int d0 = ok0 ? min(max(t_end - skew0, 0), nchunks) : 0;
+            const int d1 = ok1 ? min(max(t_end - skew1, 0), nchunks) : 0;
+            const bool p0 = (min(d0, nfull) >> 3) > fl0, p1 = (min(d1, nfull) >> 3) > fl1;
+            const uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
+            const int n = __builtin_popcountll(b0) + __builtin_popcountll(b1);
+            if (n == 0) return;
+            const int r0 = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b0 >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b0), 0));
+            const int r1 = __builtin_popcountll(b0) +
+                           __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b1 >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b1), 0));
+            if (p0) list[r0] = static_cast<uint32_t>(2 * lane) << 16 | static_cast<uint32_t>(fl0);
+            if (p1) list[r1] = static_cast<uint32_t>(2 * lane + 1) << 16 | static_cast<uint32_t>(fl1);
+            wave_lds_sync();
+            for (int e0 = 0; e0 < n; e0 += 8) {
+                const int e = e0 + (lane >> 3);
+                if (e < n) {
+                    const uint32_t ent = list[e];
+                    const int r = static_cast<int>(ent >> 16);
+                    const int k = static_cast<int>(ent & 0xffffu) * 8 + (lane & 7);
+                    const uint32_t *src = &ring[r * RS + (k % kSlots) * CW];
+                    uint32_t ob[4];
+#pragma unroll
+                    for (int i = 0; i < CW; i++) ob[i] = src[i];
+                    if constexpr (CW == 3) ob[3] = 0;
+                    const uint32_t y = base + static_cast<uint32_t>(r);
+                    gu8 *orow = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
+                    put_chunk<DEPTH>(ps, orow, k, expand_chunk<DEPTH>(ps, ob));
+                }
+            }
+            fl0 += p0 ? 1 : 0;
+            fl1 += p1 ? 1 : 0;
+            wave_lds_sync(); // the list is rewritten at the next flush
+        };
+
+        load_group(B0, B1, 0);
+        for (int g0 = 0; g0 < nsteps; g0 += kG) {
+#pragma unroll
+            for (int i = 0; i < GD; i++) {
+                A0[i] = B0[i];
+                A1[i] = B1[i];
+            }
+            if (g0 + kG < nsteps) load_group(B0, B1, g0 + kG);
+            if (wait_prev) wait_window(g0);
+#pragma unroll
+            for (int st = 0; st < kG; st++) {
+                const int step = g0 + st;
+                // ---- the row above, one step late
+                uint32_t up[CB];
+                if (wait_prev && step < nchunks) { // lane 0's old operand: the previous band's last row
+#pragma unroll
+                    for (int i = 0; i < CB; i++) {
+                        const uint32_t old = win[st * CB + i];
+                        up[i] = __builtin_amdgcn_alignbit(
+                            outp[i], static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(old),
+                                                                                      static_cast<int>(outp[i]),
+                                                                                      0x138, 0xf, 0xf, false)),
+                            16);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < CB; i++)
+                        up[i] = __builtin_amdgcn_alignbit(
+                            outp[i], static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                                         0, static_cast<int>(outp[i]), 0x138, 0xf, 0xf, false)),
+                            16);
+                }
+                // ---- filtered bytes of both rows' chunks, packed
+                uint32_t f[CB];
+#pragma unroll
+                for (int w = 0; w < CW; w++) {
+                    const uint32_t lo = __builtin_amdgcn_alignbyte(A0[st * CW + w + 1], A0[st * CW + w], mis0);
+                    const uint32_t hi = __builtin_amdgcn_alignbyte(A1[st * CW + w + 1], A1[st * CW + w], mis1);
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        f[4 * w + b] = __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (4u + b) << 16 | static_cast<uint32_t>(b));
+                }
+                // ---- a row's first chunk starts from zero left / up-left (x < bpp)
+                const uint32_t keep = (k0 != 0 ? 0x0000ffffu : 0u) | (k1 != 0 ? 0xffff0000u : 0u);
+#pragma unroll
+                for (int i = 0; i < BPP; i++) {
+                    left[i] &= keep;
+                    ul[i] &= keep;
+                }
+                // ---- reconstruct CB byte pairs, left to right
+                uint32_t o[CB];
+#pragma unroll
+                for (int i = 0; i < CB; i++) {
+                    const uint32_t a = i < BPP ? left[i] : o[i < BPP ? 0 : i - BPP];
+                    const uint32_t c = i < BPP ? ul[i] : up[i < BPP ? 0 : i - BPP];
+                    const uint32_t b = up[i];
+                    const uint32_t ka = (pk_absdiff(b, c) << 7) | kKA;
+                    o[i] = recon_pair(f[i], a, b, c, ka, pk_add(c, c), pf);
+                }
+#pragma unroll
+                for (int i = 0; i < BPP; i++) {
+                    left[i] = o[CB - BPP + i];
+                    ul[i] = up[CB - BPP + i];
+                }
+#pragma unroll
+                for (int i = 0; i < CB; i++) outp[i] = o[i];
+                // ---- bytes of each row into its ring slot (or the trash slot)
+                uint32_t lo[CW], hi[CW];
+#pragma unroll
+                for (int w = 0; w < CW; w++) {
+                    const uint32_t x01 = __builtin_amdgcn_perm(o[4 * w + 1], o[4 * w], 0x06020400u);
+                    const uint32_t x23 = __builtin_amdgcn_perm(o[4 * w + 3], o[4 * w + 2], 0x06020400u);
+                    lo[w] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+                    hi[w] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
+                }
+                const bool act0 = ok0 && k0 >= 0 && k0 < nchunks, act1 = ok1 && k1 >= 0 && k1 < nchunks;
+                uint32_t *d0 = &ring[act0 ? ring0 + s0 * CW : kTrash];
+                uint32_t *d1 = &ring[act1 ? ring1 + s1 * CW : kTrash];
+#pragma unroll
+                for (int w = 0; w < CW; w++) {
+                    d0[w] = lo[w];
+                    d1[w] = hi[w];
+                }
+                // ---- publish the band's last row (row 127, lane 63's high half): the data is the flag
+                if (has_next && lane == 63 && act1) {
+                    uint64_t *dst = my_bnd + static_cast<size_t>(k1) * CW;
+#pragma unroll
+                    for (int w = 0; w < CW; w++) st_sc1_64(dst + w, ep64 | hi[w]);
+                }
+                k0++;
+                k1++;
+                s0 = s0 == kSlots - 1 ? 0 : s0 + 1;
+                s1 = s1 == kSlots - 1 ? 0 : s1 + 1;
+            }
+            wave_lds_sync();
+            flush(g0 + kG);
+        }
+        // ---- row tails: the last (< 8) full chunks and a partial one
+        wave_lds_sync();
+        for (int h = 0; h < 2; h++) {
+            const bool ok = h ? ok1 : ok0;
+            if (!ok) continue;
+            const int fl = h ? fl1 : fl0;
+            gu8 *orow = h ? out1 : out0;
+            const int rbase = h ? ring1 : ring0;
+            for (int k = fl * 8; k < nchunks; k++) {
+                uint32_t ob[4];
+#pragma unroll
+                for (int i = 0; i < CW; i++) ob[i] = ring[rbase + (k % kSlots) * CW + i];
+                if constexpr (CW == 3) ob[3] = 0;
+                const v4u v = expand_chunk<DEPTH>(ps, ob);
+                if (k < nfull) put_chunk<DEPTH>(ps, orow, k, v);
+                else put_partial<DEPTH>(ps, orow, k, v, static_cast<int>(ps.width) - k * C);
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// Per-launch control block (as png_kernels.hip): epoch++, ticket = 0, the
+// previous launch's status folded into the sticky word, status = 0.
+__global__ void png_pair_ctl_kernel(uint32_t *ctl)
+{
+    ctl[0] += 1;
+    ctl[1] = 0;
+    ctl[3] |= ctl[2];
+    ctl[2] = 0;
+}
+
+template <int DEPTH>
+void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
+                   uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
+{
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        const char *e = getenv("ZPX_PNG_WAVES_PER_CU");
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH>, 64, 0) != hipSuccess || occ < 1)
+            occ = 4;
+        per_cu = e ? atoi(e) : occ;
+        if (per_cu < 1) per_cu = 1;
+    }
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t want = static_cast<uint32_t>(cus * per_cu);
+    const uint32_t grid = nsched < want ? nsched : want;
+    hipLaunchKernelGGL(png_pair_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
+    hipLaunchKernelGGL((png_pair_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
+                       band_granules, spin_limit);
+}
+
+} // namespace
+
+bool png_pair_supported(int depth, int interlace, bool use_trns)
+{
+    switch (depth) {
+    case ZPX_PNG_TC8: case ZPX_PNG_TCA8: case ZPX_PNG_TC16: case ZPX_PNG_TCA16: return true;
+    case ZPX_PNG_G8: case ZPX_PNG_G16: return !interlace && !use_trns;
+    default: return false;
+    }
+}
+
+int launch_png_pair(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
+                    uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit)
+{
+    const uint32_t sl = spin_limit ? spin_limit : png_default_spin_limit();
+    switch (depth) {
+#define ZPX_CASE(D) case D: launch_pair_t<D>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
+        ZPX_CASE(ZPX_PNG_G8) ZPX_CASE(ZPX_PNG_G16) ZPX_CASE(ZPX_PNG_TC8) ZPX_CASE(ZPX_PNG_TCA8)
+        ZPX_CASE(ZPX_PNG_TC16) ZPX_CASE(ZPX_PNG_TCA16)
+#undef ZPX_CASE
+    default: return -2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace zpx

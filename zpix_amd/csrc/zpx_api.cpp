@@ -325,6 +325,7 @@ struct JpegGroup {
 };
 struct PngGroup {
     int depth = 0;
+    bool pair = false; // png_pair_kernel (128-row bands) or png_unfilter_kernel (64)
     DevBuf passes, sched, scratch, boundary;
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
     size_t scratch_zero_bytes = 0;
@@ -422,23 +423,16 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
                            const std::vector<uint32_t> &pass_rowbytes)
 {
     std::vector<DevPngPass> passes = passes_in;
-    uint32_t base = 0, max_bands = 0, max_rb = 0;
-    for (size_t i = 0; i < passes.size(); i++) {
-        DevPngPass &p = passes[i];
-        p.nbands = (p.rows + 63) / 64;
-        p.band_base = base;
-        base += p.nbands;
-        max_bands = std::max(max_bands, p.nbands);
-        max_rb = std::max(max_rb, pass_rowbytes[i]);
-    }
-    if (!png_band_fits(max_rb)) {
-        ctx->last_error = "png: a 64-row band of this image exceeds the kernel's 2 GiB band range";
+    const PngBandPlan bp = png_plan_bands(g.depth, g.pair, passes, pass_rowbytes);
+    if (!png_band_fits(bp.max_rb, bp.band_rows)) {
+        ctx->last_error = "png: a band of this image exceeds the kernel's 2 GiB band range";
         return ZPX_E_UNSUPPORTED;
     }
-    const std::vector<DevPngBand> sched = png_schedule(passes); // output-row order (api_internal.h)
+    const std::vector<DevPngBand> &sched = bp.sched; // output-row order (api_internal.h)
+    const uint32_t base = bp.nbands;
     g.nsched = static_cast<uint32_t>(sched.size());
     g.nbands = base;
-    g.band_bytes = static_cast<uint32_t>(png_band_granules(g.depth, max_rb)); // granules per band
+    g.band_bytes = bp.granules; // granules per band
     HIPCHK(ctx, g.passes.alloc(passes.size() * sizeof(DevPngPass)));
     HIPCHK(ctx, hipMemcpy(g.passes.ptr, passes.data(), passes.size() * sizeof(DevPngPass), hipMemcpyHostToDevice));
     HIPCHK(ctx, g.sched.alloc(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand)));
@@ -527,15 +521,18 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
     std::unique_ptr<zpx_plan> plan(new zpx_plan);
     plan->ctx = ctx;
     plan->kind = 2;
-    std::map<int, std::vector<int>> by_depth;
+    // one launch per (depth, kernel): the paired-row kernel takes what it supports
+    std::map<std::pair<int, bool>, std::vector<int>> by_depth;
     for (int i = 0; i < n_frames; i++) {
         if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
-        by_depth[frames[i].depth].push_back(i);
+        const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, frames[i].use_transparent != 0);
+        by_depth[{frames[i].depth, pair}].push_back(i);
     }
     uint64_t bytes = 0;
     for (auto &kv : by_depth) {
         std::unique_ptr<PngGroup> g(new PngGroup);
-        g->depth = kv.first;
+        g->depth = kv.first.first;
+        g->pair = kv.first.second;
         std::vector<DevPngPass> passes;
         std::vector<uint32_t> rowbytes;
         for (int idx : kv.second) {
@@ -573,8 +570,9 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
     for (auto &g : plan->png) {
-        const int rc = launch_png_unfilter(g->depth, g->passes.as<DevPngPass>(), g->sched.as<DevPngBand>(), g->nsched,
-                                           g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes, st);
+        const int rc = (g->pair ? launch_png_pair : launch_png_unfilter)(g->depth, g->passes.as<DevPngPass>(),
+                                                                        g->sched.as<DevPngBand>(), g->nsched,
+                                           g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes, st, 0);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
     }
     return ZPX_OK;
