@@ -458,12 +458,13 @@ int zpx_batch_decode_sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *ite
 /* ---------------------------------------------------------------------- */
 /* fault injection (tests)                                                 */
 /* ---------------------------------------------------------------------- */
-/* Launches the PNG unfilter kernel on a 2-band image whose second band waits
- * for a first band that is never scheduled (a producer that never
- * publishes), with `spin_limit` polls per wait, and returns what
- * zpx_plan_status reports for it: ZPX_E_HIP when the bounded wait gave up
- * (the expected outcome).  `seconds` (may be NULL) receives the launch's wall
- * time, which must stay about one spin limit, not one per step. */
+/* Launches each PNG unfilter kernel (one row per lane, and paired rows) on a
+ * 2-band image whose second band waits for a first band that is never
+ * scheduled (a producer that never publishes), with `spin_limit` polls per
+ * wait, and returns what zpx_plan_status reports: ZPX_E_HIP when both
+ * bounded waits gave up (the expected outcome).  `seconds` (may be NULL)
+ * receives the slower launch's wall time, which must stay about one spin
+ * limit, not one per step. */
 int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds);
 
 #ifdef __cplusplus

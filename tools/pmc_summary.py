@@ -13,7 +13,8 @@ for p in sorted(os.listdir(base)):
         continue
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = "jpeg_rgba" if "jpeg_rgba" in name else "png_unfilter" if "png_unfilter" in name else None
+        short = ("jpeg_rgba" if "jpeg_rgba" in name else "png_unfilter" if "png_unfilter" in name
+                 else "png_pair" if "png_pair_kernel" in name else None)
         if not short:
             continue
         acc[short][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))

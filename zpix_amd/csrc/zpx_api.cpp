@@ -1097,13 +1097,13 @@ extern "C" int zpx_from_file_path(zpx_ctx *ctx, const zpx_allocator *al, const c
 }
 
 // ------------------------------------------------------------------ fault injection
-static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *seconds)
+// One stalled launch of either PNG kernel: a W x 2*band_rows RGB8 image,
+// every row Up-filtered, of which only band 1 is scheduled, so its first row
+// waits for band 0's last row forever.
+static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &secs, bool &timed_out)
 {
-    if (!ctx || spin_limit == 0) return ZPX_E_INVALID_ARGUMENT;
-    CtxScope s(ctx);
-    // a 64 x 128 RGB8 image, every row Up-filtered: band 1's first row reads
-    // band 0's last row through the boundary granules
-    const uint32_t W = 64, H = 128, rb = W * 3;
+    const uint32_t band_rows = pair ? 128 : 64;
+    const uint32_t W = 64, H = 2 * band_rows, rb = W * 3;
     std::vector<uint8_t> filt(size_t(H) * (rb + 1) + ZPX_PNG_INPUT_PAD, 0);
     for (uint32_t y = 0; y < H; y++) filt[size_t(y) * (rb + 1)] = 2;
     DevBuf din, dout, ctl, bound, dpass, dsched;
@@ -1136,14 +1136,33 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
     HIPCHK(ctx, hipMemcpy(dsched.ptr, &only, sizeof(DevPngBand), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
-    if (launch_png_unfilter(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1, ctl.as<uint32_t>(),
-                            bound.as<uint64_t>(), granules, ctx->stream, spin_limit))
+    if ((pair ? launch_png_pair : launch_png_unfilter)(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
+                                                      ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream,
+                                                      spin_limit))
         return hip_fail(ctx, hipGetLastError(), "png stall kernel launch");
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     uint32_t st[2] = {0, 0};
     HIPCHK(ctx, hipMemcpy(st, ctl.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost));
-    if (st[0] | st[1]) {
+    timed_out = (st[0] | st[1]) != 0;
+    return ZPX_OK;
+}
+
+static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *seconds)
+{
+    if (!ctx || spin_limit == 0) return ZPX_E_INVALID_ARGUMENT;
+    CtxScope s(ctx);
+    double worst = 0;
+    bool all_timed_out = true;
+    for (bool pair : {false, true}) { // both kernels' bounded waits
+        double secs = 0;
+        bool to = false;
+        if (int e = png_stall_once(ctx, pair, spin_limit, secs, to)) return e;
+        worst = std::max(worst, secs);
+        all_timed_out &= to;
+    }
+    if (seconds) *seconds = worst;
+    if (all_timed_out) {
         ctx->last_error = "png wavefront hand-off timed out";
         return ZPX_E_HIP;
     }
