@@ -142,17 +142,17 @@ struct PngBandPlan {
     std::vector<DevPngBand> sched;
 };
 int png_band_granules(int depth, uint32_t max_row_bytes);      // kernels.h
-bool png_pair_supported(int depth, int interlace, bool use_trns); // kernels.h
+bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride); // kernels.h
 // Which kernel takes a PNG image: the paired-row kernel wherever it
 // supports the depth (ZPX_PNG_PAIR=0 forces the one-row-per-lane kernel, for
 // A/B runs).
-inline bool png_use_pair(int depth, int interlace, bool use_trns)
+inline bool png_use_pair(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride)
 {
     static const bool off = [] {
         const char *e = getenv("ZPX_PNG_PAIR");
         return e && e[0] == '0';
     }();
-    return !off && png_pair_supported(depth, interlace, use_trns);
+    return !off && png_pair_supported(depth, interlace, use_trns, width, out_stride);
 }
 inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> &passes,
                                   const std::vector<uint32_t> &rowbytes)

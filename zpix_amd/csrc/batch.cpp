@@ -371,7 +371,7 @@ int Pipeline::issue_png(Slot &s)
     std::vector<uint32_t> rowbytes;
     uint64_t bytes = 0;
     png_frame_passes(f, passes, rowbytes, bytes);
-    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent);
+    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W, img_stride);
     const PngBandPlan bp = png_plan_bands(ps.depth, pair, passes, rowbytes);
     const std::vector<DevPngBand> &sched = bp.sched; // output-row order (api_internal.h)
     const uint32_t granules = bp.granules;
@@ -453,8 +453,7 @@ int Pipeline::issue(Slot &s, bool &sync_done)
     }
     if (d.fmt == 2)
         for (int p = 0; p < d.ps.npasses; p++)
-            if (!png_band_fits(d.ps.pass[p].row_bytes,
-                               png_use_pair(d.ps.depth, d.ps.interlace, d.ps.use_transparent) ? 128 : 64)) {
+            if (!png_band_fits(d.ps.pass[p].row_bytes, 64)) { // (the paired-row kernel declines wider bands)
                 it.status = ZPX_E_UNSUPPORTED;
                 sync_done = true;
                 return ZPX_OK;

@@ -239,33 +239,45 @@ __device__ __forceinline__ void load_dwords(uint32_t (&d)[N], Rsrc rsrc, int off
         d[T + 2] = v[2];
     }
 }
-// the same, dword by dword, for a lane whose group may start before its row
-// (any offset < 0 is selected out of range: the range check does not wrap
-// voffset + the instruction's immediate)
-template <int N>
-__device__ __forceinline__ void load_dwords_neg(uint32_t (&d)[N], Rsrc rsrc, int off)
-{
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        const int o = off + 4 * i;
-        d[i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
-    }
-}
-
-__device__ __forceinline__ uint64_t ld_sc1_64(const uint64_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1_64(uint64_t *p, uint64_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// Polls one window of boundary granules (lane l holds granules 2l, 2l+1 at
+// offset o) until every granule the band reads carries `epoch`; bounded:
+// past spin_limit polls (or once any wave has timed out: the status word)
+// it sets the status word and gives up.  Out of line: the group loop's own
+// loads keep exact s_waitcnt counts.
+struct Polled {
+    v4u w;
+    uint32_t timed_out;
+};
+__device__ __noinline__ Polled poll_window(Rsrc rsrc, int o, int need, uint32_t epoch, uint32_t spin_limit,
+                                           uint32_t *status)
+{
+    const int lane = threadIdx.x;
+    v4u w = v4u{0, 0, 0, 0};
+    for (uint32_t spins = 1;; spins++) {
+        if (spins > spin_limit ||
+            ((spins & 255) == 0 && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+            if (lane == 0) atomicOr(status, 1u);
+            return Polled{w, 1u};
+        }
+        __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
+        w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 16 /* sc1 */);
+        const bool ok = (2 * lane >= need || w[1] == epoch) && (2 * lane + 1 >= need || w[3] == epoch);
+        if (__ballot(!ok) == 0) return Polled{w, 0u};
+    }
+}
+
+// Cache policy of the boundary hand-off (agent scope, the data is the flag):
+// sc1 on the loads and stores (MI355X_MICROARCH.md, inter-workgroup visibility)
+constexpr int kSc1 = 16;
+// an offset every buffer access drops (stores) or reads as zero (loads)
+constexpr int kOOR = 0x7ffffff0;
 
 template <int DEPTH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
@@ -276,10 +288,10 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
     constexpr int BPP = T::BPP, CB = T::CB, CW = T::CW, C = T::C;
     constexpr int GD = kG * CW + 1;         // input dwords per row per group (+1: alignbyte carry)
     constexpr int RS = kSlots * CW + 1;     // ring dwords per row (odd: spreads the banks)
-    constexpr int WINP = kG * CB;           // boundary window: packed pairs of kG chunks
+    constexpr int WG = kG * CW;             // boundary granules of one window (kG chunks)
+    static_assert(WG % 2 == 0, "window loads are granule pairs");
     __shared__ __attribute__((aligned(16))) uint32_t ring[128 * RS + 4]; // + a trash slot
-    __shared__ __attribute__((aligned(16))) uint32_t win[WINP];
-    __shared__ uint32_t list[128];
+    __shared__ __attribute__((aligned(16))) uint32_t fstate[128];
     constexpr int kTrash = 128 * RS;
 
     const int lane = threadIdx.x;
@@ -325,27 +337,38 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         }
 
         // band input: one descriptor from the dword below the band's first
-        // byte over its rows + ZPX_PNG_INPUT_PAD
+        // byte over its rows + ZPX_PNG_INPUT_PAD.  The host routes passes with
+        // rows shorter than a chunk to the one-row kernel, so no lane's group
+        // ever starts before the descriptor (skew <= row index).
         const uint8_t *band0 = ps.filtered + static_cast<size_t>(base) * (rb + 1);
         const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
         const uint32_t delta = static_cast<uint32_t>(band0 - base4);
         const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
-        const Rsrc rsrc = make_rsrc(base4, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
+        const Rsrc in_rsrc = make_rsrc(base4, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
         const uint32_t roff0 = delta + static_cast<uint32_t>(2 * lane) * (rb + 1); // filter byte of row 2j
         const uint32_t roff1 = roff0 + rb + 1;
         const uint32_t mis0 = (roff0 + 1) & 3, mis1 = (roff1 + 1) & 3;
         const int doff0 = static_cast<int>(roff0 + 1 - mis0) - skew0 * CB; // group 0's first dword, row 2j
         const int doff1 = static_cast<int>(roff1 + 1 - mis1) - skew1 * CB;
 
+        // boundary hand-off: the previous band's last row (read by lane 0
+        // only; everyone else's offsets are out of range) and this band's
+        // last row (written by lane 63 only), both through descriptors whose
+        // extent is zero when there is no such band
         const bool has_prev = bd.band > 0, has_next = bd.band + 1 < ps.nbands;
-        const bool dep_first = (__ballot(ft0 >= 2) & 1ull) != 0; // row 0 of the band reads the row above
-        const bool wait_prev = has_prev && dep_first;
-        const uint64_t *prev_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) * band_granules;
-        uint64_t *my_bnd = boundary + static_cast<size_t>(ps.band_base + bd.band) * band_granules;
-        const uint64_t ep64 = static_cast<uint64_t>(epoch) << 32;
+        const bool wait_prev = has_prev && (__ballot(ft0 >= 2) & 1ull) != 0; // row 0 reads the row above
+        const uint32_t gbytes = band_granules * 8u;
+        const Rsrc prev_rsrc = make_rsrc(boundary + static_cast<size_t>(ps.band_base + bd.band - (has_prev ? 1 : 0)) *
+                                                        band_granules, wait_prev ? gbytes : 0u);
+        const Rsrc next_rsrc = make_rsrc(boundary + static_cast<size_t>(ps.band_base + bd.band) * band_granules,
+                                         has_next ? gbytes : 0u);
 
-        gu8 *out0 = (gu8 *)(ps.out + static_cast<size_t>(y0 * ps.yf + ps.yo) * ps.out_stride);
-        gu8 *out1 = (gu8 *)(ps.out + static_cast<size_t>(y1 * ps.yf + ps.yo) * ps.out_stride);
+        // band output: rows base .. base+127 of the pass in the image
+        const uint64_t orow_bytes = static_cast<uint64_t>(ps.yf) * ps.out_stride; // one pass row to the next
+        gu8 *obase = (gu8 *)(ps.out + static_cast<size_t>(base * ps.yf + ps.yo) * ps.out_stride);
+        const uint64_t oext = static_cast<uint64_t>(band_rows) * orow_bytes;
+        const Rsrc out_rsrc = make_rsrc(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(obase)),
+                                        oext > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(oext));
 
         // per-row state
         uint32_t outp[CB], left[BPP], ul[BPP];
@@ -358,128 +381,128 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         int fl0 = 0, fl1 = 0;                                           // blocks of 8 chunks flushed
         const int ring0 = (2 * lane) * RS, ring1 = ring0 + RS;
 
-        // input double buffer: A = the group being reconstructed, B = the next
+        // every buffer access of the group loop is unconditional (masked
+        // lanes use out-of-range offsets), so the number of vector memory
+        // instructions per group is fixed and s_waitcnt counts stay exact:
+        // a group waits only for the loads issued one group earlier
         uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
         auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
-            const int o0 = doff0 + g0 * CB, o1 = doff1 + g0 * CB;
-            if (__ballot(o0 < 0 || o1 < 0) != 0) {
-                load_dwords_neg<GD>(d0, rsrc, o0);
-                load_dwords_neg<GD>(d1, rsrc, o1);
-            } else {
-                load_dwords<GD>(d0, rsrc, o0);
-                load_dwords<GD>(d1, rsrc, o1);
-            }
+            load_dwords<GD>(d0, in_rsrc, doff0 + g0 * CB);
+            load_dwords<GD>(d1, in_rsrc, doff1 + g0 * CB);
+        };
+        // window of kG chunks of the previous band's last row: WG granules
+        // {data, epoch}; lane l < WG/2 holds granules 2l, 2l+1 (one 16-byte
+        // load), and each step hands its chunk's data dwords to lane 0's DPP
+        // `old` operand through v_readlane (SGPRs)
+        v4u W, Wn;
+        auto load_window = [&](v4u &w, int g0) {
+            const int o = 2 * lane < WG ? (g0 * CW + 2 * lane) * 8 : kOOR;
+            w = __builtin_amdgcn_raw_buffer_load_b128(prev_rsrc, o, 0, kSc1);
         };
 
-        // the previous band's last row, chunks [g0, g0 + kG): wait until
-        // every granule of the window carries this launch's epoch, then stage
-        // it in LDS as packed "old" operands (byte << 16) for lane 0's DPP
-        auto wait_window = [&](int g0) {
-            const int nwc = min(kG, nchunks - g0);
-            if (nwc <= 0) return;
-            const int ng = nwc * CW; // granules (<= 16): lanes 0..7 take 2 each
-            const bool mine = 2 * lane < ng;
-            const uint64_t *src = prev_bnd + static_cast<size_t>(g0) * CW + (mine ? 2 * lane : 0);
-            uint64_t ga = 0, gb = 0;
-            uint32_t spins = 0;
-            for (;;) {
-                ga = ld_sc1_64(src);
-                gb = ld_sc1_64(src + 1);
-                const bool ready = !mine || ((ga >> 32) == epoch && (2 * lane + 1 >= ng || (gb >> 32) == epoch));
-                if (__ballot(!ready) == 0) break;
-                if (timed_out) break;
-                ++spins;
-                if (spins > spin_limit ||
-                    ((spins & 255) == 0 && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-                    timed_out = true;
-                    if (lane == 0) atomicOr(status, 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
-            }
-            if (mine) {
-                const uint32_t da = static_cast<uint32_t>(ga), db = static_cast<uint32_t>(gb);
-                v4u p, q;
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    p[b] = ((da >> (8 * b)) & 0xffu) << 16;
-                    q[b] = ((db >> (8 * b)) & 0xffu) << 16;
-                }
-                *reinterpret_cast<v4u *>(&win[8 * lane]) = p;
-                *reinterpret_cast<v4u *>(&win[8 * lane + 4]) = q;
-            }
-            wave_lds_sync();
-        };
-
-        // every kG steps: rows that completed an aligned block of 8 full
-        // chunks are listed, 8 lanes per listed row store it from the ring
+        // every kG steps: each row that completed an aligned block of 8 full
+        // chunks (one 128-byte line of RGBA8) posts it; in round i, lanes
+        // 8g..8g+7 store row 8i+g's posted block from the ring, one chunk each
         auto flush = [&](int t_end) {
             const int d0 = ok0 ? min(max(t_end - skew0, 0), nchunks) : 0;
             const int d1 = ok1 ? min(max(t_end - skew1, 0), nchunks) : 0;
             const bool p0 = (min(d0, nfull) >> 3) > fl0, p1 = (min(d1, nfull) >> 3) > fl1;
-            const uint64_t b0 = __ballot(p0), b1 = __ballot(p1);
-            const int n = __builtin_popcountll(b0) + __builtin_popcountll(b1);
-            if (n == 0) return;
-            const int r0 = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b0 >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b0), 0));
-            const int r1 = __builtin_popcountll(b0) +
-                           __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b1 >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b1), 0));
-            if (p0) list[r0] = static_cast<uint32_t>(2 * lane) << 16 | static_cast<uint32_t>(fl0);
-            if (p1) list[r1] = static_cast<uint32_t>(2 * lane + 1) << 16 | static_cast<uint32_t>(fl1);
-            wave_lds_sync();
-            for (int e0 = 0; e0 < n; e0 += 8) {
-                const int e = e0 + (lane >> 3);
-                if (e < n) {
-                    const uint32_t ent = list[e];
-                    const int r = static_cast<int>(ent >> 16);
-                    const int k = static_cast<int>(ent & 0xffffu) * 8 + (lane & 7);
-                    const uint32_t *src = &ring[r * RS + (k % kSlots) * CW];
-                    uint32_t ob[4];
-#pragma unroll
-                    for (int i = 0; i < CW; i++) ob[i] = src[i];
-                    if constexpr (CW == 3) ob[3] = 0;
-                    const uint32_t y = base + static_cast<uint32_t>(r);
-                    gu8 *orow = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
-                    put_chunk<DEPTH>(ps, orow, k, expand_chunk<DEPTH>(ps, ob));
-                }
-            }
+            *reinterpret_cast<v2u *>(&fstate[2 * lane]) = v2u{p0 ? static_cast<uint32_t>(fl0) : 0xffffu,
+                                                               p1 ? static_cast<uint32_t>(fl1) : 0xffffu};
             fl0 += p0 ? 1 : 0;
             fl1 += p1 ? 1 : 0;
-            wave_lds_sync(); // the list is rewritten at the next flush
+            wave_lds_sync();
+            auto round = [&](int i, auto &&store) __attribute__((always_inline)) {
+                const int r = 8 * i + (lane >> 3);
+                const uint32_t blk = fstate[r];
+                const bool post = blk != 0xffffu;
+                const int k = static_cast<int>(post ? blk : 0u) * 8 + (lane & 7);
+                const uint32_t *src = &ring[r * RS + (k % kSlots) * CW];
+                uint32_t ob[4];
+#pragma unroll
+                for (int w = 0; w < CW; w++) ob[w] = src[w];
+                if constexpr (CW == 3) ob[3] = 0;
+                store(post, r * static_cast<int>(orow_bytes), k, expand_chunk<DEPTH>(ps, ob));
+            };
+            if (ps.xf == 1) { // contiguous rows: one 16-byte store per chunk
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    round(i, [&](bool post, int ro, int k, v4u v) {
+                        __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc, post ? ro + k * 16 : kOOR, 0, 0);
+                    });
+            } else { // Adam7 pass: pixels xf apart
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    round(i, [&](bool post, int ro, int k, v4u v) {
+#pragma unroll
+                        for (int u = 0; u < C; u++) {
+                            const int xo =
+                                static_cast<int>((static_cast<uint32_t>(k * C + u) * ps.xf + ps.xo) * T::OBPX);
+                            if constexpr (T::OBPX == 8)
+                                __builtin_amdgcn_raw_buffer_store_b64(v2u{v[2 * u], v[2 * u + 1]}, out_rsrc,
+                                                                      post ? ro + xo : kOOR, 0, 0);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b32(v[u], out_rsrc, post ? ro + xo : kOOR, 0, 0);
+                        }
+                    });
+            }
         };
 
         load_group(B0, B1, 0);
+        load_window(Wn, 0);
+        // A group waits for its inputs with s_waitcnt vmcnt(N), N = the
+        // vector memory operations issued since them: the previous group's
+        // publish stores (2 per step) and flush stores (16).  The first
+        // group's N must agree (the count is static, merged over the loop
+        // entry and back edge), so the same number of dropped stores follows
+        // the first loads here.
+        {
+            const Rsrc none = make_rsrc(base4, 0u); // extent 0: every store is dropped
+#pragma unroll
+            for (int i = 0; i < 2 * kG + 16; i++)  // distinct, unmergeable offsets
+                __builtin_amdgcn_raw_buffer_store_b32(0u, none, 4096 * i + lane * 4, 0, 0);
+        }
         for (int g0 = 0; g0 < nsteps; g0 += kG) {
 #pragma unroll
             for (int i = 0; i < GD; i++) {
                 A0[i] = B0[i];
                 A1[i] = B1[i];
             }
-            if (g0 + kG < nsteps) load_group(B0, B1, g0 + kG);
-            if (wait_prev) wait_window(g0);
+            W = Wn;
+            load_group(B0, B1, g0 + kG);
+            load_window(Wn, g0 + kG);
+            if (wait_prev) {
+                // lane 0's window must carry this launch's epoch in every
+                // granule the band reads (chunks < nchunks); else poll
+                const int need = min(kG, nchunks - g0) * CW; // granules the band reads
+                const bool ok = (2 * lane >= need || W[1] == epoch) && (2 * lane + 1 >= need || W[3] == epoch);
+                if (__ballot(!ok) != 0 && !timed_out) { // the producer is behind: poll (rare, out of line)
+                    const int o = 2 * lane < WG ? (g0 * CW + 2 * lane) * 8 : kOOR;
+                    const Polled pw = poll_window(prev_rsrc, o, need, epoch, spin_limit, status);
+                    W = pw.w;
+                    timed_out = pw.timed_out != 0;
+                }
+            }
 #pragma unroll
             for (int st = 0; st < kG; st++) {
-                const int step = g0 + st;
-                // ---- the row above, one step late
-                uint32_t up[CB];
-                if (wait_prev && step < nchunks) { // lane 0's old operand: the previous band's last row
+                // ---- the row above, one step late; lane 0's DPP `old` is the
+                // previous band's last row (zero without one: out-of-range loads)
+                uint32_t up[CB], gdat[CW];
 #pragma unroll
-                    for (int i = 0; i < CB; i++) {
-                        const uint32_t old = win[st * CB + i];
-                        up[i] = __builtin_amdgcn_alignbit(
-                            outp[i], static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(old),
-                                                                                      static_cast<int>(outp[i]),
-                                                                                      0x138, 0xf, 0xf, false)),
-                            16);
-                    }
-                } else {
+                for (int w = 0; w < CW; w++) { // granule st*CW+w: lane (st*CW+w)/2, dword 0 or 2
+                    const int gi = st * CW + w;
+                    gdat[w] = static_cast<uint32_t>(
+                        __builtin_amdgcn_readlane(static_cast<int>((gi & 1) ? W[2] : W[0]), gi >> 1));
+                }
 #pragma unroll
-                    for (int i = 0; i < CB; i++)
-                        up[i] = __builtin_amdgcn_alignbit(
-                            outp[i], static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
-                                         0, static_cast<int>(outp[i]), 0x138, 0xf, 0xf, false)),
-                            16);
+                for (int i = 0; i < CB; i++) {
+                    const uint32_t g = gdat[i >> 2];
+                    const uint32_t old = __builtin_amdgcn_perm(0u, g, 0x0c000c0cu | static_cast<uint32_t>(i & 3) << 16);
+                    up[i] = __builtin_amdgcn_alignbit(
+                        outp[i],
+                        static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(old), static_cast<int>(outp[i]),
+                                                                          0x138, 0xf, 0xf, false)),
+                        16);
                 }
                 // ---- filtered bytes of both rows' chunks, packed
                 uint32_t f[CB];
@@ -532,11 +555,16 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                     d0[w] = lo[w];
                     d1[w] = hi[w];
                 }
-                // ---- publish the band's last row (row 127, lane 63's high half): the data is the flag
-                if (has_next && lane == 63 && act1) {
-                    uint64_t *dst = my_bnd + static_cast<size_t>(k1) * CW;
-#pragma unroll
-                    for (int w = 0; w < CW; w++) st_sc1_64(dst + w, ep64 | hi[w]);
+                // ---- publish the band's last row (row 127: lane 63's high
+                // half) as {epoch, data} granules: the data is the flag
+                {
+                    const int po = (lane == 63 && act1) ? k1 * CW * 8 : kOOR;
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{hi[0], epoch, hi[1], epoch}, next_rsrc, po, 0, kSc1);
+                    if constexpr (CW == 4)
+                        __builtin_amdgcn_raw_buffer_store_b128(v4u{hi[2], epoch, hi[3], epoch}, next_rsrc, po + 16, 0,
+                                                               kSc1);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b64(v2u{hi[2], epoch}, next_rsrc, po + 16, 0, kSc1);
                 }
                 k0++;
                 k1++;
@@ -545,9 +573,11 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             }
             wave_lds_sync();
             flush(g0 + kG);
+            wave_lds_sync(); // fstate is rewritten at the next flush
         }
         // ---- row tails: the last (< 8) full chunks and a partial one
-        wave_lds_sync();
+        gu8 *out0 = obase + static_cast<size_t>(2 * lane) * orow_bytes;
+        gu8 *out1 = out0 + orow_bytes;
         for (int h = 0; h < 2; h++) {
             const bool ok = h ? ok1 : ok0;
             if (!ok) continue;
@@ -602,13 +632,33 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
 
 } // namespace
 
-bool png_pair_supported(int depth, int interlace, bool use_trns)
+bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride)
 {
+    int bpp = 0, cb = 16;
     switch (depth) {
-    case ZPX_PNG_TC8: case ZPX_PNG_TCA8: case ZPX_PNG_TC16: case ZPX_PNG_TCA16: return true;
-    case ZPX_PNG_G8: case ZPX_PNG_G16: return !interlace && !use_trns;
+    case ZPX_PNG_TC8: bpp = 3; cb = 12; break;
+    case ZPX_PNG_TCA8: bpp = 4; break;
+    case ZPX_PNG_TC16: bpp = 6; cb = 12; break;
+    case ZPX_PNG_TCA16: bpp = 8; break;
+    case ZPX_PNG_G8: bpp = 1; break;
+    case ZPX_PNG_G16: bpp = 2; break;
     default: return false;
     }
+    if ((depth == ZPX_PNG_G8 || depth == ZPX_PNG_G16) && (interlace || use_trns)) return false;
+    // every (non-empty) pass row holds at least one chunk's bytes (no lane's
+    // group starts before the band), and a band's 128 pass rows of output
+    // span less than the 2 GiB buffer range
+    static const uint32_t kA7[7][2] = {{0, 8}, {4, 8}, {0, 4}, {2, 4}, {0, 2}, {1, 2}, {0, 1}}; // xo, xf
+    uint32_t min_w = width;
+    if (interlace)
+        for (const auto &p : kA7) {
+            const uint32_t w = ((width > p[0] ? width - p[0] : 0) + p[1] - 1) / p[1];
+            if (w) min_w = w < min_w ? w : min_w;
+        }
+    if (uint64_t(min_w) * bpp + 1 < uint64_t(cb)) return false;
+    const uint64_t yf = interlace ? 8 : 1;
+    const uint64_t in_band = 128ull * (uint64_t(width) * bpp + 1) + ZPX_PNG_INPUT_PAD + 4;
+    return in_band < 0x7ffffff0ull && 128ull * yf * out_stride < 0x7ffffff0ull;
 }
 
 int launch_png_pair(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,

@@ -525,7 +525,8 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
     std::map<std::pair<int, bool>, std::vector<int>> by_depth;
     for (int i = 0; i < n_frames; i++) {
         if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
-        const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, frames[i].use_transparent != 0);
+        const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, frames[i].use_transparent != 0,
+                                       frames[i].width, frames[i].out_stride);
         by_depth[{frames[i].depth, pair}].push_back(i);
     }
     uint64_t bytes = 0;
