@@ -56,8 +56,8 @@ typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gptr(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
-constexpr int kG = 4;       // steps per group (input burst, flush period)
-constexpr int kSlots = 12;  // ring slots per row: an 8-chunk block + one group's chunks fit
+constexpr int kG = 8;       // steps per group (input burst, flush period)
+constexpr int kSlots = 16;  // ring slots per row: a pending block's 7 + one group's 8 chunks fit
 #ifndef ZPX_PNG_SLEEP
 #define ZPX_PNG_SLEEP 2
 #endif
@@ -117,9 +117,9 @@ __device__ __forceinline__ PairFilter half_filter(int ft, int h)
     return PairFilter{keep << sh, force << sh};
 }
 
-// One byte pair: out = (f + predictor) mod 256 per half.
+// One byte pair: out = (f + predictor) mod 256 per half (zero where vmask says so).
 __device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, uint32_t ka,
-                                               uint32_t c2, PairFilter pf)
+                                               uint32_t c2, PairFilter pf, uint32_t vmask)
 {
     const uint32_t pb = pk_absdiff(a, c);
     const uint32_t s = pk_add(a, b);
@@ -131,7 +131,7 @@ __device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t 
     const uint32_t ab = a | (b << 8);
     const uint32_t cav = c | (pk_shr1(s) << 8);
     const uint32_t t = __builtin_amdgcn_perm(cav, ab, sel);
-    return (f + t) & 0x00ff00ffu;
+    return (f + t) & vmask; // vmask: 0x00ff per half, 0 while a row is before its first chunk
 }
 
 // ---- output of one chunk: the 16 bytes store_chunk writes (readImagePass
@@ -141,10 +141,10 @@ __device__ __forceinline__ v4u expand_chunk(const DevPngPass &ps, const uint32_t
 {
     if constexpr (DEPTH == ZPX_PNG_TC8) { // RGBA, alpha 0xff (NRGBA with the colour key)
         v4u w;
-        w[0] = __builtin_amdgcn_perm(ob[0], ob[0], 0x0c020100u) | 0xff000000u;
-        w[1] = __builtin_amdgcn_perm(ob[1], ob[0], 0x0c050403u) | 0xff000000u;
-        w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x0c040302u) | 0xff000000u;
-        w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0c030201u) | 0xff000000u;
+        w[0] = __builtin_amdgcn_perm(ob[0], ob[0], 0x0d020100u); // selector 0x0d: byte 0xff
+        w[1] = __builtin_amdgcn_perm(ob[1], ob[0], 0x0d050403u);
+        w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x0d040302u);
+        w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0d030201u);
         if (ps.use_trns) {
             const uint32_t key = uint32_t(ps.trns[1]) | uint32_t(ps.trns[3]) << 8 | uint32_t(ps.trns[5]) << 16;
 #pragma unroll
@@ -273,6 +273,18 @@ __device__ __noinline__ Polled poll_window(Rsrc rsrc, int o, int need, uint32_t 
     }
 }
 
+// ZPX_PNG_TRACE=1 (diagnostic builds only): per ticket, lane 0 records the
+// band's start and end (s_memrealtime, 100 MHz), its wave's HW_ID and XCC_ID
+// and the wave's first ticket, read back with zpx_debug_png_trace.  No output
+// value depends on it.
+#ifndef ZPX_PNG_TRACE
+#define ZPX_PNG_TRACE 0
+#endif
+#if ZPX_PNG_TRACE
+constexpr int kTraceMax = 1 << 14;
+__device__ uint64_t g_png_trace[kTraceMax * 4];
+#endif
+
 // Cache policy of the boundary hand-off (agent scope, the data is the flag):
 // sc1 on the loads and stores (MI355X_MICROARCH.md, inter-workgroup visibility)
 constexpr int kSc1 = 16;
@@ -280,18 +292,18 @@ constexpr int kSc1 = 16;
 constexpr int kOOR = 0x7ffffff0;
 
 template <int DEPTH>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__restrict__ sched, uint32_t nsched,
                      uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit)
 {
     using T = PairTraits<DEPTH>;
     constexpr int BPP = T::BPP, CB = T::CB, CW = T::CW, C = T::C;
     constexpr int GD = kG * CW + 1;         // input dwords per row per group (+1: alignbyte carry)
-    constexpr int RS = kSlots * CW + 1;     // ring dwords per row (odd: spreads the banks)
+    constexpr int RS = kSlots * 4 + 4;      // ring dwords per row: 16 output chunks of 16 bytes + 16 bytes of bank skew
     constexpr int WG = kG * CW;             // boundary granules of one window (kG chunks)
-    static_assert(WG % 2 == 0, "window loads are granule pairs");
+    static_assert(WG % 2 == 0 && WG / 2 <= 64, "window loads are granule pairs, one per lane");
     __shared__ __attribute__((aligned(16))) uint32_t ring[128 * RS + 4]; // + a trash slot
-    __shared__ __attribute__((aligned(16))) uint32_t fstate[128];
+    __shared__ __attribute__((aligned(16))) uint32_t fst[128];           // flush state, [row % 8][row / 8]
     constexpr int kTrash = 128 * RS;
 
     const int lane = threadIdx.x;
@@ -305,6 +317,9 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
         if (t >= nsched) break;
         const DevPngBand bd = sched[t];
+#if ZPX_PNG_TRACE
+        const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const DevPngPass ps = passes[bd.pass];
         const uint32_t rb = ps.row_bytes;
         const int nchunks = static_cast<int>(((rb + BPP - 1) / BPP + C - 1) / C);
@@ -351,10 +366,10 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const int doff0 = static_cast<int>(roff0 + 1 - mis0) - skew0 * CB; // group 0's first dword, row 2j
         const int doff1 = static_cast<int>(roff1 + 1 - mis1) - skew1 * CB;
 
-        // boundary hand-off: the previous band's last row (read by lane 0
-        // only; everyone else's offsets are out of range) and this band's
-        // last row (written by lane 63 only), both through descriptors whose
-        // extent is zero when there is no such band
+        // boundary hand-off: the previous band's last row (read by lanes
+        // 0..WG/2-1, one granule pair each; offsets out of range otherwise)
+        // and this band's last row (written by lane 63 only), both through
+        // descriptors whose extent is zero when there is no such band
         const bool has_prev = bd.band > 0, has_next = bd.band + 1 < ps.nbands;
         const bool wait_prev = has_prev && (__ballot(ft0 >= 2) & 1ull) != 0; // row 0 reads the row above
         const uint32_t gbytes = band_granules * 8u;
@@ -370,15 +385,15 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const Rsrc out_rsrc = make_rsrc(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(obase)),
                                         oext > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(oext));
 
-        // per-row state
-        uint32_t outp[CB], left[BPP], ul[BPP];
+        // per-row state: the previous step's output bytes of both rows (the
+        // row above of the next step), and the last pixel's pairs
+        uint32_t plo[CW], phi[CW], left[BPP], ul[BPP];
 #pragma unroll
-        for (int i = 0; i < CB; i++) outp[i] = 0;
+        for (int w = 0; w < CW; w++) plo[w] = phi[w] = 0;
 #pragma unroll
         for (int i = 0; i < BPP; i++) left[i] = ul[i] = 0;
-        int k0 = -skew0, k1 = -skew1;                                   // chunk of the current step
-        int s0 = ((k0 % kSlots) + kSlots) % kSlots, s1 = ((k1 % kSlots) + kSlots) % kSlots; // k mod 12
-        int fl0 = 0, fl1 = 0;                                           // blocks of 8 chunks flushed
+        int k0 = -skew0, k1 = -skew1; // chunk of the current step
+        int fl0 = 0, fl1 = 0;         // blocks of 8 chunks flushed
         const int ring0 = (2 * lane) * RS, ring1 = ring0 + RS;
 
         // every buffer access of the group loop is unconditional (masked
@@ -407,22 +422,27 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             const int d0 = ok0 ? min(max(t_end - skew0, 0), nchunks) : 0;
             const int d1 = ok1 ? min(max(t_end - skew1, 0), nchunks) : 0;
             const bool p0 = (min(d0, nfull) >> 3) > fl0, p1 = (min(d1, nfull) >> 3) > fl1;
-            *reinterpret_cast<v2u *>(&fstate[2 * lane]) = v2u{p0 ? static_cast<uint32_t>(fl0) : 0xffffu,
-                                                               p1 ? static_cast<uint32_t>(fl1) : 0xffffu};
+            const int r0 = 2 * lane, r1 = r0 + 1; // row r's state at fst[(r % 8) * 16 + r / 8]
+            fst[(r0 & 7) * 16 + (r0 >> 3)] = p0 ? static_cast<uint32_t>(fl0) : 0xffffu;
+            fst[(r1 & 7) * 16 + (r1 >> 3)] = p1 ? static_cast<uint32_t>(fl1) : 0xffffu;
             fl0 += p0 ? 1 : 0;
             fl1 += p1 ? 1 : 0;
             wave_lds_sync();
+            uint32_t blk[16]; // this lane group's rows 8i + g, i = 0..15
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const v4u v = *reinterpret_cast<const v4u *>(&fst[(lane >> 3) * 16 + 4 * q]);
+                blk[4 * q] = v[0];
+                blk[4 * q + 1] = v[1];
+                blk[4 * q + 2] = v[2];
+                blk[4 * q + 3] = v[3];
+            }
             auto round = [&](int i, auto &&store) __attribute__((always_inline)) {
                 const int r = 8 * i + (lane >> 3);
-                const uint32_t blk = fstate[r];
-                const bool post = blk != 0xffffu;
-                const int k = static_cast<int>(post ? blk : 0u) * 8 + (lane & 7);
-                const uint32_t *src = &ring[r * RS + (k % kSlots) * CW];
-                uint32_t ob[4];
-#pragma unroll
-                for (int w = 0; w < CW; w++) ob[w] = src[w];
-                if constexpr (CW == 3) ob[3] = 0;
-                store(post, r * static_cast<int>(orow_bytes), k, expand_chunk<DEPTH>(ps, ob));
+                const bool post = blk[i] != 0xffffu;
+                const int k = static_cast<int>(post ? blk[i] : 0u) * 8 + (lane & 7);
+                const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + (k & (kSlots - 1)) * 4]);
+                store(post, r * static_cast<int>(orow_bytes), k, v);
             };
             if (ps.xf == 1) { // contiguous rows: one 16-byte store per chunk
 #pragma unroll
@@ -472,8 +492,8 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             load_group(B0, B1, g0 + kG);
             load_window(Wn, g0 + kG);
             if (wait_prev) {
-                // lane 0's window must carry this launch's epoch in every
-                // granule the band reads (chunks < nchunks); else poll
+                // the window must carry this launch's epoch in every granule
+                // the band reads (chunks < nchunks); else poll
                 const int need = min(kG, nchunks - g0) * CW; // granules the band reads
                 const bool ok = (2 * lane >= need || W[1] == epoch) && (2 * lane + 1 >= need || W[3] == epoch);
                 if (__ballot(!ok) != 0 && !timed_out) { // the producer is behind: poll (rare, out of line)
@@ -485,24 +505,21 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             }
 #pragma unroll
             for (int st = 0; st < kG; st++) {
-                // ---- the row above, one step late; lane 0's DPP `old` is the
-                // previous band's last row (zero without one: out-of-range loads)
-                uint32_t up[CB], gdat[CW];
+                // ---- the row above, one step late: row 2j reads lane j-1's
+                // high row (DPP wave_shr:1; lane 0's `old` is the previous
+                // band's last row, zero without one), row 2j+1 its own low row
+                uint32_t up[CB];
 #pragma unroll
-                for (int w = 0; w < CW; w++) { // granule st*CW+w: lane (st*CW+w)/2, dword 0 or 2
-                    const int gi = st * CW + w;
-                    gdat[w] = static_cast<uint32_t>(
+                for (int w = 0; w < CW; w++) {
+                    const int gi = st * CW + w; // granule: lane gi/2, dword 0 or 2
+                    const uint32_t old = static_cast<uint32_t>(
                         __builtin_amdgcn_readlane(static_cast<int>((gi & 1) ? W[2] : W[0]), gi >> 1));
-                }
+                    const uint32_t dh = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                        static_cast<int>(old), static_cast<int>(phi[w]), 0x138, 0xf, 0xf, false));
 #pragma unroll
-                for (int i = 0; i < CB; i++) {
-                    const uint32_t g = gdat[i >> 2];
-                    const uint32_t old = __builtin_amdgcn_perm(0u, g, 0x0c000c0cu | static_cast<uint32_t>(i & 3) << 16);
-                    up[i] = __builtin_amdgcn_alignbit(
-                        outp[i],
-                        static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(old), static_cast<int>(outp[i]),
-                                                                          0x138, 0xf, 0xf, false)),
-                        16);
+                    for (int b = 0; b < 4; b++)
+                        up[4 * w + b] = __builtin_amdgcn_perm(dh, plo[w], 0x0c000c04u | static_cast<uint32_t>(b) << 16 |
+                                                                             static_cast<uint32_t>(b));
                 }
                 // ---- filtered bytes of both rows' chunks, packed
                 uint32_t f[CB];
@@ -514,13 +531,9 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                     for (int b = 0; b < 4; b++)
                         f[4 * w + b] = __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (4u + b) << 16 | static_cast<uint32_t>(b));
                 }
-                // ---- a row's first chunk starts from zero left / up-left (x < bpp)
-                const uint32_t keep = (k0 != 0 ? 0x0000ffffu : 0u) | (k1 != 0 ? 0xffff0000u : 0u);
-#pragma unroll
-                for (int i = 0; i < BPP; i++) {
-                    left[i] &= keep;
-                    ul[i] &= keep;
-                }
+                // ---- a row outputs zeros until its first chunk (k < 0), so
+                // that chunk starts from zero left / up / up-left
+                const uint32_t vmask = (k0 >= 0 ? 0x000000ffu : 0u) | (k1 >= 0 ? 0x00ff0000u : 0u);
                 // ---- reconstruct CB byte pairs, left to right
                 uint32_t o[CB];
 #pragma unroll
@@ -529,53 +542,46 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                     const uint32_t c = i < BPP ? ul[i] : up[i < BPP ? 0 : i - BPP];
                     const uint32_t b = up[i];
                     const uint32_t ka = (pk_absdiff(b, c) << 7) | kKA;
-                    o[i] = recon_pair(f[i], a, b, c, ka, pk_add(c, c), pf);
+                    o[i] = recon_pair(f[i], a, b, c, ka, pk_add(c, c), pf, vmask);
                 }
 #pragma unroll
                 for (int i = 0; i < BPP; i++) {
                     left[i] = o[CB - BPP + i];
                     ul[i] = up[CB - BPP + i];
                 }
-#pragma unroll
-                for (int i = 0; i < CB; i++) outp[i] = o[i];
-                // ---- bytes of each row into its ring slot (or the trash slot)
-                uint32_t lo[CW], hi[CW];
+                // ---- bytes of each row: the next step's row above, the
+                // output chunk (ring slot, or the trash slot), the boundary
 #pragma unroll
                 for (int w = 0; w < CW; w++) {
                     const uint32_t x01 = __builtin_amdgcn_perm(o[4 * w + 1], o[4 * w], 0x06020400u);
                     const uint32_t x23 = __builtin_amdgcn_perm(o[4 * w + 3], o[4 * w + 2], 0x06020400u);
-                    lo[w] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
-                    hi[w] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
+                    plo[w] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
+                    phi[w] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
                 }
                 const bool act0 = ok0 && k0 >= 0 && k0 < nchunks, act1 = ok1 && k1 >= 0 && k1 < nchunks;
-                uint32_t *d0 = &ring[act0 ? ring0 + s0 * CW : kTrash];
-                uint32_t *d1 = &ring[act1 ? ring1 + s1 * CW : kTrash];
-#pragma unroll
-                for (int w = 0; w < CW; w++) {
-                    d0[w] = lo[w];
-                    d1[w] = hi[w];
-                }
+                *reinterpret_cast<v4u *>(&ring[act0 ? ring0 + (k0 & (kSlots - 1)) * 4 : kTrash]) =
+                    expand_chunk<DEPTH>(ps, plo);
+                *reinterpret_cast<v4u *>(&ring[act1 ? ring1 + (k1 & (kSlots - 1)) * 4 : kTrash]) =
+                    expand_chunk<DEPTH>(ps, phi);
                 // ---- publish the band's last row (row 127: lane 63's high
-                // half) as {epoch, data} granules: the data is the flag
+                // half) as {data, epoch} granules: the data is the flag
                 {
                     const int po = (lane == 63 && act1) ? k1 * CW * 8 : kOOR;
-                    __builtin_amdgcn_raw_buffer_store_b128(v4u{hi[0], epoch, hi[1], epoch}, next_rsrc, po, 0, kSc1);
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{phi[0], epoch, phi[1], epoch}, next_rsrc, po, 0, kSc1);
                     if constexpr (CW == 4)
-                        __builtin_amdgcn_raw_buffer_store_b128(v4u{hi[2], epoch, hi[3], epoch}, next_rsrc, po + 16, 0,
-                                                               kSc1);
+                        __builtin_amdgcn_raw_buffer_store_b128(v4u{phi[2], epoch, phi[3], epoch}, next_rsrc, po + 16,
+                                                               0, kSc1);
                     else
-                        __builtin_amdgcn_raw_buffer_store_b64(v2u{hi[2], epoch}, next_rsrc, po + 16, 0, kSc1);
+                        __builtin_amdgcn_raw_buffer_store_b64(v2u{phi[2], epoch}, next_rsrc, po + 16, 0, kSc1);
                 }
                 k0++;
                 k1++;
-                s0 = s0 == kSlots - 1 ? 0 : s0 + 1;
-                s1 = s1 == kSlots - 1 ? 0 : s1 + 1;
             }
             wave_lds_sync();
             flush(g0 + kG);
-            wave_lds_sync(); // fstate is rewritten at the next flush
+            wave_lds_sync(); // fst is rewritten at the next flush
         }
-        // ---- row tails: the last (< 8) full chunks and a partial one
+        // ---- row tails: the last (< 16) unflushed chunks, the last partial
         gu8 *out0 = obase + static_cast<size_t>(2 * lane) * orow_bytes;
         gu8 *out1 = out0 + orow_bytes;
         for (int h = 0; h < 2; h++) {
@@ -585,16 +591,21 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             gu8 *orow = h ? out1 : out0;
             const int rbase = h ? ring1 : ring0;
             for (int k = fl * 8; k < nchunks; k++) {
-                uint32_t ob[4];
-#pragma unroll
-                for (int i = 0; i < CW; i++) ob[i] = ring[rbase + (k % kSlots) * CW + i];
-                if constexpr (CW == 3) ob[3] = 0;
-                const v4u v = expand_chunk<DEPTH>(ps, ob);
+                const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
                 if (k < nfull) put_chunk<DEPTH>(ps, orow, k, v);
                 else put_partial<DEPTH>(ps, orow, k, v, static_cast<int>(ps.width) - k * C);
             }
         }
         wave_lds_sync();
+#if ZPX_PNG_TRACE
+        if (lane == 0 && t < static_cast<uint32_t>(kTraceMax)) {
+            g_png_trace[4 * t] = trace_t0;
+            g_png_trace[4 * t + 1] = __builtin_amdgcn_s_memrealtime();
+            g_png_trace[4 * t + 2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32 |
+                                     static_cast<uint32_t>(__builtin_amdgcn_s_getreg(0xF804));
+            g_png_trace[4 * t + 3] = static_cast<uint64_t>(nsteps) << 32 | static_cast<uint32_t>(max_skew);
+        }
+#endif
     }
 }
 
@@ -631,6 +642,14 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
 }
 
 } // namespace
+
+#if ZPX_PNG_TRACE
+extern "C" int zpx_debug_png_trace(uint64_t *out, size_t n)
+{
+    if (n > size_t(kTraceMax) * 4) n = size_t(kTraceMax) * 4;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_png_trace), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride)
 {
