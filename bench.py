@@ -509,9 +509,10 @@ def main():
         pv = pb.pixels * ws * steps / wall / 1e6
         ach = pb.bytes / (kern_ms * 1e-3) / 1e9
         ptraffic = None
+        pkernel = "png_unfilter_kernel<TC8>" if os.environ.get("ZPX_PNG_PAIR") == "0" else "png_pair_kernel<TC8>"
         try:
-            tp = json.load(open(args.traffic_json)).get("png_unfilter", {})
-            if tp.get("images") == args.images and tp.get("size") == args.size:
+            tp = json.load(open(args.traffic_json)).get("png", {})
+            if tp.get("images") == args.images and tp.get("size") == args.size and tp.get("kernel") == pkernel:
                 ptraffic = tp.get("hbm_bytes_per_launch")
         except Exception:
             ptraffic = None
@@ -519,7 +520,7 @@ def main():
                 "unit": "MPixels/sec", "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
                 "config": {"workload": f"{args.images}x {W}x{H} tc8 PNG unfilter -> RGBA, configs[2]"},
                 "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": ptraffic, "kernel": "png_unfilter_kernel",
+                             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": ptraffic, "kernel": pkernel,
                              "kernel_ms_per_launch": round(kern_ms, 3), "algorithmic_bytes_per_launch": pb.bytes},
                 "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1)}
         if result:

@@ -396,10 +396,14 @@ int Pipeline::issue_png(Slot &s)
     uint8_t *dd = s.ddesc.as<uint8_t>();
     ZPX_TRACE("png: item %d %ux%u depth %d interlace %d passes %zu bands %zu granules %u", d.item, W, H, ps.depth,
               ps.interlace, passes.size(), sched.size(), granules);
-    if ((pair ? launch_png_pair : launch_png_unfilter)(ps.depth, reinterpret_cast<const DevPngPass *>(dd),
-                                                       reinterpret_cast<const DevPngBand *>(dd + pass_b),
-                                                       static_cast<uint32_t>(sched.size()), s.dctl.as<uint32_t>(),
-                                                       s.dbound.as<uint64_t>(), granules, ctx_->stream, 0))
+    const DevPngPass *dp = reinterpret_cast<const DevPngPass *>(dd);
+    const DevPngBand *dsch = reinterpret_cast<const DevPngBand *>(dd + pass_b);
+    const uint32_t ns = static_cast<uint32_t>(sched.size());
+    const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, dp, dsch, ns, s.dctl.as<uint32_t>(),
+                                           s.dbound.as<uint64_t>(), granules, ctx_->stream)
+                         : launch_png_unfilter(ps.depth, dp, dsch, ns, s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(),
+                                               granules, ctx_->stream);
+    if (lrc)
         return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
     HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, ctx_->stream));
     s.check_png = true;

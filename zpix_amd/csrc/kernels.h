@@ -34,8 +34,9 @@ uint32_t png_default_spin_limit();
 // png_pair_kernels.hip: two rows per lane, 128-row bands (the byte-aligned
 // depths whose chunk is 16 output bytes); the rest take launch_png_unfilter
 bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride);
-int launch_png_pair(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
-                    uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit = 0);
+// trns: the images carry a tRNS colour key (RGB8 / RGB16; one value per launch)
+int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
+                    uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit = 0);
 
 // color_kernels.hip
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);

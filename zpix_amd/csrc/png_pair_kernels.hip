@@ -136,7 +136,7 @@ __device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t 
 
 // ---- output of one chunk: the 16 bytes store_chunk writes (readImagePass
 // :947-950, :963-968, :994-1015, :1033-1039, :1062-1078), from CW raw dwords
-template <int DEPTH>
+template <int DEPTH, bool TRNS>
 __device__ __forceinline__ v4u expand_chunk(const DevPngPass &ps, const uint32_t *ob)
 {
     if constexpr (DEPTH == ZPX_PNG_TC8) { // RGBA, alpha 0xff (NRGBA with the colour key)
@@ -145,7 +145,7 @@ __device__ __forceinline__ v4u expand_chunk(const DevPngPass &ps, const uint32_t
         w[1] = __builtin_amdgcn_perm(ob[1], ob[0], 0x0d050403u);
         w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x0d040302u);
         w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0d030201u);
-        if (ps.use_trns) {
+        if constexpr (TRNS) {
             const uint32_t key = uint32_t(ps.trns[1]) | uint32_t(ps.trns[3]) << 8 | uint32_t(ps.trns[5]) << 16;
 #pragma unroll
             for (int u = 0; u < 4; u++)
@@ -159,7 +159,7 @@ __device__ __forceinline__ v4u expand_chunk(const DevPngPass &ps, const uint32_t
         w[1] = __builtin_amdgcn_perm(ob[1], ob[1], 0x0d0d0100u);  // b, alpha ffff
         w[2] = __builtin_amdgcn_perm(ob[2], ob[1], 0x05040302u);  // r, g of pixel 1
         w[3] = __builtin_amdgcn_perm(ob[2], ob[2], 0x0d0d0302u);  // b, alpha ffff
-        if (ps.use_trns) {
+        if constexpr (TRNS) {
             const uint32_t k01 = uint32_t(ps.trns[0]) | uint32_t(ps.trns[1]) << 8 | uint32_t(ps.trns[2]) << 16 |
                                  uint32_t(ps.trns[3]) << 24;
             const uint32_t k2 = uint32_t(ps.trns[4]) | uint32_t(ps.trns[5]) << 8;
@@ -291,7 +291,7 @@ constexpr int kSc1 = 16;
 // an offset every buffer access drops (stores) or reads as zero (loads)
 constexpr int kOOR = 0x7ffffff0;
 
-template <int DEPTH>
+template <int DEPTH, bool TRNS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__restrict__ sched, uint32_t nsched,
                      uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit)
@@ -560,9 +560,9 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 }
                 const bool act0 = ok0 && k0 >= 0 && k0 < nchunks, act1 = ok1 && k1 >= 0 && k1 < nchunks;
                 *reinterpret_cast<v4u *>(&ring[act0 ? ring0 + (k0 & (kSlots - 1)) * 4 : kTrash]) =
-                    expand_chunk<DEPTH>(ps, plo);
+                    expand_chunk<DEPTH, TRNS>(ps, plo);
                 *reinterpret_cast<v4u *>(&ring[act1 ? ring1 + (k1 & (kSlots - 1)) * 4 : kTrash]) =
-                    expand_chunk<DEPTH>(ps, phi);
+                    expand_chunk<DEPTH, TRNS>(ps, phi);
                 // ---- publish the band's last row (row 127: lane 63's high
                 // half) as {data, epoch} granules: the data is the flag
                 {
@@ -619,7 +619,7 @@ __global__ void png_pair_ctl_kernel(uint32_t *ctl)
     ctl[2] = 0;
 }
 
-template <int DEPTH>
+template <int DEPTH, bool TRNS>
 void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
                    uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
 {
@@ -627,7 +627,8 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
     if (per_cu == 0) {
         const char *e = getenv("ZPX_PNG_WAVES_PER_CU");
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH>, 64, 0) != hipSuccess || occ < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH, TRNS>, 64, 0) != hipSuccess ||
+            occ < 1)
             occ = 4;
         per_cu = e ? atoi(e) : occ;
         if (per_cu < 1) per_cu = 1;
@@ -637,8 +638,8 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
     const uint32_t want = static_cast<uint32_t>(cus * per_cu);
     const uint32_t grid = nsched < want ? nsched : want;
     hipLaunchKernelGGL(png_pair_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
-    hipLaunchKernelGGL((png_pair_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
-                       band_granules, spin_limit);
+    hipLaunchKernelGGL((png_pair_kernel<DEPTH, TRNS>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl,
+                       boundary, band_granules, spin_limit);
 }
 
 } // namespace
@@ -680,15 +681,22 @@ bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width,
     return in_band < 0x7ffffff0ull && 128ull * yf * out_stride < 0x7ffffff0ull;
 }
 
-int launch_png_pair(int depth, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
-                    uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit)
+int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
+                    uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit)
 {
     const uint32_t sl = spin_limit ? spin_limit : png_default_spin_limit();
     switch (depth) {
-#define ZPX_CASE(D) case D: launch_pair_t<D>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
-        ZPX_CASE(ZPX_PNG_G8) ZPX_CASE(ZPX_PNG_G16) ZPX_CASE(ZPX_PNG_TC8) ZPX_CASE(ZPX_PNG_TCA8)
-        ZPX_CASE(ZPX_PNG_TC16) ZPX_CASE(ZPX_PNG_TCA16)
+#define ZPX_CASE(D) case D: launch_pair_t<D, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
+        ZPX_CASE(ZPX_PNG_G8) ZPX_CASE(ZPX_PNG_G16) ZPX_CASE(ZPX_PNG_TCA8) ZPX_CASE(ZPX_PNG_TCA16)
 #undef ZPX_CASE
+    case ZPX_PNG_TC8:
+        if (trns) launch_pair_t<ZPX_PNG_TC8, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        else launch_pair_t<ZPX_PNG_TC8, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        break;
+    case ZPX_PNG_TC16:
+        if (trns) launch_pair_t<ZPX_PNG_TC16, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        else launch_pair_t<ZPX_PNG_TC16, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        break;
     default: return -2;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;

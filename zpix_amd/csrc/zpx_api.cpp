@@ -326,6 +326,7 @@ struct JpegGroup {
 struct PngGroup {
     int depth = 0;
     bool pair = false; // png_pair_kernel (128-row bands) or png_unfilter_kernel (64)
+    bool trns = false; // (pair kernel) the images carry a tRNS colour key
     DevBuf passes, sched, scratch, boundary;
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
     size_t scratch_zero_bytes = 0;
@@ -522,18 +523,20 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
     plan->ctx = ctx;
     plan->kind = 2;
     // one launch per (depth, kernel): the paired-row kernel takes what it supports
-    std::map<std::pair<int, bool>, std::vector<int>> by_depth;
+    std::map<std::tuple<int, bool, bool>, std::vector<int>> by_depth; // (depth, pair kernel, colour key)
     for (int i = 0; i < n_frames; i++) {
         if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
-        const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, frames[i].use_transparent != 0,
-                                       frames[i].width, frames[i].out_stride);
-        by_depth[{frames[i].depth, pair}].push_back(i);
+        const bool trns = frames[i].use_transparent != 0;
+        const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, trns, frames[i].width,
+                                       frames[i].out_stride);
+        by_depth[{frames[i].depth, pair, pair && trns}].push_back(i);
     }
     uint64_t bytes = 0;
     for (auto &kv : by_depth) {
         std::unique_ptr<PngGroup> g(new PngGroup);
-        g->depth = kv.first.first;
-        g->pair = kv.first.second;
+        g->depth = std::get<0>(kv.first);
+        g->pair = std::get<1>(kv.first);
+        g->trns = std::get<2>(kv.first);
         std::vector<DevPngPass> passes;
         std::vector<uint32_t> rowbytes;
         for (int idx : kv.second) {
@@ -571,9 +574,12 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
     for (auto &g : plan->png) {
-        const int rc = (g->pair ? launch_png_pair : launch_png_unfilter)(g->depth, g->passes.as<DevPngPass>(),
-                                                                        g->sched.as<DevPngBand>(), g->nsched,
-                                           g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes, st, 0);
+        const int rc = g->pair ? launch_png_pair(g->depth, g->trns, g->passes.as<DevPngPass>(),
+                                                 g->sched.as<DevPngBand>(), g->nsched, g->scratch.as<uint32_t>(),
+                                                 g->boundary.as<uint64_t>(), g->band_bytes, st)
+                               : launch_png_unfilter(g->depth, g->passes.as<DevPngPass>(), g->sched.as<DevPngBand>(),
+                                                     g->nsched, g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(),
+                                                     g->band_bytes, st);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
     }
     return ZPX_OK;
@@ -1137,9 +1143,12 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
     HIPCHK(ctx, hipMemcpy(dsched.ptr, &only, sizeof(DevPngBand), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
-    if ((pair ? launch_png_pair : launch_png_unfilter)(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
-                                                      ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream,
-                                                      spin_limit))
+    const int rc = pair ? launch_png_pair(ZPX_PNG_TC8, false, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
+                                          ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream, spin_limit)
+                        : launch_png_unfilter(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
+                                              ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream,
+                                              spin_limit);
+    if (rc)
         return hip_fail(ctx, hipGetLastError(), "png stall kernel launch");
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
