@@ -1,0 +1,579 @@
+// gfx950 fused JPEG pixel kernel, one 8x8 block per lane: dequant + 8x8
+// integer IDCT + level shift/clamp (reconstructBlock, src/jpeg/decoder.zig:
+// 1553-1634; idct.zig:77-201) fused with nearest chroma upsample and
+// YCbCr->RGB (Image.rgbaPixels over a YCbCrImage: image.zig:103-130, YCbCrAt
+// :614-630, Color.toRGBA .ycbcr color.zig:90-113).  It takes the common
+// frames -- int8/int16 coefficients within the 24-bit bound ("narrow"),
+// 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4 / gray, RGBA rows 16-byte aligned with a
+// width divisible by 4 -- and the strip kernel (jpeg_kernels.hip) the rest.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <type_traits>
+#include <utility>
+
+#include "device_types.h"
+#include "jpeg_idct.h"
+#include "kernels.h"
+
+namespace zpx {
+namespace {
+
+// Wave-local LDS ordering: a wave's LDS operations complete in order, so a
+// compiler fence plus lgkmcnt(0) orders its lanes' writes before its reads.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ---------------------------------------------------------------------------
+// Fused RGBA kernel, one 8x8 block per lane (jpeg_block_kernel).
+//
+// A wave owns a task: MCU row `my`, the T = 64 / H0 MCUs from column mx0,
+// i.e. 64 luma block columns.  A task is NP passes of (up to) 64 blocks, one
+// block per lane.  A pass:
+//   1. dequantizes its lane's block from the wave's LDS coefficient image
+//      (written by the previous pass's LDS-DMA loads),
+//   2. issues the next pass's loads into that image: global_load_lds of
+//      1 KiB contiguous per instruction (16 int8 / 8 int16 blocks), the
+//      per-lane source addresses permuted so that step 1's ds_read_b128 of
+//      a block's 16-byte pieces is bank-conflict-free,
+//   3. runs the 2-D IDCT + level shift + clamp in 64 registers (no LDS
+//      transpose, no barrier),
+//   4. then either writes the block's chroma samples as bytes to the task's
+//      chroma tile in LDS (chroma pass), or -- luma pass -- for each of the
+//      block's 8 pixel rows reads the row's chroma samples back (nearest
+//      upsample: image.zig:614-630), converts YCbCr -> RGBA (color.zig:90-113)
+//      and stores the row's 8 pixels as two 16-byte stores.
+// Every load and store is unconditional (a block past the grid's edge reads
+// a clamped address and never reaches the output; stores outside the image
+// get an offset the buffer range check drops), so the vmcnt counts stay
+// static and the next pass's loads overlap the whole IDCT + colour work of
+// the current one.
+// ---------------------------------------------------------------------------
+#ifndef ZPX_JPEGB_WAVES_PER_EU
+#define ZPX_JPEGB_WAVES_PER_EU 3
+#endif
+#ifndef ZPX_JPEGB_INLANE
+#define ZPX_JPEGB_INLANE 0 // 1: aligned chroma blocks stay in registers (costs 32 VGPRs)
+#endif
+#ifndef ZPX_JPEGB_STORE_AUX
+#define ZPX_JPEGB_STORE_AUX 0 // cache policy of the RGBA stores (a row's two halves meet in L2)
+#endif
+
+// The wave's LDS image of one pass's coefficients: 64 blocks as 16-byte
+// pieces (P per block: 4 int8, 8 int16).  DMA instruction k (of P) covers
+// blocks B*k .. B*k+B-1 (B = 64 / P; 1 KiB of the grid when the blocks are
+// contiguous) and writes slots 64k .. 64k+63; block j's piece q sits in slot
+//   64 * (j / B) + B * ((q + rot) % P) + j % B,   rot = (P == 8 ? j / B : 0),
+// so that for every piece q the 16-lane groups of a ds_read_b128 (lanes j)
+// hit 16 distinct 16-byte bank slots.
+template <typename CoefT>
+struct CoefImage {
+    static constexpr int P = 4 * static_cast<int>(sizeof(CoefT)); // pieces per block
+    static constexpr int B = 64 / P;                                // blocks per DMA instruction
+    static __device__ __forceinline__ int slot(int j, int q)
+    {
+        const int k = j / B;
+        return 64 * k + B * ((q + (P == 8 ? k : 0)) % P) + j % B;
+    }
+};
+
+// One LDS-DMA load: 16 bytes from each lane's `src` to lds_base + 16 * lane.
+// Inline asm, because for the builtin hipcc waits vmcnt(0) -- every store in
+// flight -- before any later LDS read; the kernel counts these loads itself
+// (the asm is absent from hipcc's s_waitcnt bookkeeping, which can only make
+// hipcc's own waits longer, never shorter).  M0 is set and restored inside the
+// statement (hipcc reserves it).
+__device__ __forceinline__ void glds16(const void *src, const void *lds_base)
+{
+    const uint32_t dst = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+        (const __attribute__((address_space(3))) void *)lds_base));
+    uint32_t keep;
+#if ZPX_COEF_NT
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+#else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+#endif
+}
+
+// s[k] = coef[k] * q[k] (natural order), lane j's block from the LDS image
+template <typename CoefT>
+__device__ __forceinline__ void dequant_block(const uint8_t *img, int j, const int32_t *q, int32_t s[64])
+{
+    using I = CoefImage<CoefT>;
+    constexpr int PER = 16 / static_cast<int>(sizeof(CoefT)); // coefficients per piece
+#pragma unroll
+    for (int pc = 0; pc < I::P; pc++) {
+        const u32x4 w = *reinterpret_cast<const u32x4 *>(img + 16 * I::slot(j, pc));
+#pragma unroll
+        for (int i = 0; i < PER; i += 4) {
+            const i32x4 qv = *reinterpret_cast<const i32x4 *>(q + pc * PER + i);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int k = pc * PER + i + e; // coefficient index
+                const int kk = i + e;           // index inside the piece
+                if constexpr (sizeof(CoefT) == 1) {
+                    // |coef| < 2^7, q < 2^17: the 24-bit multiply is exact
+                    s[k] = __mul24(static_cast<int32_t>(w[kk >> 2] << (24 - 8 * (kk & 3))) >> 24, qv[e]);
+                } else {
+                    s[k] = __mul24(static_cast<int32_t>(w[kk >> 1] << (16 - 16 * (kk & 1))) >> 16, qv[e]);
+                }
+                // materialize the product here: otherwise hipcc sinks the
+                // multiplies into the IDCT and keeps all 64 table values live
+                asm volatile("" : "+v"(s[k]));
+            }
+        }
+    }
+}
+
+// 2-D IDCT of one block in registers: rows (idct.zig:79-145), then columns
+// with level shift and clamp (idct.zig:148-200, decoder.zig:1622-1628).
+template <bool NARROW>
+__device__ __forceinline__ void idct_block(int32_t s[64])
+{
+    // (scheduling barriers between the 1-D transforms: interleaving them
+    // buys ILP the other resident waves already provide, and costs the
+    // registers that push the kernel into scratch)
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        idct_row<NARROW>(s + 8 * r);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        __builtin_amdgcn_sched_barrier(0);
+        int32_t t[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
+        idct_col_clamp<NARROW>(t);
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[8 * i + c] = t[i];
+    }
+}
+
+// four samples (0..255) -> one dword of bytes
+__device__ __forceinline__ uint32_t pack4(const int32_t *v)
+{
+    return static_cast<uint32_t>(v[0]) | static_cast<uint32_t>(v[1]) << 8 | static_cast<uint32_t>(v[2]) << 16 |
+           static_cast<uint32_t>(v[3]) << 24;
+}
+
+// The chroma terms of color.zig:95-106 for one (Cb, Cr) sample.
+struct ChromaTerms {
+    int32_t r, g, b;
+};
+__device__ __forceinline__ ChromaTerms chroma_terms(uint32_t cb, uint32_t cr)
+{
+    const int32_t cb1 = static_cast<int32_t>(cb) - 128, cr1 = static_cast<int32_t>(cr) - 128;
+    return ChromaTerms{__mul24(91881, cr1), -(__mul24(22554, cb1) + __mul24(46802, cr1)), __mul24(116130, cb1)};
+}
+
+// One RGBA pixel (see P3b of jpeg_rgba_kernel for the clamp form).
+template <int COLOR>
+__device__ __forceinline__ uint32_t rgba_pixel(int32_t Yv, uint32_t cb, uint32_t cr, ChromaTerms t)
+{
+    if constexpr (COLOR == ZPX_JPEG_COLOR_GRAY) {
+        return static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
+    } else if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
+        return static_cast<uint32_t>(Yv) | cb << 8 | cr << 16 | 0xff000000u;
+    } else {
+        const int32_t r = __mul24(Yv, 0x10101) + t.r;
+        const int32_t g = __mul24(Yv, 0x10101) + t.g;
+        const int32_t b = __mul24(Yv, 0x10101) + t.b;
+        const uint32_t rc = static_cast<uint32_t>(min(max(r, 0), 0xffffff));
+        const uint32_t gc = static_cast<uint32_t>(min(max(g, 0), 0xffffff));
+        const uint32_t bc = static_cast<uint32_t>(min(max(b, 0), 0xffffff));
+        const uint32_t rg = __builtin_amdgcn_perm(gc, rc, 0x0d0c0602u);
+        return __builtin_amdgcn_perm(bc, rg, 0x03060100u);
+    }
+}
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 4 ? 2 : ZPX_JPEGB_WAVES_PER_EU)))
+void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int tasks_per_frame, int total_tasks)
+{
+    constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
+    constexpr int T = 64 / H0;                                  // MCUs per task
+    constexpr bool kInLane = ZPX_JPEGB_INLANE && !kGray && HC == H0 && VC == V0; // chroma block (x, y) <-> luma block (x, y)
+    constexpr int CBW = kGray ? 1 : T * HC;                     // chroma blocks across a task, per component
+    constexpr int CBH = kGray ? 1 : VC;
+    constexpr int NCB = kGray ? 0 : 2 * CBW * CBH;              // chroma blocks of a task
+    constexpr int CP = (kGray || kInLane) ? 0 : (NCB + 63) / 64; // chroma passes through the LDS tile
+    constexpr int NP = kGray ? V0 : (kInLane ? 3 * V0 : CP + V0);
+    constexpr int RX = kGray ? 1 : H0 / HC, RY = kGray ? 1 : V0 / VC; // upsample ratios
+    constexpr int CPX = CBW * 8;                                // chroma tile row (bytes)
+    constexpr int CTILE = (kGray || kInLane) ? 16 : CBH * 8 * CPX;
+    constexpr int PXH = V0 * 8;                                 // task height in pixels
+    constexpr int NS = 8 / RX;                                  // chroma samples per block row
+    static_assert(T * H0 == 64, "a task spans 64 luma block columns");
+    // pass p: kind 0 = luma row, 1 = chroma through LDS, 2 = Cb in lane, 3 = Cr in lane
+    constexpr auto kind = [](int p) {
+        return kGray ? 0 : kInLane ? (p % 3 == 2 ? 0 : 2 + p % 3) : (p < CP ? 1 : 0);
+    };
+    constexpr auto yrow = [](int p) { return kGray ? p : kInLane ? p / 3 : p - CP; };
+
+    __shared__ __attribute__((aligned(16))) int32_t qs[3][64]; // Y, Cb, Cr (natural order)
+    __shared__ __attribute__((aligned(16))) uint8_t cimg[64 * 64 * sizeof(CoefT)]; // one pass's coefficients
+    __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
+    const int lane = threadIdx.x;
+
+    // per-frame uniform values, read once per frame change (frame fields
+    // read inside the loop compile to vector loads whose vmcnt waits would
+    // also wait for the stores in flight)
+    struct TaskSrc {
+        const CoefT *g[3];
+        uint8_t *rgba;
+        int gwy, gwc, myy, width, height;
+        uint32_t stride;
+    };
+    // (every field through readfirstlane: hipcc reads the descriptor with
+    // vector loads, and a use of their results after the rare frame-change
+    // branch would cost a vmcnt(0) -- a wait for every store in flight -- in
+    // every task; this way the wait stays inside the branch)
+    auto task_src = [&](int f) __attribute__((always_inline)) {
+        const DevJpegFrame &fr = frames[f];
+        auto u32 = [](uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(x)); };
+        auto ptr = [&](const void *p) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+            return reinterpret_cast<const void *>(static_cast<uintptr_t>(u32(static_cast<uint32_t>(a >> 32))) << 32 |
+                                                  u32(static_cast<uint32_t>(a)));
+        };
+        TaskSrc s;
+        s.g[0] = static_cast<const CoefT *>(ptr(fr.coeffs[0]));
+        s.g[1] = kGray ? nullptr : static_cast<const CoefT *>(ptr(fr.coeffs[1]));
+        s.g[2] = kGray ? nullptr : static_cast<const CoefT *>(ptr(fr.coeffs[2]));
+        const int mxx = static_cast<int>(u32(static_cast<uint32_t>(fr.mxx)));
+        s.gwy = mxx * H0;
+        s.gwc = mxx * HC;
+        s.myy = static_cast<int>(u32(static_cast<uint32_t>(fr.myy)));
+        s.rgba = static_cast<uint8_t *>(const_cast<void *>(ptr(fr.rgba)));
+        s.width = static_cast<int>(u32(static_cast<uint32_t>(fr.width)));
+        s.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
+        s.stride = u32(static_cast<uint32_t>(fr.rgba_stride));
+        return s;
+    };
+    auto coords = [&](int t, int &f, int &my, int &mx0) __attribute__((always_inline)) {
+        f = t / tasks_per_frame;
+        const int r = t - f * tasks_per_frame;
+        my = r / tasks_x;
+        mx0 = (r - my * tasks_x) * T;
+    };
+    // lane's block of pass P: its component (-> quant table, 3 = zeros when
+    // the block does not exist) and the chroma block's place in the tile
+    struct PassBlock {
+        int comp, cx, cy;
+        bool ok;
+    };
+    auto pass_block = [&](auto P, int j) __attribute__((always_inline)) {
+        constexpr int p = decltype(P)::value;
+        PassBlock b{0, j, yrow(p), true};
+        if constexpr (kind(p) == 1) {
+            const int idx = p * 64 + j;
+            constexpr int PER = CBW * CBH;
+            b.ok = idx < NCB;
+            b.comp = idx < PER ? 1 : 2;
+            const int k = idx < PER ? idx : idx - PER;
+            b.cx = k % CBW;
+            b.cy = k / CBW;
+        } else if constexpr (kind(p) >= 2) {
+            b.comp = kind(p) - 1;
+        }
+        return b;
+    };
+    auto load_q = [&](int f) __attribute__((always_inline)) {
+        const DevJpegFrame &fr = frames[f];
+#pragma unroll
+        for (int i = lane; i < 3 * 64; i += 64) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
+        wave_lds_sync();
+    };
+
+    int task = blockIdx.x;
+    if (task >= total_tasks) return;
+    const int tstride = static_cast<int>(gridDim.x);
+    int f, my, mx0;
+    coords(task, f, my, mx0);
+    load_q(f);
+    TaskSrc ts = task_src(f);
+    // one pass's 64 blocks -> cimg (LDS-DMA, see CoefImage).  DMA
+    // instruction k carries blocks B*k .. B*k+B-1, which lie in one grid row
+    // of one component (B divides a task's chroma blocks per component and
+    // the 64 luma columns), so its row address is uniform; a block past the
+    // grid's right edge is clamped onto the last one (its pixels never reach
+    // the output), a missing grid or row reads the descriptor array.
+    auto issue_pass = [&](const TaskSrc &t, int my_, int mx0_, auto P) __attribute__((always_inline)) {
+        using I = CoefImage<CoefT>;
+        constexpr int BYTES = 64 * static_cast<int>(sizeof(CoefT));
+#pragma unroll
+        for (int k = 0; k < I::P; k++) {
+            const PassBlock b0 = pass_block(P, I::B * k);
+            const int hh = b0.comp == 0 ? H0 : HC, vv = b0.comp == 0 ? V0 : VC;
+            const int gw = b0.comp == 0 ? t.gwy : t.gwc;
+            const CoefT *g = b0.comp == 0 ? t.g[0] : (b0.comp == 1 ? t.g[1] : t.g[2]);
+            const bool row_ok = b0.ok && g != nullptr && my_ < t.myy;
+            const uint8_t *row = row_ok ? reinterpret_cast<const uint8_t *>(g) +
+                                              static_cast<size_t>(my_ * vv + b0.cy) * gw * BYTES
+                                        : reinterpret_cast<const uint8_t *>(frames);
+            const int last = row_ok ? gw - 1 : 0;
+            const int bx = min(mx0_ * hh + b0.cx + lane % I::B, last);
+            const int q = (lane / I::B + I::P - (I::P == 8 ? k : 0)) % I::P;
+            glds16(row + static_cast<uint32_t>(bx * BYTES + 16 * q), cimg + 1024 * k);
+        }
+    };
+    issue_pass(ts, my, mx0, std::integral_constant<int, 0>{});
+    {
+        // 16 dropped stores (empty range, distinct offsets): at the loop head
+        // the first loads are followed by as many stores as on the back edge
+        // (the last pass's), so hipcc's vmcnt there waits for the loads only
+        const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, ZPX_JPEGB_STORE_AUX);
+    }
+    uint32_t cbr[kInLane ? 16 : 1], crr[kInLane ? 16 : 1]; // in-lane chroma samples (bytes)
+    (void)cbr;
+    (void)crr;
+    constexpr uint32_t kDrop = 0x80000000u;
+
+    for (;;) {
+        const int tn = task + tstride;
+        const bool more = tn < total_tasks;
+        int fn = f, myn = my, mxn = mx0;
+        if (more) coords(tn, fn, myn, mxn);
+        const TaskSrc tsn = fn == f ? ts : task_src(fn);
+        // output rows of this task through a buffer descriptor (the host
+        // guarantees 32 * rgba_stride < 2^31); a ragged batch's task past a
+        // smaller frame's last MCU row gets an empty range
+        const int W = ts.width, Y0 = my * PXH;
+        const int rows_here = max(0, min(PXH, ts.height - Y0));
+        const uint32_t ostride = ts.stride;
+        uint8_t *const obase = ts.rgba + static_cast<size_t>(Y0) * ostride;
+        // (readfirstlane: the values are uniform; without it hipcc keeps the
+        // descriptor in VGPRs and wraps every store in a waterfall loop)
+        const uintptr_t oa = reinterpret_cast<uintptr_t>(obase);
+        const uint64_t oa_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(oa)));
+        const uint64_t oa_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(oa >> 32)));
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void *>(static_cast<uintptr_t>(oa_hi << 32 | oa_lo)), 0,
+            __builtin_amdgcn_readfirstlane(rows_here * static_cast<int>(ostride)), 0x00020000);
+        const int xpix = (mx0 * H0 + lane) * 8; // first pixel column of the lane's luma block
+        const bool y_present = ts.g[0] != nullptr;
+
+        static_for<NP>([&](auto P) __attribute__((always_inline)) {
+            constexpr int p = decltype(P)::value;
+            int32_t s[64];
+            // this pass's image has landed: the DMA was followed by the
+            // previous pass's stores only (16 after a luma pass)
+            if constexpr (kind(p == 0 ? NP - 1 : p - 1) == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            dequant_block<CoefT>(cimg, lane, &qs[pass_block(P, lane).comp][0], s);
+            // every lane's reads of the image are done before the DMA refills it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // the next pass's coefficients load while this pass computes
+            if constexpr (p + 1 < NP)
+                issue_pass(ts, my, mx0, std::integral_constant<int, p + 1>{});
+            else
+                issue_pass(tsn, myn, mxn, std::integral_constant<int, 0>{});
+            idct_block<NARROW>(s);
+
+            if constexpr (kind(p) == 1) {
+                // chroma block -> tile (never-scanned component: samples 0)
+                const PassBlock b = pass_block(P, lane);
+                const bool present = (b.comp == 1 ? ts.g[1] : ts.g[2]) != nullptr;
+                const uint32_t pm = present ? 0xffffffffu : 0u;
+                uint8_t *t = &ctile[b.comp - 1][(b.cy * 8) * CPX + b.cx * 8];
+                if (b.ok) {
+#pragma unroll
+                    for (int r = 0; r < 8; r++)
+                        *reinterpret_cast<u32x2 *>(t + r * CPX) = u32x2{pack4(s + 8 * r) & pm, pack4(s + 8 * r + 4) & pm};
+                }
+                if constexpr (p == CP - 1) wave_lds_sync(); // tile complete before the luma passes
+            } else if constexpr (kind(p) >= 2) {
+                // chroma block kept in this lane: 8 rows x 8 bytes
+                const uint32_t pm = ts.g[kind(p) - 1] != nullptr ? 0xffffffffu : 0u;
+                uint32_t *dst = kind(p) == 2 ? cbr : crr;
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    dst[2 * r] = pack4(s + 8 * r) & pm;
+                    dst[2 * r + 1] = pack4(s + 8 * r + 4) & pm;
+                }
+            } else {
+                // luma block -> 8 rows of 8 RGBA pixels
+                constexpr int yr = yrow(p);
+                if (!y_present) { // never-scanned luma: samples 0
+#pragma unroll
+                    for (int i = 0; i < 64; i++) s[i] = 0;
+                }
+                uint32_t cs[kGray ? 1 : (NS + 3) / 4][2]; // this chroma row's samples, Cb / Cr
+                ChromaTerms ct[kGray ? 1 : NS];
+#pragma unroll
+                for (int y = 0; y < 8; y++) {
+                    if constexpr (!kGray) {
+                        if (y % RY == 0) {
+                            if constexpr (kInLane) {
+                                cs[0][0] = cbr[2 * y];
+                                cs[1][0] = cbr[2 * y + 1];
+                                cs[0][1] = crr[2 * y];
+                                cs[1][1] = crr[2 * y + 1];
+                            } else {
+                                const int crow = (yr * 8 + y) / RY;
+                                const uint8_t *c0 = &ctile[0][crow * CPX + lane * NS];
+                                const uint8_t *c1 = &ctile[1][crow * CPX + lane * NS];
+                                if constexpr (NS == 8) {
+                                    const u32x2 a = *reinterpret_cast<const u32x2 *>(c0);
+                                    const u32x2 b = *reinterpret_cast<const u32x2 *>(c1);
+                                    cs[0][0] = a[0];
+                                    cs[1][0] = a[1];
+                                    cs[0][1] = b[0];
+                                    cs[1][1] = b[1];
+                                } else if constexpr (NS == 4) {
+                                    cs[0][0] = *reinterpret_cast<const uint32_t *>(c0);
+                                    cs[0][1] = *reinterpret_cast<const uint32_t *>(c1);
+                                } else {
+                                    cs[0][0] = *reinterpret_cast<const uint16_t *>(c0);
+                                    cs[0][1] = *reinterpret_cast<const uint16_t *>(c1);
+                                }
+                            }
+                            if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) {
+#pragma unroll
+                                for (int u = 0; u < NS; u++)
+                                    ct[u] = chroma_terms((cs[u >> 2][0] >> (8 * (u & 3))) & 0xff,
+                                                         (cs[u >> 2][1] >> (8 * (u & 3))) & 0xff);
+                            }
+                        }
+                    }
+                    uint32_t px[8];
+#pragma unroll
+                    for (int x = 0; x < 8; x++) {
+                        const int u = x / RX;
+                        uint32_t cb = 0, cr = 0;
+                        ChromaTerms t{0, 0, 0};
+                        if constexpr (!kGray) {
+                            cb = (cs[u >> 2][0] >> (8 * (u & 3))) & 0xff;
+                            cr = (cs[u >> 2][1] >> (8 * (u & 3))) & 0xff;
+                            if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) t = ct[u];
+                        }
+                        px[x] = rgba_pixel<COLOR>(s[8 * y + x], cb, cr, t);
+                    }
+                    const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
+                    // (the host sends only frames with 16-byte aligned rows and
+                    // W % 4 == 0: a 4-pixel piece is wholly inside or outside)
+                    const uint32_t o0 = xpix < W ? rowoff + static_cast<uint32_t>(xpix) * 4 : kDrop;
+                    const uint32_t o1 = xpix + 4 < W ? rowoff + static_cast<uint32_t>(xpix) * 4 + 16 : kDrop;
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{px[0], px[1], px[2], px[3]}, orsrc, o0, 0,
+                                                           ZPX_JPEGB_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{px[4], px[5], px[6], px[7]}, orsrc, o1, 0,
+                                                           ZPX_JPEGB_STORE_AUX);
+                }
+            }
+        });
+        if (!more) break;
+        if (fn != f) {
+            wave_lds_sync(); // every dequant of this task has read qs
+            load_q(fn);
+        }
+        if constexpr (CP > 0) wave_lds_sync(); // the tile's reads precede the next task's writes
+        task = tn;
+        f = fn;
+        my = myn;
+        mx0 = mxn;
+        ts = tsn;
+    }
+}
+
+} // namespace
+
+namespace {
+int block_cu_count()
+{
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        n = cus;
+    }
+    return n;
+}
+
+// resident one-wave workgroups on the device for one kernel instance
+// (occupancy API: registers + LDS), capped by ZPX_JPEGB_WAVES_PER_CU (A/B runs)
+template <typename K>
+int resident_waves(K kernel)
+{
+    static int n = 0;
+    if (n == 0) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess || per_cu < 1)
+            per_cu = 8;
+        if (const char *e = getenv("ZPX_JPEGB_WAVES_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+        n = block_cu_count() * per_cu;
+    }
+    return n;
+}
+
+template <typename CoefT, int H0, int V0, int HC, int VC, int COLOR>
+int launch_block_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int max_myy, hipStream_t stream)
+{
+    constexpr int T = 64 / H0;
+    const int tasks_x = (max_mxx + T - 1) / T;
+    const int per_frame = tasks_x * max_myy;
+    const int total = per_frame * n_frames;
+    auto kernel = jpeg_block_kernel<CoefT, true, H0, V0, HC, VC, COLOR>;
+    const int resident = resident_waves(kernel);
+    const int grid = total < resident ? total : resident;
+    if (grid > 0) hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, tasks_x, per_frame, total);
+    return 0;
+}
+
+template <typename CoefT, int COLOR>
+int block_geom(int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStream_t s)
+{
+    switch (key) {
+    case 0x2211: return launch_block_t<CoefT, 2, 2, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:2:0
+    case 0x2111: return launch_block_t<CoefT, 2, 1, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:2:2
+    case 0x1211: return launch_block_t<CoefT, 1, 2, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:4:0
+    case 0x1111: return launch_block_t<CoefT, 1, 1, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:4:4
+    }
+    return -2;
+}
+
+template <typename CoefT>
+int block_color(int color, int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStream_t s)
+{
+    switch (color) {
+    case ZPX_JPEG_COLOR_YCBCR: return block_geom<CoefT, ZPX_JPEG_COLOR_YCBCR>(key, d, n, mxx, myy, s);
+    case ZPX_JPEG_COLOR_RGB: return block_geom<CoefT, ZPX_JPEG_COLOR_RGB>(key, d, n, mxx, myy, s);
+    case ZPX_JPEG_COLOR_GRAY: return launch_block_t<CoefT, 1, 1, 1, 1, ZPX_JPEG_COLOR_GRAY>(d, n, mxx, myy, s);
+    }
+    return -2;
+}
+} // namespace
+
+int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
+                      int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream)
+{
+    if (!narrow || (coeff_bits != 8 && coeff_bits != 16)) return -2;
+    const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
+    const int rc = coeff_bits == 8 ? block_color<int8_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
+                                   : block_color<int16_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
+    if (rc) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace zpx

@@ -16,6 +16,7 @@
 #include <cstdint>
 
 #include "device_types.h"
+#include "jpeg_idct.h"
 #include "kernels.h"
 
 namespace zpx {
@@ -25,119 +26,7 @@ constexpr int kThreads = 256;
 #ifndef ZPX_RGBA_STORE_AUX
 #define ZPX_RGBA_STORE_AUX 2 // cache policy bits of the fused kernel's output stores (2 = nt)
 #endif
-#ifndef ZPX_COEF_NT
-#define ZPX_COEF_NT 1 // 1: non-temporal coefficient loads (read once)
-#endif
 constexpr int kBlkStride = 72; // dwords per 8x8 block in LDS (64 + 8 pad: conflict-free column reads)
-
-// idct.zig:50-65
-constexpr int32_t W1 = 2841, W2 = 2676, W3 = 2408, W5 = 1609, W6 = 1108, W7 = 565;
-constexpr int32_t R2 = 181;
-
-// Left shift with two's-complement wrap (no UB for negative operands).
-__device__ __forceinline__ int32_t shl(int32_t x, int n) { return static_cast<int32_t>(static_cast<uint32_t>(x) << n); }
-
-// Multiply by an IDCT constant.  NARROW: the host proved every operand of the
-// stage-1/2 products fits in 24 signed bits (max |coef*q| <= 16384, see
-// DESIGN.md), so v_mul_i32_i24 gives the same low 32 bits as a 32-bit product.
-template <bool NARROW>
-__device__ __forceinline__ int32_t mulc(int32_t c, int32_t x)
-{
-    if constexpr (NARROW) return __mul24(c, x);
-    else return c * x;
-}
-
-// Horizontal 1-D IDCT of one row (idct.zig:79-145).  s[] holds dequantized
-// coefficients of the row in natural order.
-template <bool NARROW>
-__device__ __forceinline__ void idct_row(int32_t s[8])
-{
-    const int32_t dc = s[0];
-    const bool ac_zero = (s[1] | s[2] | s[3] | s[4] | s[5] | s[6] | s[7]) == 0;
-    int32_t x0 = shl(s[0], 11) + 128, x1 = shl(s[4], 11), x2 = s[6], x3 = s[2];
-    int32_t x4 = s[1], x5 = s[7], x6 = s[5], x7 = s[3], x8;
-    x8 = mulc<NARROW>(W7, x4 + x5);
-    x4 = x8 + mulc<NARROW>(W1 - W7, x4);
-    x5 = x8 - mulc<NARROW>(W1 + W7, x5);
-    x8 = mulc<NARROW>(W3, x6 + x7);
-    x6 = x8 - mulc<NARROW>(W3 - W5, x6);
-    x7 = x8 - mulc<NARROW>(W3 + W5, x7);
-    x8 = x0 + x1;
-    x0 -= x1;
-    x1 = mulc<NARROW>(W6, x3 + x2);
-    x2 = x1 - mulc<NARROW>(W2 + W6, x2);
-    x3 = x1 + mulc<NARROW>(W2 - W6, x3);
-    x1 = x4 + x6;
-    x4 -= x6;
-    x6 = x5 + x7;
-    x5 -= x7;
-    x7 = x8 + x3;
-    x8 -= x3;
-    x3 = x0 + x2;
-    x0 -= x2;
-    x2 = (R2 * (x4 + x5) + 128) >> 8;
-    x4 = (R2 * (x4 - x5) + 128) >> 8;
-    s[0] = (x7 + x1) >> 8;
-    s[1] = (x3 + x2) >> 8;
-    s[2] = (x0 + x4) >> 8;
-    s[3] = (x8 + x6) >> 8;
-    s[4] = (x8 - x6) >> 8;
-    s[5] = (x0 - x4) >> 8;
-    s[6] = (x3 - x2) >> 8;
-    s[7] = (x7 - x1) >> 8;
-    if constexpr (!NARROW) {
-        // DC-only shortcut (idct.zig:84-97).  Identical to the full path
-        // unless dc<<11 overflows, which only the wide variant can see.
-        if (ac_zero) {
-            const int32_t d = shl(dc, 3);
-#pragma unroll
-            for (int i = 0; i < 8; i++) s[i] = d;
-        }
-    } else {
-        (void)dc;
-        (void)ac_zero;
-    }
-}
-
-// Vertical 1-D IDCT of one column (idct.zig:148-200) + level shift and clamp
-// (decoder.zig:1622-1628): c<-128 -> 0, c>127 -> 255, else c+128.
-template <bool NARROW>
-__device__ __forceinline__ void idct_col_clamp(int32_t s[8])
-{
-    int32_t y0 = shl(s[0], 8) + 8192, y1 = shl(s[4], 8), y2 = s[6], y3 = s[2];
-    int32_t y4 = s[1], y5 = s[7], y6 = s[5], y7 = s[3], y8;
-    y8 = mulc<NARROW>(W7, y4 + y5) + 4;
-    y4 = (y8 + mulc<NARROW>(W1 - W7, y4)) >> 3;
-    y5 = (y8 - mulc<NARROW>(W1 + W7, y5)) >> 3;
-    y8 = mulc<NARROW>(W3, y6 + y7) + 4;
-    y6 = (y8 - mulc<NARROW>(W3 - W5, y6)) >> 3;
-    y7 = (y8 - mulc<NARROW>(W3 + W5, y7)) >> 3;
-    y8 = y0 + y1;
-    y0 -= y1;
-    y1 = mulc<NARROW>(W6, y3 + y2) + 4;
-    y2 = (y1 - mulc<NARROW>(W2 + W6, y2)) >> 3;
-    y3 = (y1 + mulc<NARROW>(W2 - W6, y3)) >> 3;
-    y1 = y4 + y6;
-    y4 -= y6;
-    y6 = y5 + y7;
-    y5 -= y7;
-    y7 = y8 + y3;
-    y8 -= y3;
-    y3 = y0 + y2;
-    y0 -= y2;
-    y2 = (R2 * (y4 + y5) + 128) >> 8;
-    y4 = (R2 * (y4 - y5) + 128) >> 8;
-    s[0] = (y7 + y1) >> 14;
-    s[1] = (y3 + y2) >> 14;
-    s[2] = (y0 + y4) >> 14;
-    s[3] = (y8 + y6) >> 14;
-    s[4] = (y8 - y6) >> 14;
-    s[5] = (y0 - y4) >> 14;
-    s[6] = (y3 - y2) >> 14;
-    s[7] = (y7 - y1) >> 14;
-#pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = min(max(s[i], -128), 127) + 128;
-}
 
 // Load one 8-coefficient row of a block (natural order) and dequantize it.
 template <typename CoefT>
@@ -243,9 +132,6 @@ __global__ __launch_bounds__(kThreads) void jpeg_planar_kernel(const DevJpegFram
 //        reuses the row buffer;
 //   P3c: 16-byte stores, a wave writes 1 KiB of one output row per instruction.
 // ---------------------------------------------------------------------------
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-#define ZPX_GLOBAL __attribute__((address_space(1)))
 
 #ifndef ZPX_JPEG_GROUP
 #define ZPX_JPEG_GROUP 256 // threads that cooperate on one strip: 256 (workgroup) or 64 (one wave)
@@ -276,7 +162,6 @@ __device__ __forceinline__ void group_sync()
     }
 }
 
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // One coefficient row, raw (not yet dequantized): 8 B (int8), 16 B (int16)
 // or 32 B (int32).
@@ -505,8 +390,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
             group_sync<G>();
         }
 
-        // ---- P3a: luma columns
+        // ---- P3a: luma columns (a never-scanned luma plane stays 0)
         int32_t yv[YCOL_IT][8];
+        const int32_t y_mask = fr.coeffs[0] != nullptr ? -1 : 0;
 #pragma unroll
         for (int it = 0; it < YCOL_IT; it++) {
             const int task = it * G + tid;
@@ -515,6 +401,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
 #pragma unroll
                 for (int i = 0; i < 8; i++) yv[it][i] = buf[blk * kBlkStride + i * 8 + c];
                 idct_col_clamp<NARROW>(yv[it]);
+#pragma unroll
+                for (int i = 0; i < 8; i++) yv[it][i] &= y_mask;
             }
         }
         group_sync<G>(); // row buffer is free: reuse it as the RGBA tile
@@ -591,7 +479,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
         const int X0 = mx0 * H0 * 8, Y0 = my * V0 * 8;
         const uint32_t ostride = static_cast<uint32_t>(fr.rgba_stride);
         uint8_t *const out = fr.rgba + static_cast<size_t>(Y0) * fr.rgba_stride;
-        const int rows_here = min(PXH, H - Y0);
+        const int rows_here = max(0, min(PXH, H - Y0)); // ragged batch: a smaller frame ends above
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, rows_here * static_cast<int>(ostride), 0x00020000);
         constexpr uint32_t kDrop = 0x80000000u;
         // 16-byte stores when every chunk of a row is whole and aligned
@@ -739,8 +627,19 @@ bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc)
 }
 
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc,
-                     int vc, int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream)
+                     int vc, int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, hipStream_t stream)
 {
+    // the block-per-lane kernel (jpeg_block_kernels.hip) takes the common
+    // frames; ZPX_JPEG_KERNEL=strip forces the strip kernel (A/B runs)
+    static const bool strip_only = [] {
+        const char *e = getenv("ZPX_JPEG_KERNEL");
+        return e && e[0] == 's';
+    }();
+    if (vec_out && !strip_only) {
+        const int rc = launch_jpeg_block(d_frames, n_frames, color, h0, v0, hc, vc, max_mxx, max_myy, coeff_bits,
+                                         narrow, stream);
+        if (rc != -2) return rc;
+    }
     const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
     int rc;
     if (coeff_bits == 8)

@@ -15,8 +15,14 @@ namespace zpx {
 int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh, int coeff_bits,
                        bool narrow, hipStream_t stream);
 bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc);
+// vec_out: every frame's RGBA rows are 16-byte aligned and its width is a
+// multiple of 4 (the block-per-lane kernel's store layout)
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
-                     int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream);
+                     int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, hipStream_t stream);
+
+// jpeg_block_kernels.hip: -2 when the frame kind is not one it takes
+int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
+                      int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream);
 
 // png_kernels.hip
 int png_chunk_bytes(int depth);

@@ -30,13 +30,18 @@
 //   out = (f + t) & 0x00ff00ff
 // about 23 instructions per byte PAIR, against ~21 per byte one row per lane.
 //
-// Memory: every lane burst-loads its two rows' next group of 4 chunks one
-// group ahead; reconstructed chunks go to a per-row LDS ring of 12 slots
-// (raw filtered-order bytes), and every 4 steps the rows that completed an
-// aligned 8-chunk block (one 128-byte line of output) are listed, and 8 lanes
-// per listed row store its block as whole lines (cooperative flush).  The
-// hot loop is one 4-step group, so the loop body stays a few KB of code (the
-// one-row-per-lane kernel's 94 KB loop missed the instruction cache).
+// Memory: every lane burst-loads its two rows' next group of kG = 8 chunks one
+// group ahead through buffer descriptors (every load and store of the group
+// loop is unconditional -- out-of-range offsets read zero / drop the store --
+// so s_waitcnt counts stay exact); each reconstructed chunk is expanded to
+// its 16 output bytes (colour key, 16-bit order) into a per-row LDS ring of
+// kSlots = 16 slots; every group, a fixed 16 rounds of cooperative flush
+// store each row's newly completed aligned 8-chunk block (one 128-byte line
+// of RGBA8) with 8 lanes per row, from a transposed per-row flush state.
+// The boundary window of the band above is prefetched one group ahead and
+// polled out of line.  The hot loop is one group, so the loop body stays a
+// few KB of code (the one-row-per-lane kernel's 94 KB loop missed the
+// instruction cache).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

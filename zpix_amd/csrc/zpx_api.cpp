@@ -231,7 +231,13 @@ int zpx::launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_f
     const int color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
     const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
     const int hc = f.n_comp == 3 ? f.h[1] : 1, vc = f.n_comp == 3 ? f.v[1] : 1;
-    return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits, f.narrow != 0, st);
+    return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits, f.narrow != 0,
+                            jpeg_rgba_vec_out(f), st);
+}
+
+bool zpx::jpeg_rgba_vec_out(const zpx_jpeg_frame &f)
+{
+    return (f.rgba_stride & 15) == 0 && (reinterpret_cast<uintptr_t>(f.rgba) & 15) == 0 && (f.width & 3) == 0;
 }
 // jpeg.decode's planes (reconstructBlock into makeImg's layout) followed by
 // the colour pass of Image.rgbaPixels, for the frames the fused kernel does
@@ -322,6 +328,7 @@ struct JpegGroup {
     bool narrow = true;
     int color = 0, h0 = 1, v0 = 1, hc = 1, vc = 1;
     int max_gw = 0, max_gh = 0, max_mxx = 0, max_myy = 0;
+    bool vec_out = true; // every frame: 16-byte aligned RGBA rows, width % 4 == 0
 };
 struct PngGroup {
     int depth = 0;
@@ -401,6 +408,7 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
             }
             bytes += uint64_t(f.n_comp) * 64 * 4; // quant tables
             if (output == ZPX_JPEG_RGBA) bytes += uint64_t(f.width) * f.height * 4;
+            g->vec_out = g->vec_out && jpeg_rgba_vec_out(f);
             g->max_mxx = std::max(g->max_mxx, f.mxx);
             g->max_myy = std::max(g->max_myy, f.myy);
         }
@@ -569,7 +577,7 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
             rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->max_gw, g->max_gh, g->bits, g->narrow, st);
         else
             rc = launch_jpeg_rgba(g->frames.as<DevJpegFrame>(), g->n, g->color, g->h0, g->v0, g->hc, g->vc,
-                                  g->max_mxx, g->max_myy, g->bits, g->narrow, st);
+                                  g->max_mxx, g->max_myy, g->bits, g->narrow, g->vec_out, st);
         if (rc == -2) return ZPX_E_UNSUPPORTED;
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
