@@ -423,10 +423,12 @@ def main():
         launch_bytes = batch.bytes
         achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
+        # the kernel the plan ran (jpeg_kernels.hip: ZPX_JPEG_KERNEL=strip forces the strip kernel)
+        jkernel = "jpeg_rgba_kernel" if os.environ.get("ZPX_JPEG_KERNEL", "").startswith("s") else "jpeg_block_kernel"
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("images") == args.images and tj.get("size") == args.size and tj.get("kernel", "").startswith("jpeg_rgba"):
+                if tj.get("images") == args.images and tj.get("size") == args.size and tj.get("kernel") == jkernel:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -476,7 +478,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "frac_of_measured_copy": round(achieved / MEASURED_COPY_GBS, 4),
-                         "kernel": "jpeg_rgba_kernel", "kernel_ms_per_launch": round(kern_ms, 4),
+                         "kernel": jkernel, "kernel_ms_per_launch": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": launch_bytes},
             "host_entropy_mpix_s": round(host_entropy, 1),
         }

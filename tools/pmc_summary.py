@@ -13,7 +13,8 @@ for p in sorted(os.listdir(base)):
         continue
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = ("jpeg_rgba" if "jpeg_rgba" in name else "png_unfilter" if "png_unfilter" in name
+        short = ("jpeg_rgba" if "jpeg_rgba" in name else "jpeg_block" if "jpeg_block_kernel" in name
+                 else "png_unfilter" if "png_unfilter" in name
                  else "png_pair" if "png_pair_kernel" in name else None)
         if not short:
             continue
@@ -29,9 +30,10 @@ print(json.dumps(out, indent=1))
 # roofline.traffic for bench.py: HBM bytes per launch of the fused JPEG kernel,
 # FETCH_SIZE/WRITE_SIZE in KiB; FETCH_SIZE doubled (gfx950 tallies a 128-B
 # streaming read request as 64 B, MI355X_MICROARCH.md "HBM").
-if len(sys.argv) > 2 and "jpeg_rgba" in out:
-    j = out["jpeg_rgba"]
-    tr = {"kernel": "jpeg_rgba_kernel", "images": int(sys.argv[3]) if len(sys.argv) > 3 else 64,
+jk = "jpeg_block" if "jpeg_block" in out else "jpeg_rgba"
+if len(sys.argv) > 2 and jk in out:
+    j = out[jk]
+    tr = {"kernel": jk + "_kernel", "images": int(sys.argv[3]) if len(sys.argv) > 3 else 64,
           "size": int(sys.argv[4]) if len(sys.argv) > 4 else 4096,
           "fetch_bytes_per_launch": 2 * j["FETCH_SIZE"] * 1024, "write_bytes_per_launch": j["WRITE_SIZE"] * 1024,
           "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, KiB -> B, mean per dispatch"}

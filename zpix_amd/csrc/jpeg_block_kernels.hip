@@ -54,10 +54,16 @@ __device__ __forceinline__ void wave_lds_sync()
 // the current one.
 // ---------------------------------------------------------------------------
 #ifndef ZPX_JPEGB_WAVES_PER_EU
-#define ZPX_JPEGB_WAVES_PER_EU 3
+#define ZPX_JPEGB_WAVES_PER_EU 3 // int8 instances (168 VGPRs, no scratch)
+#endif
+#ifndef ZPX_JPEGB_WAVES_PER_EU16
+#define ZPX_JPEGB_WAVES_PER_EU16 2 // int16 instances (at 3 they spill)
 #endif
 #ifndef ZPX_JPEGB_INLANE
 #define ZPX_JPEGB_INLANE 0 // 1: aligned chroma blocks stay in registers (costs 32 VGPRs)
+#endif
+#ifndef ZPX_JPEGB_DEPTH2
+#define ZPX_JPEGB_DEPTH2 0 // 1: int8 coefficient DMA two passes ahead (measured slower)
 #endif
 #ifndef ZPX_JPEGB_STORE_AUX
 #define ZPX_JPEGB_STORE_AUX 0 // cache policy of the RGBA stores (a row's two halves meet in L2)
@@ -205,7 +211,7 @@ __device__ __forceinline__ void static_for(F &&f)
 }
 
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 4 ? 2 : ZPX_JPEGB_WAVES_PER_EU)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 2 ? ZPX_JPEGB_WAVES_PER_EU16 : ZPX_JPEGB_WAVES_PER_EU)))
 void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int tasks_per_frame, int total_tasks)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
@@ -229,7 +235,12 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     constexpr auto yrow = [](int p) { return kGray ? p : kInLane ? p / 3 : p - CP; };
 
     __shared__ __attribute__((aligned(16))) int32_t qs[3][64]; // Y, Cb, Cr (natural order)
-    __shared__ __attribute__((aligned(16))) uint8_t cimg[64 * 64 * sizeof(CoefT)]; // one pass's coefficients
+    // coefficient images: DEPTH passes in flight (int8: the DMA runs two
+    // passes ahead, int16 one -- LDS per wave stays within the occupancy
+    // the registers allow)
+    constexpr int IMG = 64 * 64 * static_cast<int>(sizeof(CoefT));
+    constexpr int DEPTH = (ZPX_JPEGB_DEPTH2 && sizeof(CoefT) == 1 && NP >= 2) ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) uint8_t cimg[DEPTH * IMG];
     __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
     const int lane = threadIdx.x;
 
@@ -316,7 +327,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     // the 64 luma columns), so its row address is uniform; a block past the
     // grid's right edge is clamped onto the last one (its pixels never reach
     // the output), a missing grid or row reads the descriptor array.
-    auto issue_pass = [&](const TaskSrc &t, int my_, int mx0_, auto P) __attribute__((always_inline)) {
+    auto issue_pass = [&](const TaskSrc &t, int my_, int mx0_, auto P, uint8_t *img) __attribute__((always_inline)) {
         using I = CoefImage<CoefT>;
         constexpr int BYTES = 64 * static_cast<int>(sizeof(CoefT));
 #pragma unroll
@@ -332,19 +343,35 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             const int last = row_ok ? gw - 1 : 0;
             const int bx = min(mx0_ * hh + b0.cx + lane % I::B, last);
             const int q = (lane / I::B + I::P - (I::P == 8 ? k : 0)) % I::P;
-            glds16(row + static_cast<uint32_t>(bx * BYTES + 16 * q), cimg + 1024 * k);
+            glds16(row + static_cast<uint32_t>(bx * BYTES + 16 * q), img + 1024 * k);
         }
     };
-    issue_pass(ts, my, mx0, std::integral_constant<int, 0>{});
-    {
-        // 16 dropped stores (empty range, distinct offsets): at the loop head
-        // the first loads are followed by as many stores as on the back edge
-        // (the last pass's), so hipcc's vmcnt there waits for the loads only
-        const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
+    // vmcnt bookkeeping (the DMA is inline asm, so the kernel counts it):
+    // S(p) stores per pass, L DMA instructions per pass; the image of pass p
+    // was issued DEPTH passes earlier, and at pass p's start the operations
+    // issued after it are the intervening passes' stores and DMAs.
+    constexpr int L = CoefImage<CoefT>::P;
+    constexpr auto S = [=](int p) { return kind(((p % NP) + NP) % NP) == 0 ? 16 : 0; };
+    constexpr auto vm_wait = [=](int p) { return DEPTH == 2 ? S(p - 2) + L + S(p - 1) : S(p - 1); };
+    // the loop head expects the steady state: the first DEPTH images in
+    // flight, each followed by the previous task's stores it would have seen
+    // (dropped stores: empty range, distinct offsets)
+    const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
+    auto pad_stores = [&](int n) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 16; i++)
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, ZPX_JPEGB_STORE_AUX);
+            if (i < n) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, ZPX_JPEGB_STORE_AUX);
+    };
+    if constexpr (DEPTH == 2) {
+        issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
+        pad_stores(S(NP - 2));
+        issue_pass(ts, my, mx0, std::integral_constant<int, 1>{}, cimg + IMG);
+        pad_stores(S(NP - 1));
+    } else {
+        issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
+        pad_stores(S(NP - 1));
     }
+    int cur = 0; // image of the current pass
     uint32_t cbr[kInLane ? 16 : 1], crr[kInLane ? 16 : 1]; // in-lane chroma samples (bytes)
     (void)cbr;
     (void)crr;
@@ -379,17 +406,24 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             int32_t s[64];
             // this pass's image has landed: the DMA was followed by the
             // previous pass's stores only (16 after a luma pass)
-            if constexpr (kind(p == 0 ? NP - 1 : p - 1) == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            dequant_block<CoefT>(cimg, lane, &qs[pass_block(P, lane).comp][0], s);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(vm_wait(p)) : "memory");
+            uint8_t *const img = cimg + (DEPTH == 2 ? cur * IMG : 0);
+            dequant_block<CoefT>(img, lane, &qs[pass_block(P, lane).comp][0], s);
             // every lane's reads of the image are done before the DMA refills it
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // the next pass's coefficients load while this pass computes
-            if constexpr (p + 1 < NP)
-                issue_pass(ts, my, mx0, std::integral_constant<int, p + 1>{});
+            // pass p + DEPTH's coefficients load while this pass (and the next) computes
+            constexpr int pn = p + DEPTH;
+            if constexpr (pn < NP)
+                issue_pass(ts, my, mx0, std::integral_constant<int, pn>{}, img);
             else
-                issue_pass(tsn, myn, mxn, std::integral_constant<int, 0>{});
+                issue_pass(tsn, myn, mxn, std::integral_constant<int, pn - NP>{}, img);
+            if constexpr (DEPTH == 2) cur ^= 1;
+#ifndef ZPX_JPEGB_TIMING_NO_IDCT // timing-only builds (wrong pixels): cost breakdown
             idct_block<NARROW>(s);
+#else
+#pragma unroll
+            for (int i = 0; i < 64; i++) s[i] &= 0xff;
+#endif
 
             if constexpr (kind(p) == 1) {
                 // chroma block -> tile (never-scanned component: samples 0)
@@ -468,7 +502,11 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                             cr = (cs[u >> 2][1] >> (8 * (u & 3))) & 0xff;
                             if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) t = ct[u];
                         }
+#ifndef ZPX_JPEGB_TIMING_NO_COLOR
                         px[x] = rgba_pixel<COLOR>(s[8 * y + x], cb, cr, t);
+#else
+                        px[x] = static_cast<uint32_t>(s[8 * y + x]) ^ cb ^ (cr << 8) ^ static_cast<uint32_t>(t.r);
+#endif
                     }
                     const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
                     // (the host sends only frames with 16-byte aligned rows and
@@ -516,15 +554,14 @@ int block_cu_count()
 template <typename K>
 int resident_waves(K kernel)
 {
-    static int n = 0;
-    if (n == 0) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess || per_cu < 1)
-            per_cu = 8;
-        if (const char *e = getenv("ZPX_JPEGB_WAVES_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
-        n = block_cu_count() * per_cu;
-    }
-    return n;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64, 0) != hipSuccess || per_cu < 1) per_cu = 8;
+    // a multiple of the CU's 4 SIMDs: every wave gets the same number of
+    // tasks, so a SIMD holding one wave more than the others would set the
+    // launch's end (9 waves per CU ran 4:4:4 int16 22 % slower than 8)
+    if (per_cu > 4) per_cu &= ~3;
+    if (const char *e = getenv("ZPX_JPEGB_WAVES_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+    return block_cu_count() * per_cu;
 }
 
 template <typename CoefT, int H0, int V0, int HC, int VC, int COLOR>
@@ -535,7 +572,7 @@ int launch_block_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int 
     const int per_frame = tasks_x * max_myy;
     const int total = per_frame * n_frames;
     auto kernel = jpeg_block_kernel<CoefT, true, H0, V0, HC, VC, COLOR>;
-    const int resident = resident_waves(kernel);
+    static const int resident = resident_waves(kernel); // (one per instance: this function is)
     const int grid = total < resident ? total : resident;
     if (grid > 0) hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, tasks_x, per_frame, total);
     return 0;

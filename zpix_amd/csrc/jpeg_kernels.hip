@@ -553,15 +553,11 @@ int cu_count()
 template <typename K>
 int persistent_workgroups(K kernel)
 {
-    static int n = 0;
-    if (n == 0) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu < 1)
-            per_cu = 4;
-        if (const char *e = getenv("ZPX_JPEG_WG_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
-        n = cu_count() * per_cu;
-    }
-    return n;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu < 1)
+        per_cu = 4;
+    if (const char *e = getenv("ZPX_JPEG_WG_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+    return cu_count() * per_cu;
 }
 
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
@@ -575,7 +571,7 @@ void launch_rgba_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int 
     const int total = per_frame * n_frames;
     const int groups_needed = (total + NG - 1) / NG;
     auto kernel = jpeg_rgba_kernel<CoefT, NARROW, H0, V0, HC, VC, COLOR>;
-    const int resident = persistent_workgroups(kernel);
+    static const int resident = persistent_workgroups(kernel); // (one per instance: this function is)
     const int grid = groups_needed < resident ? groups_needed : resident;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), 0, stream, d_frames, strips_x, per_frame, total);
 }
