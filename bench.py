@@ -335,6 +335,9 @@ def bench_e2e(args, torch, dist, ws, rank, ctx, S, threads):
            "per_gpu_mpix_s": round(total * W * H / wall / 1e6 / ws, 1),
            "images": total, "images_per_gpu": len(plan.owned[rank]), "host_threads_per_rank": st.host_threads,
            "depth": st.depth, "decode_wall_s": round(wall, 3), "host_cpu_s_rank0": round(st.host_s, 3),
+           "host_cpu_s_by_stage_rank0": {
+               "jpeg_entropy": round(st.host_jpeg_s, 3), "jpeg_items": st.jpeg_items,
+               "png_inflate": round(st.host_png_s, 3), "png_items": st.png_items},
            "h2d_gb_rank0": round(st.h2d_bytes / 1e9, 3),
            "config": {"workload": f"{total}x {W}x{H} JPEG 4:2:0 / tc8 PNG (half each per shard), encoded bytes in "
                                   f"host memory -> RGBA8 in HBM (zpx_batch_decode_rgba), image i -> GPU i mod {ws}"

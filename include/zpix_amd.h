@@ -415,6 +415,9 @@ typedef struct zpx_batch_stats {
     int32_t host_threads, depth;
     int32_t failed;          /* items with status != ZPX_OK */
     int32_t pad;
+    double host_jpeg_s;      /* host_s split by stage: JPEG entropy decode (processSos) */
+    double host_png_s;       /*   and PNG chunk walk + inflate (parseIdat) */
+    int32_t jpeg_items, png_items;
 } zpx_batch_stats;
 
 /* Decodes the whole batch and returns when every item is complete.
@@ -466,6 +469,11 @@ int zpx_batch_decode_sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *ite
  * receives the slower launch's wall time, which must stay about one spin
  * limit, not one per step. */
 int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds);
+
+/* Number of scans the host entropy stage has decoded restart-interval-
+ * parallel in this process (tests: the parallel path ran, not its serial
+ * fallback).  Host-only. */
+int64_t zpx_debug_jpeg_parallel_scans(void);
 
 #ifdef __cplusplus
 }

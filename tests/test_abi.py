@@ -141,6 +141,76 @@ def test_host_entropy_error_cases():
         assert _jpeg_err_product(r[:2816] + infix + r[2816:]) == want
 
 
+def _dri_jpegs():
+    """Baseline JPEGs with restart intervals: the reference's restart2
+    fixture and Pillow encodes (restart every N MCUs / every row)."""
+    import io
+
+    from PIL import Image
+    from tools import synthetic as S
+
+    out = [("restart2", read("testdata", "video-001.restart2.jpeg"))]
+    for name, sub, w, h, kw in [("420_b7", 2, 264, 120, {"restart_marker_blocks": 7}),
+                                ("444_b1", 0, 96, 40, {"restart_marker_blocks": 1}),
+                                ("422_rows", 1, 200, 72, {"restart_marker_rows": 1}),
+                                ("gray_b5", None, 120, 56, {"restart_marker_blocks": 5})]:
+        b = io.BytesIO()
+        px = S.content(w * 3 + h, w, h)
+        if sub is None:
+            Image.fromarray(px[..., 0]).save(b, "JPEG", quality=85, **kw)
+        else:
+            Image.fromarray(px).save(b, "JPEG", quality=85, subsampling=sub, **kw)
+        out.append((name, b.getvalue()))
+    return out
+
+
+def test_host_entropy_restart_parallel_matches_oracle(monkeypatch):
+    """Restart-interval-parallel Huffman (jpeg_host.cpp restart_parallel,
+    splitting at decoder.zig:1432-1452): the same coefficients as the serial
+    oracle on every DRI file, the same error names on corrupted segments, and
+    the parallel path actually taken on the clean files."""
+    monkeypatch.setenv("ZPX_HUFF_PAR_MIN_MCUS", "1")  # small files still split
+    L = _lib.lib()
+    for name, data in _dri_jpegs():
+        before = L.zpx_debug_jpeg_parallel_scans()
+        oc = O.jpeg_coefficients(data)
+        pc = J.Coefficients(data)
+        assert L.zpx_debug_jpeg_parallel_scans() == before + 1, name
+        for c in range(oc.n_comp):
+            assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32)), (name, c)
+        m = max(int(np.abs(g).max()) for g in oc.grids if g is not None)
+        assert pc.frame.coeff_bits == (8 if m <= 127 else 16), name  # narrowest width, as serially
+    # corrupted segments: every outcome equals the oracle's (serial fallback)
+    r = read("testdata", "video-001.restart2.jpeg")
+    for infix in [b"", b"\x61\x62\x63\xff\x00\x64", b"\xff\xff\xff\x00\xff\x00\x00\xff\xff\xff",
+                  b"\xff\x03", b"\xff\xd5", b"\xff\xff\xd5"]:
+        data = r[:2816] + infix + r[2816:]
+        try:
+            oc = O.jpeg_coefficients(data)
+        except O.OracleError as e:
+            assert _jpeg_err_product(data) == e.name
+            continue
+        pc = J.Coefficients(data)
+        for c in range(oc.n_comp):
+            assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32))
+    rng = np.random.default_rng(3)
+    srcs = [d for _, d in _dri_jpegs()]
+    for it in range(40):
+        d = bytearray(srcs[it % len(srcs)])
+        for _ in range(rng.integers(1, 3)):
+            d[rng.integers(len(d) // 4, len(d))] = rng.integers(0, 256)
+        data = bytes(d)
+        try:
+            oc = O.jpeg_coefficients(data)
+        except O.OracleError as e:
+            assert _jpeg_err_product(data) == e.name
+            continue
+        pc = J.Coefficients(data)
+        for c in range(oc.n_comp):
+            if oc.grids[c] is not None:
+                assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32))
+
+
 def test_host_entropy_fuzz_matches_oracle():
     """Random byte corruption of fixtures: same coefficients or same error name."""
     rng = np.random.default_rng(7)

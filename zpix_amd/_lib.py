@@ -124,6 +124,10 @@ class zpx_batch_stats(C.Structure):
         ("depth", C.c_int32),
         ("failed", C.c_int32),
         ("pad", C.c_int32),
+        ("host_jpeg_s", C.c_double),
+        ("host_png_s", C.c_double),
+        ("jpeg_items", C.c_int32),
+        ("png_items", C.c_int32),
     ]
 
 
@@ -143,7 +147,7 @@ EXPORTS = [
     "zpx_jpeg_coeffs_frame", "zpx_jpeg_coeffs_free", "zpx_jpeg_coeffs_widen", "zpx_png_inflate", "zpx_png_stream_frame",
     "zpx_png_stream_data", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
     "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config", "zpx_plan_status",
-    "zpx_batch_decode_sharded", "zpx_debug_png_stall",
+    "zpx_batch_decode_sharded", "zpx_debug_png_stall", "zpx_debug_jpeg_parallel_scans",
 ]
 
 _lib = None
@@ -205,6 +209,7 @@ def lib():
                                            C.POINTER(zpx_batch_opts), C.POINTER(zpx_batch_stats),
                                            C.POINTER(zpx_gather_stats)]),
         "zpx_debug_png_stall": (i32, [vp, C.c_uint32, C.POINTER(C.c_double)]),
+        "zpx_debug_jpeg_parallel_scans": (C.c_int64, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -125,7 +125,8 @@ class Pipeline {
     int tokens_ = 0;
     bool stop_ = false;
     std::atomic<int> next_{0};
-    double host_s_ = 0;
+    double host_s_ = 0, host_jpeg_s_ = 0, host_png_s_ = 0;
+    int jpeg_items_ = 0, png_items_ = 0;
     double h2d_bytes_ = 0, d2h_bytes_ = 0, pixels_ = 0;
     int failed_ = 0;
 };
@@ -177,7 +178,8 @@ void Pipeline::worker()
             d->status = png_parse(it.buf, it.len, d->ps);
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
-            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc);
+            // spare pool threads (fewer images than threads) split restart intervals
+            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, std::max(1, threads_ / std::max(1, n_)));
         } else if (it.buf && it.len >= 4 && (memcmp(it.buf, "qoif", 4) == 0 || (it.buf[0] == 'B' && it.buf[1] == 'M'))) {
             d->status = ZPX_E_UNSUPPORTED; // QOI / BMP: out of scope (zpx_from_buffer)
         } else {
@@ -188,6 +190,13 @@ void Pipeline::worker()
         {
             std::lock_guard<std::mutex> lk(mu_);
             host_s_ += dt;
+            if (d->fmt == 1) {
+                host_jpeg_s_ += dt;
+                jpeg_items_++;
+            } else if (d->fmt == 2) {
+                host_png_s_ += dt;
+                png_items_++;
+            }
             ready_.push_back(std::move(d));
         }
         cv_ready_.notify_one();
@@ -580,6 +589,10 @@ int Pipeline::run(zpx_batch_stats *stats)
         memset(stats, 0, sizeof(*stats));
         stats->wall_s = now_s() - t0;
         stats->host_s = host_s_;
+        stats->host_jpeg_s = host_jpeg_s_;
+        stats->host_png_s = host_png_s_;
+        stats->jpeg_items = jpeg_items_;
+        stats->png_items = png_items_;
         stats->h2d_bytes = h2d_bytes_;
         stats->d2h_bytes = d2h_bytes_;
         stats->pixels = pixels_;

@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <map>
 #include <mutex>
 
@@ -213,6 +215,41 @@ bool CoeffGrid::store_sparse(size_t blk, const int32_t *b, const uint8_t *pos, i
     return true;
 }
 
+bool CoeffGrid::store_sparse_fixed(size_t blk, const int32_t *b, const uint8_t *pos, int n, int32_t &max_abs,
+                                   std::vector<std::pair<size_t, int32_t>> &overflow) const
+{
+    const int lim = bits_ == 8 ? 127 : bits_ == 16 ? 32767 : INT32_MAX;
+    const size_t base = blk * 64;
+    if (bits_ == 8) memset(static_cast<int8_t *>(buf_.ptr) + base, 0, 64);
+    else if (bits_ == 16) memset(static_cast<int16_t *>(buf_.ptr) + base, 0, 128);
+    else memset(static_cast<int32_t *>(buf_.ptr) + base, 0, 256);
+    for (int i = 0; i < n; i++) {
+        const int32_t v = b[pos[i]];
+        const int32_t a = v < 0 ? (v == INT32_MIN ? INT32_MAX : -v) : v;
+        max_abs = a > max_abs ? a : max_abs;
+        if (a > lim) {
+            overflow.emplace_back(base + pos[i], v);
+            continue;
+        }
+        if (bits_ == 8) static_cast<int8_t *>(buf_.ptr)[base + pos[i]] = static_cast<int8_t>(v);
+        else if (bits_ == 16) static_cast<int16_t *>(buf_.ptr)[base + pos[i]] = static_cast<int16_t>(v);
+        else static_cast<int32_t *>(buf_.ptr)[base + pos[i]] = v;
+    }
+    return true;
+}
+
+bool CoeffGrid::apply_overflow(int32_t max_abs, const std::vector<std::pair<size_t, int32_t>> &overflow)
+{
+    max_abs_ = max_abs > max_abs_ ? max_abs : max_abs_;
+    const int need = max_abs_ > 32767 ? 32 : max_abs_ > 127 ? 16 : 8;
+    if (!widen_to(need)) return false;
+    for (const auto &o : overflow) {
+        if (bits_ == 16) static_cast<int16_t *>(buf_.ptr)[o.first] = static_cast<int16_t>(o.second);
+        else static_cast<int32_t *>(buf_.ptr)[o.first] = o.second;
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- decoder
 namespace {
 
@@ -239,8 +276,8 @@ struct Huff { // HuffTable.zig
 
 class Decoder {
   public:
-    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out, bool config_only = false)
-        : src_(p), len_(n), o_(out), config_only_(config_only)
+    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out, bool config_only = false, int threads = 1)
+        : src_(p), len_(n), o_(out), config_only_(config_only), threads_(threads)
     {
     }
     int run();
@@ -418,6 +455,38 @@ class Decoder {
         return 0;
     }
 
+    // one scan's parameters (processSos :1148-1296)
+    struct Scan {
+        int ns = 0;
+        struct {
+            uint8_t id = 0, td = 0, ta = 0;
+        } c[4];
+        int32_t zs = 0, ze = 63, mxx = 0, myy = 0;
+        uint32_t ah = 0, al = 0;
+        bool prog = false;
+    };
+    // how one decoded block is stored: the serial path widens the grid as
+    // values need it; the parallel path writes a grid of fixed width
+    struct SerialSink {
+        JpegCoeffs &o;
+        int put(int ci, size_t blk, int32_t *b, const uint8_t *pos, int n)
+        {
+            return o.grid[ci].store_sparse(blk, b, pos, n) ? 0 : ZPX_E_OUT_OF_MEMORY;
+        }
+    };
+    struct FixedSink {
+        JpegCoeffs &o;
+        int32_t max_abs[4] = {0, 0, 0, 0};
+        std::vector<std::pair<size_t, int32_t>> overflow[4]; // values too wide for the grid
+        int put(int ci, size_t blk, int32_t *b, const uint8_t *pos, int n)
+        {
+            return o.grid[ci].store_sparse_fixed(blk, b, pos, n, max_abs[ci], overflow[ci]) ? 0 : ZPX_E_PANIC;
+        }
+    };
+    template <class Sink>
+    int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
+            Sink &sink);
+    int restart_parallel(const Scan &sc, bool &done);
     int sof(int32_t n);
     int dqt(int32_t n);
     int dht(int32_t n);
@@ -441,6 +510,7 @@ class Decoder {
     bool seen_sos_ = false;
     bool config_only_ = false;
     bool interleaved_[4] = {}, noninterleaved_[4] = {};
+    int threads_ = 1; // restart-interval-parallel Huffman (baseline scans with DRI)
 };
 
 int Decoder::sof(int32_t n)
@@ -705,109 +775,250 @@ int Decoder::sos(int32_t n)
     }
     for (int k = 0; k < ns; k++) (ns != 1 ? interleaved_ : noninterleaved_)[scan[k].id] = true;
 
+    Scan sc;
+    sc.ns = ns;
+    for (int k = 0; k < ns; k++) {
+        sc.c[k].id = scan[k].id;
+        sc.c[k].td = scan[k].td;
+        sc.c[k].ta = scan[k].ta;
+    }
+    sc.zs = zs;
+    sc.ze = ze;
+    sc.ah = ah;
+    sc.al = al;
+    sc.prog = o_.progressive;
+    sc.mxx = mxx;
+    sc.myy = myy;
     ba_ = bm_ = 0;
     bn_ = 0;
-    int32_t mcu = 0, block_count = 0;
-    uint8_t expected_rst = 0xd0;
-    int32_t dc[4] = {0, 0, 0, 0};
-    int32_t b[64];
-    uint8_t nzpos[64];
-    memset(b, 0, sizeof(b));
-    const bool prog = o_.progressive;
-    for (int32_t my = 0; my < myy; my++) {
-        for (int32_t mx = 0; mx < mxx; mx++) {
-            for (int k = 0; k < ns; k++) {
-                const int ci = scan[k].id;
-                const int32_t hi = o_.comp[ci].h, vi = o_.comp[ci].v;
-                CoeffGrid &g = o_.grid[ci];
-                const Huff &hdc = huff_[0][scan[k].td];
-                const Huff &hac = huff_[1][scan[k].ta];
-                for (int32_t j = 0; j < hi * vi; j++) {
-                    int32_t bx, by;
-                    if (ns != 1) {
-                        bx = hi * mx + j % hi;
-                        by = vi * my + j / hi;
-                    } else {
-                        bx = block_count % (mxx * hi);
-                        by = block_count / (mxx * hi);
-                        block_count++;
-                        if (bx * 8 >= static_cast<int32_t>(o_.width) ||
-                            by * 8 >= static_cast<int32_t>(o_.height))
-                            continue;
-                    }
-                    const size_t blk = size_t(by) * size_t(mxx * hi) + size_t(bx);
-                    // baseline: b stays all-zero between blocks; the positions a
-                    // block writes are recorded and cleared after its store
-                    int nnz = 0;
-                    if (prog) g.load(blk, b);
-                    if (ah != 0) {
-                        ZTRY(refine(b, hac, zs, ze, int32_t(1) << al));
-                    } else {
-                        int32_t zig = zs;
-                        if (zig == 0) {
-                            zig++;
-                            uint8_t t;
-                            ZTRY(huffman(hdc, t));
-                            if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
-                            int32_t delta;
-                            ZTRY(receive_extend(t, delta));
-                            dc[ci] += delta;
-                            b[0] = dc[ci] << al;
-                            nzpos[nnz++] = 0;
-                        }
-                        if (zig <= ze && eob_run_ > 0) {
-                            eob_run_--;
-                        } else {
-                            for (; zig <= ze; zig++) {
-                                uint8_t value;
-                                ZTRY(huffman(hac, value));
-                                const uint8_t v0r = value >> 4, v1 = value & 0x0f;
-                                if (v1 != 0) {
-                                    zig += v0r;
-                                    if (zig > ze) break;
-                                    int32_t ac;
-                                    ZTRY(receive_extend(v1, ac));
-                                    b[kUnzig[zig]] = ac << al;
-                                    nzpos[nnz++] = kUnzig[zig];
-                                } else {
-                                    if (v0r != 0x0f) {
-                                        eob_run_ = static_cast<uint16_t>(1u << v0r);
-                                        if (v0r != 0) {
-                                            uint32_t x;
-                                            ZTRY(bits(v0r, x));
-                                            eob_run_ |= static_cast<uint16_t>(x);
-                                        }
-                                        eob_run_--;
-                                        break;
-                                    }
-                                    zig += 0x0f;
-                                }
-                            }
-                        }
-                    }
-                    if (prog) {
-                        if (!g.store(blk, b)) return ZPX_E_OUT_OF_MEMORY;
-                    } else {
-                        if (!g.store_sparse(blk, b, nzpos, nnz)) return ZPX_E_OUT_OF_MEMORY;
-                        for (int i = 0; i < nnz; i++) b[nzpos[i]] = 0;
-                    }
+    bool done = false;
+    ZTRY(restart_parallel(sc, done));
+    if (!done) {
+        int32_t mcu_i = 0, block_count = 0;
+        uint8_t expected_rst = 0xd0;
+        int32_t dc[4] = {0, 0, 0, 0};
+        int32_t b[64];
+        uint8_t nzpos[64];
+        memset(b, 0, sizeof(b));
+        SerialSink sink{o_};
+        for (int32_t my = 0; my < myy; my++) {
+            for (int32_t mx = 0; mx < mxx; mx++) {
+                ZTRY(mcu(sc, my, mx, block_count, dc, b, nzpos, sink));
+                mcu_i++;
+                if (restart_interval_ > 0 && mcu_i % restart_interval_ == 0 && mcu_i < mxx * myy) {
+                    ZTRY(full(tmp_, 2));
+                    if (tmp_[0] != 0xff || tmp_[1] != expected_rst) ZTRY(find_rst(expected_rst));
+                    expected_rst = expected_rst == 0xd7 ? 0xd0 : static_cast<uint8_t>(expected_rst + 1);
+                    ba_ = bm_ = 0;
+                    bn_ = 0;
+                    dc[0] = dc[1] = dc[2] = dc[3] = 0;
+                    eob_run_ = 0;
                 }
-            }
-            mcu++;
-            if (restart_interval_ > 0 && mcu % restart_interval_ == 0 && mcu < mxx * myy) {
-                ZTRY(full(tmp_, 2));
-                if (tmp_[0] != 0xff || tmp_[1] != expected_rst) ZTRY(find_rst(expected_rst));
-                expected_rst = expected_rst == 0xd7 ? 0xd0 : static_cast<uint8_t>(expected_rst + 1);
-                ba_ = bm_ = 0;
-                bn_ = 0;
-                dc[0] = dc[1] = dc[2] = dc[3] = 0;
-                eob_run_ = 0;
             }
         }
     }
     // baseline reconstructs during the scan with the table current now
-    if (!prog)
+    if (!o_.progressive)
         for (int k = 0; k < ns; k++) snapshot_quant(scan[k].id);
+    return 0;
+}
+
+// One MCU of a scan: its blocks' Huffman / refinement decode and store (the
+// body of processSos's MCU loop, :1300-1431).  b is all-zero on entry for
+// baseline scans; the positions a block writes are recorded and cleared
+// after its store.
+template <class Sink>
+int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b,
+                 uint8_t *nzpos, Sink &sink)
+{
+    const int32_t mxx = sc.mxx;
+    for (int k = 0; k < sc.ns; k++) {
+        const int ci = sc.c[k].id;
+        const int32_t hi = o_.comp[ci].h, vi = o_.comp[ci].v;
+        CoeffGrid &g = o_.grid[ci];
+        const Huff &hdc = huff_[0][sc.c[k].td];
+        const Huff &hac = huff_[1][sc.c[k].ta];
+        for (int32_t j = 0; j < hi * vi; j++) {
+            int32_t bx, by;
+            if (sc.ns != 1) {
+                bx = hi * mx + j % hi;
+                by = vi * my + j / hi;
+            } else {
+                bx = block_count % (mxx * hi);
+                by = block_count / (mxx * hi);
+                block_count++;
+                if (bx * 8 >= static_cast<int32_t>(o_.width) || by * 8 >= static_cast<int32_t>(o_.height))
+                    continue;
+            }
+            const size_t blk = size_t(by) * size_t(mxx * hi) + size_t(bx);
+            int nnz = 0;
+            if (sc.prog) g.load(blk, b);
+            if (sc.ah != 0) {
+                ZTRY(refine(b, hac, sc.zs, sc.ze, int32_t(1) << sc.al));
+            } else {
+                int32_t zig = sc.zs;
+                if (zig == 0) {
+                    zig++;
+                    uint8_t t;
+                    ZTRY(huffman(hdc, t));
+                    if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+                    int32_t delta;
+                    ZTRY(receive_extend(t, delta));
+                    dc[ci] += delta;
+                    b[0] = dc[ci] << sc.al;
+                    nzpos[nnz++] = 0;
+                }
+                if (zig <= sc.ze && eob_run_ > 0) {
+                    eob_run_--;
+                } else {
+                    for (; zig <= sc.ze; zig++) {
+                        uint8_t value;
+                        ZTRY(huffman(hac, value));
+                        const uint8_t v0r = value >> 4, v1 = value & 0x0f;
+                        if (v1 != 0) {
+                            zig += v0r;
+                            if (zig > sc.ze) break;
+                            int32_t ac;
+                            ZTRY(receive_extend(v1, ac));
+                            b[kUnzig[zig]] = ac << sc.al;
+                            nzpos[nnz++] = kUnzig[zig];
+                        } else {
+                            if (v0r != 0x0f) {
+                                eob_run_ = static_cast<uint16_t>(1u << v0r);
+                                if (v0r != 0) {
+                                    uint32_t x;
+                                    ZTRY(bits(v0r, x));
+                                    eob_run_ |= static_cast<uint16_t>(x);
+                                }
+                                eob_run_--;
+                                break;
+                            }
+                            zig += 0x0f;
+                        }
+                    }
+                }
+            }
+            if (sc.prog) {
+                if (!g.store(blk, b)) return ZPX_E_OUT_OF_MEMORY;
+            } else {
+                ZTRY(sink.put(ci, blk, b, nzpos, nnz));
+                for (int i = 0; i < nnz; i++) b[nzpos[i]] = 0;
+            }
+        }
+    }
+    return 0;
+}
+
+std::atomic<int64_t> g_parallel_scans{0}; // zpx_debug_jpeg_parallel_scans
+
+// Restart-interval-parallel Huffman decoding of a baseline scan with DRI.
+// The RSTn markers (byte aligned; 0xFF inside entropy-coded data is always
+// stuffed as FF 00) split the scan into independent segments: each restarts
+// with an empty bit buffer, zero DC predictors and no EOB run (:1432-1452).
+// Segments decode on `threads_` threads, each with its own copy of the bit
+// reader over the whole input (so reads that run into a marker behave as in
+// the serial loop), and each must end exactly where the serial loop would
+// read its RST marker.  Anything else -- markers out of order or missing,
+// fill bytes, an error inside a segment, a segment ending elsewhere, a value
+// too wide for the grid -- leaves done = false, and the caller runs the
+// serial loop from the scan's start: its result and error are the
+// reference's by construction.  The last segment runs on this decoder, so
+// the state after the scan is the serial loop's.
+int Decoder::restart_parallel(const Scan &sc, bool &done)
+{
+    done = false;
+    const int32_t total = sc.mxx * sc.myy, ri = restart_interval_;
+    if (sc.prog || threads_ <= 1 || ri <= 0) return 0;
+    const char *mn = getenv("ZPX_HUFF_PAR_MIN_MCUS");
+    if (total < (mn ? atoi(mn) : 4096)) return 0;
+    const int32_t nseg = (total + ri - 1) / ri;
+    if (nseg < 2 || unread_ != 0) return 0;
+    std::vector<size_t> start(static_cast<size_t>(nseg)), end(static_cast<size_t>(nseg), len_);
+    start[0] = pos_;
+    int32_t k = 0;
+    for (size_t i = pos_; i + 1 < len_; i++) {
+        if (src_[i] != 0xff) continue;
+        const uint8_t m = src_[i + 1];
+        if (m == 0x00) {
+            i++;
+            continue;
+        }
+        if (m >= 0xd0 && m <= 0xd7 && k < nseg - 1) {
+            if (m != 0xd0 + (k & 7)) return 0;
+            end[static_cast<size_t>(k)] = i;
+            start[static_cast<size_t>(k) + 1] = i + 2;
+            k++;
+            i++;
+            continue;
+        }
+        break; // any other marker ends the scan's data
+    }
+    if (k != nseg - 1) return 0;
+    const int nthr = std::min<int>(threads_, nseg);
+    std::atomic<bool> ok{true};
+    std::vector<FixedSink> sinks(static_cast<size_t>(nthr), FixedSink{o_});
+    // segment s: MCUs [s * ri, min(total, (s + 1) * ri)) from byte start[s]
+    auto run_segment = [&](Decoder &d, FixedSink &sink, int32_t s) -> bool {
+        d.pos_ = start[static_cast<size_t>(s)];
+        d.unread_ = 0;
+        d.ba_ = d.bm_ = 0;
+        d.bn_ = 0;
+        d.eob_run_ = 0;
+        int32_t dc[4] = {0, 0, 0, 0}, b[64];
+        uint8_t nzpos[64];
+        memset(b, 0, sizeof(b));
+        const int32_t m0 = s * ri, m1 = std::min(total, m0 + ri);
+        int32_t block_count = 0;
+        if (sc.ns == 1) block_count = m0 * o_.comp[sc.c[0].id].h * o_.comp[sc.c[0].id].v;
+        for (int32_t m = m0; m < m1; m++)
+            if (d.mcu(sc, m / sc.mxx, m % sc.mxx, block_count, dc, b, nzpos, sink)) return false;
+        if (s == nseg - 1) return true;
+        d.settle(); // what the serial loop's readFull of the marker does first
+        return d.pos_ == end[static_cast<size_t>(s)];
+    };
+    // thread t takes the contiguous segments [nseg * t / nthr, nseg * (t+1) / nthr);
+    // workers run on copies of this decoder (made before any thread runs),
+    // this thread takes the last run, so it ends in the serial loop's state
+    std::vector<Decoder> copies;
+    copies.reserve(static_cast<size_t>(nthr - 1));
+    for (int t = 0; t < nthr - 1; t++) copies.emplace_back(*this);
+    auto run_range = [&](Decoder &d, int t) {
+        const int32_t a = nseg * t / nthr, z = nseg * (t + 1) / nthr;
+        for (int32_t s = a; s < z && ok.load(std::memory_order_relaxed); s++)
+            if (!run_segment(d, sinks[static_cast<size_t>(t)], s)) ok = false;
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr - 1 && ok; t++) {
+        try {
+            th.emplace_back([&, t] { run_range(copies[static_cast<size_t>(t)], t); });
+        } catch (...) { // no thread: the serial loop
+            ok = false;
+        }
+    }
+    const size_t scan_start = start[0];
+    if (ok) run_range(*this, nthr - 1);
+    const bool last_ok = ok;
+    for (auto &t : th) t.join();
+    if (!ok || !last_ok) { // serial from the scan's start
+        pos_ = scan_start;
+        unread_ = 0;
+        ba_ = bm_ = 0;
+        bn_ = 0;
+        eob_run_ = 0;
+        return 0;
+    }
+    for (int j = 0; j < sc.ns; j++) { // the width the values need, then the values too wide before
+        const int ci = sc.c[j].id;
+        int32_t m = 0;
+        std::vector<std::pair<size_t, int32_t>> ov;
+        for (auto &sk : sinks) {
+            m = std::max(m, sk.max_abs[ci]);
+            ov.insert(ov.end(), sk.overflow[ci].begin(), sk.overflow[ci].end());
+        }
+        if (!o_.grid[ci].apply_overflow(m, ov)) return ZPX_E_OUT_OF_MEMORY;
+    }
+    done = true;
+    g_parallel_scans.fetch_add(1, std::memory_order_relaxed);
     return 0;
 }
 
@@ -904,10 +1115,10 @@ int Decoder::run()
 
 } // namespace
 
-int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out)
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads)
 {
     try { // no exception crosses the ABI
-        Decoder d(buf, len, out);
+        Decoder d(buf, len, out, false, threads);
         if (int e = d.run()) return e;
         // one width per frame (the kernels take one coefficient type per frame)
         int bits = 8;
@@ -919,6 +1130,18 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out)
     } catch (...) {
         return ZPX_E_OUT_OF_MEMORY;
     }
+}
+
+int64_t jpeg_parallel_scans() { return g_parallel_scans.load(); }
+
+int jpeg_huff_threads()
+{
+    static const int n = [] {
+        if (const char *e = getenv("ZPX_HUFF_THREADS")) return std::max(1, atoi(e));
+        const unsigned hw = std::thread::hardware_concurrency();
+        return static_cast<int>(std::min(8u, hw ? hw : 1u));
+    }();
+    return n;
 }
 
 int jpeg_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h, int &model)

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "zpix_amd.h"
@@ -56,6 +57,14 @@ class CoeffGrid {
     // positions pos[] (all distinct).
     bool store_sparse(size_t blk, const int32_t *b, const uint8_t *pos, int n);
     bool widen_to(int bits);                  // no-op when already that wide
+    // Concurrent stores into the grid at its current width: disjoint blocks
+    // from several threads, no widening; a value too wide for the grid goes
+    // to `overflow` (element index, value) and the running max |value| to
+    // max_abs.  After the threads: apply_overflow widens to the width the
+    // max needs and writes the overflowed values.
+    bool store_sparse_fixed(size_t blk, const int32_t *b, const uint8_t *pos, int n, int32_t &max_abs,
+                            std::vector<std::pair<size_t, int32_t>> &overflow) const;
+    bool apply_overflow(int32_t max_abs, const std::vector<std::pair<size_t, int32_t>> &overflow);
     int32_t max_abs() const { return max_abs_; }
 
   private:
@@ -85,7 +94,14 @@ struct JpegCoeffs {
 // with the reference's error for malformed input.
 // Host entropy stage; on success every grid of the frame has the same
 // coefficient width (the widest any grid needed).
-int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out);
+// threads > 1: baseline scans with a restart interval decode their restart
+// segments in parallel (identical result; anything irregular falls back to
+// the serial loop).
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads = 1);
+// default thread count of the single-image entry points: ZPX_HUFF_THREADS,
+// else min(8, hardware threads)
+int jpeg_huff_threads();
+int64_t jpeg_parallel_scans(); // scans decoded restart-interval-parallel so far
 
 // jpeg.decodeConfig (decoder.zig:178-218): markers up to SOF (JFIF) or SOS,
 // skipping DQT/DRI/DHT.  model: ZPX_MODEL_GRAY or ZPX_MODEL_YCBCR.

@@ -203,6 +203,10 @@ int sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n, const 
         stats->wall_s = t1 - t0;
         for (auto &s : sh) {
             stats->host_s += s.st.host_s;
+            stats->host_jpeg_s += s.st.host_jpeg_s;
+            stats->host_png_s += s.st.host_png_s;
+            stats->jpeg_items += s.st.jpeg_items;
+            stats->png_items += s.st.png_items;
             stats->h2d_bytes += s.st.h2d_bytes;
             stats->d2h_bytes += s.st.d2h_bytes;
             stats->pixels += s.st.pixels;

@@ -654,7 +654,7 @@ static int zpx_jpeg_entropy_decode_impl(const uint8_t *buf, size_t len, zpx_jpeg
     if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
     std::unique_ptr<zpx_jpeg_coeffs> c(new zpx_jpeg_coeffs);
-    if (int e = jpeg_entropy_decode(buf, len, c->c)) return e;
+    if (int e = jpeg_entropy_decode(buf, len, c->c, jpeg_huff_threads())) return e;
     *out = c.release();
     return ZPX_OK;
 }
@@ -795,7 +795,7 @@ static int zpx_jpeg_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uin
     memset(out, 0, sizeof(*out));
     CtxScope s(ctx);
     JpegCoeffs c;
-    if (int e = jpeg_entropy_decode(buf, len, c)) return e;
+    if (int e = jpeg_entropy_decode(buf, len, c, jpeg_huff_threads())) return e;
     const JpegOut kind = jpeg_output_kind(c);
     if (c.n_comp == 4 && !c.adobe_valid) return ZPX_E_UNSUPPORTED_COLOR_MODEL; // applyBlack :793-795
     if (kind == JpegOut::YCCK) {
@@ -902,7 +902,7 @@ static int zpx_jpeg_decode_rgba_impl(zpx_ctx *ctx, const zpx_allocator *al, cons
     *rgba_len = 0;
     CtxScope s(ctx);
     JpegCoeffs c;
-    if (int e = jpeg_entropy_decode(buf, len, c)) return e;
+    if (int e = jpeg_entropy_decode(buf, len, c, jpeg_huff_threads())) return e;
     const JpegOut kind = jpeg_output_kind(c);
     const size_t n = size_t(c.width) * c.height * 4;
     bool fused = kind != JpegOut::CMYK && kind != JpegOut::YCCK;
@@ -1191,3 +1191,5 @@ extern "C" int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *se
 {
     return guarded([&] { return zpx_debug_png_stall_impl(ctx, spin_limit, seconds); });
 }
+
+extern "C" int64_t zpx_debug_jpeg_parallel_scans(void) { return jpeg_parallel_scans(); }
