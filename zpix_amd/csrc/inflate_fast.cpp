@@ -10,9 +10,13 @@
 // behaviour is zlib's by construction.  A stream it accepts is one zlib
 // accepts too, and DEFLATE output is unique, so the bytes are identical.
 //
-// Design: 64-bit bit buffer refilled 8 bytes at a time; literal/length codes
-// through an 11-bit table (symbol + length, or a flag for longer codes that
-// a canonical first-code walk resolves), distances through an 8-bit table.
+// Design: 64-bit bit buffer refilled 8 bytes at a time; two-level decode
+// tables of 32-bit entries (an 11-bit literal/length root and an 8-bit
+// distance root, subtables for longer codes) whose entries carry the decoded
+// result -- literal byte, or length / distance base and extra-bit count -- so
+// a symbol costs one or two lookups and no bit loop.  A "fast zone" loop runs
+// while at least 32 input bytes and 258 + 8 output bytes remain: there no
+// literal needs an end-of-input or end-of-output check.
 #include "inflate_fast.h"
 
 #include <cstring>
@@ -22,62 +26,106 @@ namespace {
 
 constexpr int kLitBits = 11, kDistBits = 8;
 
-struct Table {
-    // fast[code >> (15 - bits)] = symbol << 4 | length (0 = code longer than `bits`)
-    uint16_t fast[1 << kLitBits];
-    int bits;
-    // canonical tables for the slow walk
-    uint16_t count[16];
-    uint16_t first[16]; // first code of each length (left-aligned in `len` bits)
-    uint16_t index[16]; // index in `sorted` of the first symbol of each length
-    uint16_t sorted[320];
-    int max_len;
-};
+// entry: bits 0-4 = bits to drop; bits 5-8 = extra-bit count (length /
+// distance) or index bits (subtable); flags in bits 9-12; payload in bits
+// 16-31 = the literal byte, the length / distance base (<= 24577), the
+// subtable's offset from the table start, or the code-length symbol
+constexpr uint32_t kLiteral = 1u << 9;
+constexpr uint32_t kSub = 1u << 10;
+constexpr uint32_t kEob = 1u << 11;     // end of block
+constexpr uint32_t kInvalid = 1u << 12; // symbol 286/287 or distance 30/31
+inline uint32_t drop_of(uint32_t e) { return e & 31; }
+inline uint32_t extra_of(uint32_t e) { return (e >> 5) & 15; }
+inline uint32_t payload(uint32_t e) { return e >> 16; }
 
-// Builds a canonical Huffman table; false on an over-subscribed or
-// incomplete set (zlib allows a lone length-1 distance code: we reject it and
-// let zlib handle that stream).
-bool build(Table &t, const uint8_t *lens, int n, int fast_bits)
+constexpr int kLitEntries = 8192, kDistEntries = 4096; // root + worst-case subtables
+
+const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                               31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+const uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+const uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+const uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+
+enum class Kind { LitLen, Dist, CodeLen };
+
+// the decoded result of symbol s, without the drop count
+uint32_t result(Kind k, int s)
 {
-    memset(t.count, 0, sizeof(t.count));
-    for (int i = 0; i < n; i++) t.count[lens[i]]++;
-    t.count[0] = 0;
+    switch (k) {
+    case Kind::LitLen:
+        if (s < 256) return kLiteral | uint32_t(s) << 16;
+        if (s == 256) return kEob;
+        if (s - 257 >= 29) return kInvalid;
+        return uint32_t(kLenBase[s - 257]) << 16 | uint32_t(kLenExtra[s - 257]) << 5;
+    case Kind::Dist:
+        if (s >= 30) return kInvalid;
+        return uint32_t(kDistBase[s]) << 16 | uint32_t(kDistExtra[s]) << 5;
+    default:
+        return uint32_t(s) << 16; // code-length alphabet: the symbol
+    }
+}
+
+// Builds a two-level canonical Huffman table (root `root` bits); false on an
+// over-subscribed or incomplete set (zlib allows a lone length-1 distance
+// code: we reject it and let zlib handle that stream).
+bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind)
+{
+    uint16_t count[16] = {};
+    for (int i = 0; i < n; i++) count[lens[i]]++;
+    count[0] = 0;
     int left = 1;
     for (int l = 1; l < 16; l++) {
         left <<= 1;
-        left -= t.count[l];
+        left -= count[l];
         if (left < 0) return false; // over-subscribed
     }
     if (left != 0) return false; // incomplete (or empty)
-    // canonical first codes (RFC 1951 3.2.2) and sorted symbol order
-    uint16_t code = 0, idx = 0;
-    t.max_len = 0;
+    uint16_t next[16];
+    uint16_t code = 0;
     for (int l = 1; l < 16; l++) {
-        code = static_cast<uint16_t>((code + t.count[l - 1]) << 1);
-        t.first[l] = code;
-        t.index[l] = idx;
-        idx = static_cast<uint16_t>(idx + t.count[l]);
-        if (t.count[l]) t.max_len = l;
+        code = static_cast<uint16_t>((code + count[l - 1]) << 1);
+        next[l] = code;
     }
-    uint16_t offs[16], next[16];
-    for (int l = 1; l < 16; l++) {
-        offs[l] = t.index[l];
-        next[l] = t.first[l];
-    }
-    for (int s = 0; s < n; s++)
-        if (lens[s]) t.sorted[offs[lens[s]]++] = static_cast<uint16_t>(s);
-    // fast table, indexed by the next `fast_bits` stream bits: codes are
-    // stored MSB-first in an LSB-first bit stream, so by the reversed code
-    t.bits = fast_bits;
-    memset(t.fast, 0, sizeof(uint16_t) << fast_bits);
+    // codes are stored MSB-first in an LSB-first bit stream: index by the reversed code
+    uint16_t rev[320];
+    int len_of[320];
+    uint8_t sub_bits[1 << kLitBits] = {}; // per root index: bits of its subtable
     for (int s = 0; s < n; s++) {
         const int l = lens[s];
+        len_of[s] = l;
         if (!l) continue;
         const uint16_t c = next[l]++;
-        if (l > fast_bits) continue;
         uint32_t r = 0;
         for (int k = 0; k < l; k++) r |= ((c >> k) & 1u) << (l - 1 - k);
-        for (uint32_t k = r; k < (1u << fast_bits); k += (1u << l)) t.fast[k] = static_cast<uint16_t>(s << 4 | l);
+        rev[s] = static_cast<uint16_t>(r);
+        if (l > root) {
+            const uint32_t p = r & ((1u << root) - 1);
+            if (l - root > sub_bits[p]) sub_bits[p] = static_cast<uint8_t>(l - root);
+        }
+    }
+    const int nroot = 1 << root;
+    int used = nroot;
+    for (int p = 0; p < nroot; p++) {
+        if (!sub_bits[p]) continue;
+        const int size = 1 << sub_bits[p];
+        if (used + size > cap) return false;
+        t[p] = kSub | uint32_t(used) << 16 | uint32_t(sub_bits[p]) << 5 | uint32_t(root);
+        used += size;
+    }
+    for (int s = 0; s < n; s++) {
+        const int l = len_of[s];
+        if (!l) continue;
+        const uint32_t r = rev[s];
+        if (l <= root) {
+            const uint32_t e = result(kind, s) | uint32_t(l);
+            for (uint32_t k = r; k < uint32_t(nroot); k += (1u << l)) t[k] = e;
+        } else {
+            const uint32_t p = r & (uint32_t(nroot) - 1), rest = r >> root;
+            const uint32_t off = payload(t[p]), sb = extra_of(t[p]);
+            const uint32_t e = result(kind, s) | uint32_t(l - root);
+            for (uint32_t k = rest; k < (1u << sb); k += (1u << (l - root))) t[off + k] = e;
+        }
     }
     return true;
 }
@@ -91,7 +139,7 @@ struct Bits {
 
     inline void refill()
     {
-        if (cnt >= 48) return; // callers decode up to 45 bits (three codes) per refill
+        if (cnt >= 48) return;
         if (pos + 8 <= len) {
             uint64_t w;
             memcpy(&w, in + pos, 8);
@@ -106,6 +154,16 @@ struct Bits {
                 cnt += 8;
             }
         }
+    }
+    // refill with at least 8 readable input bytes (the fast zone)
+    inline void refill_fast()
+    {
+        uint64_t w;
+        memcpy(&w, in + pos, 8);
+        buf |= w << cnt;
+        const int take = (63 - cnt) >> 3;
+        pos += take;
+        cnt += take * 8;
     }
     // true once a consumed bit lay past the end of the input
     inline bool overrun() const { return cnt < pad; }
@@ -123,34 +181,34 @@ struct Bits {
     }
 };
 
-// Decodes one symbol (bit buffer holds >= 15 bits); -1 on an invalid code.
-inline int decode(Bits &b, const Table &t)
+// One symbol's entry (the buffer holds >= 15 bits); its bits are consumed.
+inline uint32_t decode(Bits &b, const uint32_t *t, int root)
 {
-    const uint16_t e = t.fast[b.peek(t.bits)];
-    if (e) {
-        b.drop(e & 15);
-        return e >> 4;
+    uint32_t e = t[b.peek(root)];
+    if (e & kSub) {
+        b.drop(root);
+        e = t[payload(e) + b.peek(static_cast<int>(extra_of(e)))];
     }
-    // canonical walk for codes longer than the fast table
-    uint32_t code = 0;
-    for (int l = 1; l <= 15; l++) {
-        code |= (b.peek(l) >> (l - 1)) & 1u;
-        const int cnt = t.count[l];
-        if (static_cast<int>(code) - static_cast<int>(t.first[l]) < cnt && code >= t.first[l]) {
-            b.drop(l);
-            return t.sorted[t.index[l] + (code - t.first[l])];
-        }
-        code <<= 1;
-    }
-    return -1;
+    b.drop(static_cast<int>(drop_of(e)));
+    return e;
 }
 
-const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                               31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-const uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-const uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
-                                193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-const uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// match copy of n bytes from distance d (d <= bytes already written)
+inline void copy_match(uint8_t *dst, size_t d, size_t n)
+{
+    const uint8_t *src = dst - d;
+    if (d >= 8) {
+        size_t k = 0;
+        for (; k + 8 <= n; k += 8) { // with d >= 8 a chunk never reads bytes it writes
+            uint64_t w;
+            memcpy(&w, src + k, 8);
+            memcpy(dst + k, &w, 8);
+        }
+        for (; k < n; k++) dst[k] = src[k];
+    } else {
+        for (size_t k = 0; k < n; k++) dst[k] = src[k];
+    }
+}
 
 } // namespace
 
@@ -164,7 +222,7 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
     b.in = in + 2;
     b.len = in_len - 2;
     size_t o = 0;
-    static thread_local Table lit, dist;
+    static thread_local uint32_t lit[kLitEntries], dist[kDistEntries];
     bool last = false;
     while (!last && o < want) {
         b.refill();
@@ -200,10 +258,10 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
             for (int i = 256; i < 280; i++) l[i] = 7;
             for (int i = 280; i < 288; i++) l[i] = 8;
             // zlib's fixed table has 288 literal/length symbols (286, 287 invalid when used)
-            if (!build(lit, l, 288, kLitBits)) return false;
+            if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen)) return false;
             uint8_t d[32];
             for (int i = 0; i < 32; i++) d[i] = 5;
-            if (!build(dist, d, 32, kDistBits)) return false;
+            if (!build(dist, kDistEntries, d, 32, kDistBits, Kind::Dist)) return false;
         } else if (type == 2) { // dynamic
             b.refill();
             const int hlit = static_cast<int>(b.take(5)) + 257;
@@ -216,14 +274,14 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
                 b.refill();
                 cl[kOrd[i]] = static_cast<uint8_t>(b.take(3));
             }
-            static thread_local Table clt;
-            if (!build(clt, cl, 19, 7)) return false;
+            static thread_local uint32_t clt[1 << 7];
+            if (!build(clt, 1 << 7, cl, 19, 7, Kind::CodeLen)) return false;
             uint8_t lens[320];
             int n = 0;
             while (n < hlit + hdist) {
                 b.refill();
-                const int sym = decode(b, clt);
-                if (sym < 0 || b.overrun()) return false;
+                const int sym = static_cast<int>(payload(decode(b, clt, 7)));
+                if (b.overrun()) return false;
                 if (sym < 16) {
                     lens[n++] = static_cast<uint8_t>(sym);
                 } else {
@@ -243,69 +301,68 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
                 }
             }
             if (lens[256] == 0) return false; // no end-of-block code
-            if (!build(lit, lens, hlit, kLitBits)) return false;
-            if (!build(dist, lens + hlit, hdist, kDistBits)) return false;
+            if (!build(lit, kLitEntries, lens, hlit, kLitBits, Kind::LitLen)) return false;
+            if (!build(dist, kDistEntries, lens + hlit, hdist, kDistBits, Kind::Dist)) return false;
         } else {
             return false;
         }
         if (b.overrun()) return false;
         // ---- the block's symbols
         for (;;) {
-            // one refill leaves >= 56 bits: up to three literal codes (<= 15
-            // bits each) decode before the next refill
-            b.refill();
-            int sym = decode(b, lit);
-            if (sym < 256 && sym >= 0) {
-                if (b.overrun() || o >= want) {
-                    if (b.overrun()) return false;
+            uint32_t e;
+            if (b.pos + 32 <= b.len && o + 258 + 8 <= want) {
+                // fast zone: real input bytes behind every bit and room for a
+                // whole match -- no end checks per symbol
+                b.refill_fast();
+                e = decode(b, lit, kLitBits);
+                if (e & kLiteral) {
+                    out[o++] = static_cast<uint8_t>(payload(e));
+                    e = decode(b, lit, kLitBits);
+                    if (e & kLiteral) {
+                        out[o++] = static_cast<uint8_t>(payload(e));
+                        e = decode(b, lit, kLitBits);
+                        if (e & kLiteral) {
+                            out[o++] = static_cast<uint8_t>(payload(e));
+                            continue;
+                        }
+                    }
+                }
+                if (e & (kEob | kInvalid)) {
+                    if (e & kInvalid) return false;
                     break;
                 }
-                out[o++] = static_cast<uint8_t>(sym);
-                sym = decode(b, lit);
-                if (sym < 256 && sym >= 0) {
-                    if (b.overrun() || o >= want) {
-                        if (b.overrun()) return false;
-                        break;
-                    }
-                    out[o++] = static_cast<uint8_t>(sym);
-                    sym = decode(b, lit);
-                    if (sym < 256 && sym >= 0) {
-                        if (b.overrun() || o >= want) {
-                            if (b.overrun()) return false;
-                            break;
-                        }
-                        out[o++] = static_cast<uint8_t>(sym);
-                        continue;
-                    }
-                }
+                // a length: its extra bits, then the distance (one refill covers
+                // extra <= 5 + distance code <= 15 + extra <= 13 bits)
+                b.refill_fast();
+                const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
+                const uint32_t de = decode(b, dist, kDistBits);
+                if (de & kInvalid) return false;
+                const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
+                if (d > o) return false; // distance past the start of the output
+                copy_match(out + o, d, len);
+                o += len;
+                continue;
             }
-            if (sym < 0 || b.overrun()) return false;
-            if (sym == 256) break;
+            // careful path near the end of the input or the output
             b.refill();
-            const int li = sym - 257;
-            if (li >= 29) return false; // 286, 287
-            const uint32_t len = kLenBase[li] + b.take(kLenExtra[li]);
+            e = decode(b, lit, kLitBits);
+            if (b.overrun() || (e & kInvalid)) return false;
+            if (e & kLiteral) {
+                if (o >= want) break;
+                out[o++] = static_cast<uint8_t>(payload(e));
+                continue;
+            }
+            if (e & kEob) break;
             b.refill();
-            const int ds = decode(b, dist);
-            if (ds < 0 || ds >= 30) return false;
-            const uint32_t d = kDistBase[ds] + b.take(kDistExtra[ds]);
+            const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
+            b.refill();
+            const uint32_t de = decode(b, dist, kDistBits);
+            if (de & kInvalid) return false;
+            const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
             if (b.overrun()) return false;
-            if (d > o) return false; // distance past the start of the output
-            size_t n = len < want - o ? len : want - o;
-            uint8_t *dst = out + o;
-            const uint8_t *src = dst - d;
-            if (d >= 8 && n >= 8) {
-                // 8-byte chunks: with d >= 8 a chunk never reads bytes it writes
-                size_t k = 0;
-                for (; k + 8 <= n; k += 8) {
-                    uint64_t w;
-                    memcpy(&w, src + k, 8);
-                    memcpy(dst + k, &w, 8);
-                }
-                for (; k < n; k++) dst[k] = src[k];
-            } else {
-                for (size_t k = 0; k < n; k++) dst[k] = src[k];
-            }
+            if (d > o) return false;
+            const size_t n = len < want - o ? len : want - o;
+            copy_match(out + o, d, n);
             o += n;
             if (o >= want) break;
         }
