@@ -16,6 +16,15 @@ for p in sorted(os.listdir(base)):
         short = ("jpeg_rgba" if "jpeg_rgba" in name else "jpeg_block" if "jpeg_block_kernel" in name
                  else "png_unfilter" if "png_unfilter" in name
                  else "png_pair" if "png_pair_kernel" in name else None)
+        import re
+        if short == "png_pair":  # one entry per depth template (tc8 vs the Adam7 RGBA16 line)
+            m = re.search(r"png_pair_kernel<(\d+)", name)
+            if m and m.group(1) != "6":
+                short = "png_pair_d" + m.group(1)
+        if short == "jpeg_block":  # the headline instance keeps the plain key
+            m = re.search(r"jpeg_block_kernel<([^>]*)>", name)
+            if m and m.group(1).replace(" ", "") not in ("signedchar,true,2,2,1,1,0", "char,true,2,2,1,1,0"):
+                short = "jpeg_block<" + m.group(1).replace(" ", "") + ">"
         if not short:
             continue
         acc[short][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))

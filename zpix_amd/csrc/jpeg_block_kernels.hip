@@ -65,8 +65,17 @@ __device__ __forceinline__ void wave_lds_sync()
 #ifndef ZPX_JPEGB_DEPTH2
 #define ZPX_JPEGB_DEPTH2 0 // 1: int8 coefficient DMA two passes ahead (measured slower)
 #endif
+#ifndef ZPX_JPEGB_STORE_LDS
+#define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores)
+#endif
+#ifndef ZPX_JPEGB_DMA_NT
+#define ZPX_JPEGB_DMA_NT 0 // 1: non-temporal coefficient DMA (measured 0.8 % slower)
+#endif
+#ifndef ZPX_JPEGB_XCD_REMAP
+#define ZPX_JPEGB_XCD_REMAP 1 // consecutive tasks on one XCD (0: round-robin)
+#endif
 #ifndef ZPX_JPEGB_STORE_AUX
-#define ZPX_JPEGB_STORE_AUX 0 // cache policy of the RGBA stores (a row's two halves meet in L2)
+#define ZPX_JPEGB_STORE_AUX 2 // cache policy of the RGBA stores (2 = nt; whole lines per instruction)
 #endif
 
 // The wave's LDS image of one pass's coefficients: 64 blocks as 16-byte
@@ -98,7 +107,7 @@ __device__ __forceinline__ void glds16(const void *src, const void *lds_base)
     const uint32_t dst = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
         (const __attribute__((address_space(3))) void *)lds_base));
     uint32_t keep;
-#if ZPX_COEF_NT
+#if ZPX_JPEGB_DMA_NT
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
 #else
@@ -113,26 +122,26 @@ __device__ __forceinline__ void dequant_block(const uint8_t *img, int j, const i
 {
     using I = CoefImage<CoefT>;
     constexpr int PER = 16 / static_cast<int>(sizeof(CoefT)); // coefficients per piece
+    // one piece at a time: its 16 bytes and its PER table values are read
+    // together (one LDS wait per piece), then multiplied
 #pragma unroll
     for (int pc = 0; pc < I::P; pc++) {
         const u32x4 w = *reinterpret_cast<const u32x4 *>(img + 16 * I::slot(j, pc));
+        i32x4 qv[PER / 4];
 #pragma unroll
-        for (int i = 0; i < PER; i += 4) {
-            const i32x4 qv = *reinterpret_cast<const i32x4 *>(q + pc * PER + i);
+        for (int i = 0; i < PER / 4; i++) qv[i] = *reinterpret_cast<const i32x4 *>(q + pc * PER + 4 * i);
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int k = pc * PER + i + e; // coefficient index
-                const int kk = i + e;           // index inside the piece
-                if constexpr (sizeof(CoefT) == 1) {
-                    // |coef| < 2^7, q < 2^17: the 24-bit multiply is exact
-                    s[k] = __mul24(static_cast<int32_t>(w[kk >> 2] << (24 - 8 * (kk & 3))) >> 24, qv[e]);
-                } else {
-                    s[k] = __mul24(static_cast<int32_t>(w[kk >> 1] << (16 - 16 * (kk & 1))) >> 16, qv[e]);
-                }
-                // materialize the product here: otherwise hipcc sinks the
-                // multiplies into the IDCT and keeps all 64 table values live
-                asm volatile("" : "+v"(s[k]));
+        for (int kk = 0; kk < PER; kk++) {
+            const int k = pc * PER + kk; // coefficient index
+            if constexpr (sizeof(CoefT) == 1) {
+                // |coef| < 2^7, q < 2^17: the 24-bit multiply is exact
+                s[k] = __mul24(static_cast<int32_t>(w[kk >> 2] << (24 - 8 * (kk & 3))) >> 24, qv[kk >> 2][kk & 3]);
+            } else {
+                s[k] = __mul24(static_cast<int32_t>(w[kk >> 1] << (16 - 16 * (kk & 1))) >> 16, qv[kk >> 2][kk & 3]);
             }
+            // materialize the product here: otherwise hipcc sinks the
+            // multiplies into the IDCT and keeps all 64 table values live
+            asm volatile("" : "+v"(s[k]));
         }
     }
 }
@@ -242,6 +251,9 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     constexpr int DEPTH = (ZPX_JPEGB_DEPTH2 && sizeof(CoefT) == 1 && NP >= 2) ? 2 : 1;
     __shared__ __attribute__((aligned(16))) uint8_t cimg[DEPTH * IMG];
     __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
+#if ZPX_JPEGB_STORE_LDS
+    __shared__ __attribute__((aligned(16))) uint8_t otile[2048]; // one output row of the task (512 RGBA px)
+#endif
     const int lane = threadIdx.x;
 
     // per-frame uniform values, read once per frame change (frame fields
@@ -314,7 +326,19 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         wave_lds_sync();
     };
 
+#if ZPX_JPEGB_XCD_REMAP
+    // workgroups are dealt to the 8 XCDs round-robin: renumber them so that
+    // the waves of one XCD hold consecutive task indices (neighbouring tasks
+    // share an XCD's L2)
+    int task;
+    {
+        const int nw = static_cast<int>(gridDim.x), w = static_cast<int>(blockIdx.x);
+        const int q = nw / 8, r = nw % 8, x = w % 8;
+        task = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+    }
+#else
     int task = blockIdx.x;
+#endif
     if (task >= total_tasks) return;
     const int tstride = static_cast<int>(gridDim.x);
     int f, my, mx0;
@@ -511,12 +535,28 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
                     // (the host sends only frames with 16-byte aligned rows and
                     // W % 4 == 0: a 4-pixel piece is wholly inside or outside)
+#if ZPX_JPEGB_STORE_LDS
+                    // the row's 512 pixels through a 2 KiB LDS row tile: each
+                    // store instruction then writes 1 KiB contiguous (whole lines)
+                    *reinterpret_cast<u32x4 *>(otile + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
+                    *reinterpret_cast<u32x4 *>(otile + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
+                    wave_lds_sync(); // (cross-lane: keep hipcc from reordering around it)
+                    const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + 16 * lane);
+                    const u32x4 vb = *reinterpret_cast<const u32x4 *>(otile + 1024 + 16 * lane);
+                    wave_lds_sync();
+                    const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
+                    __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
+                                                           0, ZPX_JPEGB_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, xb < W ? rowoff + static_cast<uint32_t>(xb) * 4 : kDrop,
+                                                           0, ZPX_JPEGB_STORE_AUX);
+#else
                     const uint32_t o0 = xpix < W ? rowoff + static_cast<uint32_t>(xpix) * 4 : kDrop;
                     const uint32_t o1 = xpix + 4 < W ? rowoff + static_cast<uint32_t>(xpix) * 4 + 16 : kDrop;
                     __builtin_amdgcn_raw_buffer_store_b128(u32x4{px[0], px[1], px[2], px[3]}, orsrc, o0, 0,
                                                            ZPX_JPEGB_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b128(u32x4{px[4], px[5], px[6], px[7]}, orsrc, o1, 0,
                                                            ZPX_JPEGB_STORE_AUX);
+#endif
                 }
             }
         });
