@@ -33,6 +33,10 @@ class BatchStats:
     host_threads: int
     depth: int
     failed: int
+    host_jpeg_s: float = 0.0  # host_s split by stage: JPEG entropy decode
+    host_png_s: float = 0.0   # PNG chunk walk + inflate
+    jpeg_items: int = 0
+    png_items: int = 0
 
     @property
     def mpix_s(self) -> float:
@@ -114,5 +118,5 @@ def decode_rgba(buffers, on_host: bool = False, host_threads: int = 0, depth: in
                                outs[i] if ok else None))
     if with_stats:
         return res, BatchStats(st.wall_s, st.host_s, st.h2d_bytes, st.d2h_bytes, st.pixels, st.host_threads,
-                               st.depth, st.failed)
+                               st.depth, st.failed, st.host_jpeg_s, st.host_png_s, st.jpeg_items, st.png_items)
     return res
