@@ -41,7 +41,8 @@ typedef struct zpx_ctx zpx_ctx;
 /* errors                                                                  */
 /* ---------------------------------------------------------------------- */
 /* Status codes.  Every name is the reference's Zig error name (the JPEG set
- * from src/jpeg/decoder.zig, the PNG set from src/png/decoder.zig), plus
+ * from src/jpeg/decoder.zig, the PNG set from src/png/decoder.zig, the BMP set
+ * from src/bmp/decoder.zig:317-325, the QOI set from src/qoi/{decoder,encoder}.zig), plus
  * Unsupported / Panic / Hip / InvalidArgument for conditions of the device
  * path itself.  zpx_error_name(code) returns the name. */
 #define ZPX_ERROR_LIST(X) \
@@ -117,7 +118,16 @@ typedef struct zpx_ctx zpx_ctx;
     X(Hip, HIP) \
     X(InvalidArgument, INVALID_ARGUMENT) \
     X(FileNotFound, FILE_NOT_FOUND) \
-    X(UnknownImageFormat, UNKNOWN_IMAGE_FORMAT)
+    X(UnknownImageFormat, UNKNOWN_IMAGE_FORMAT) \
+    X(InvalidSignature, INVALID_SIGNATURE) \
+    X(UnsupportedHeader, UNSUPPORTED_HEADER) \
+    X(UnsupportedDimensions, UNSUPPORTED_DIMENSIONS) \
+    X(UnsupportedCompression, UNSUPPORTED_COMPRESSION) \
+    X(UnsupportedBPP, UNSUPPORTED_BPP) \
+    X(UnsupportedPaletteSize, UNSUPPORTED_PALETTE_SIZE) \
+    X(UnsupportedColorOffset, UNSUPPORTED_COLOR_OFFSET) \
+    X(InvalidQoiData, INVALID_QOI_DATA) \
+    X(InvalidQoiHeader, INVALID_QOI_HEADER)
 
 enum zpx_status {
 #define ZPX_ENUM_(name, up) ZPX_E_##up,
@@ -246,8 +256,53 @@ int zpx_png_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_im
 /* png.probeBuffer, src/png/root.zig:37-40 */
 int zpx_png_probe_buffer(const uint8_t *buf, size_t len);
 
-/* zpix.fromBuffer / zpix.fromFilePath, src/root.zig:24-40 (PNG and JPEG;
- * QOI/BMP are out of scope and return ZPX_E_UNSUPPORTED). */
+/* bmp.decode / bmp.loadFromBuffer: src/bmp/decoder.zig:25-40,
+ * src/bmp/root.zig:21-25.  The header and palette (readHeader :42-158) are
+ * parsed on the host; the row loop (bottom-up flip, BGR(A) -> RGBA, palette
+ * index unpack; :160-307) is a HIP kernel.  Returns .Paletted (1/2/4/8 bpp),
+ * .RGBA (24 bpp) or .NRGBA (32 bpp); a short file is EndOfStream. */
+int zpx_bmp_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                   zpx_image *out);
+/* bmp.load, src/bmp/root.zig:8-19 */
+int zpx_bmp_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out);
+/* bmp.probeBuffer, src/bmp/root.zig:28-31 */
+int zpx_bmp_probe_buffer(const uint8_t *buf, size_t len);
+
+/* qoi.decode / qoi.loadFromBuffer: src/qoi/decoder.zig:20-130,
+ * src/qoi/root.zig:34-38.  Returns .RGBA.  Every QOI chunk depends on the
+ * previous pixel and on a hash table whose slot is picked by decoded values,
+ * so this is a serial host loop like Huffman and inflate; ctx may be NULL. */
+int zpx_qoi_decode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
+                   zpx_image *out);
+/* qoi.load, src/qoi/root.zig:20-31 */
+int zpx_qoi_load(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out);
+/* qoi.probeBuffer, src/qoi/root.zig:41-49 */
+int zpx_qoi_probe_buffer(const uint8_t *buf, size_t len);
+
+/* qoi.Desc, src/qoi/encoder.zig:20-25 */
+typedef struct zpx_qoi_desc {
+    uint32_t width, height;
+    uint8_t channels;   /* 3 = RGB, 4 = RGBA */
+    uint8_t colorspace; /* 0 = sRGB with linear alpha, 1 = all linear */
+    uint8_t pad[2];
+} zpx_qoi_desc;
+/* qoi.encode, src/qoi/encoder.zig:29-132: pixels (host, width*height*channels
+ * bytes) -> QOI file bytes, caller-owned from al.  Encoded on the GPU as a
+ * segmented scan; byte-identical to the serial loop.  InvalidQoiHeader for a
+ * desc the reference rejects (:34-36). */
+int zpx_qoi_encode(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *pixels, size_t pixels_len,
+                   const zpx_qoi_desc *desc, uint8_t **out, size_t *out_len);
+/* Upper bound of the encoded size (the reference's maxSize, encoder.zig:41-42). */
+size_t zpx_qoi_encode_bound(const zpx_qoi_desc *desc);
+/* Device form: d_pixels and d_out (>= zpx_qoi_encode_bound bytes) are device
+ * pointers; the encoded length lands in *d_out_len (device uint64).  Enqueued
+ * on `stream` (NULL = the context's stream) with no host synchronisation once
+ * the context's scratch is large enough. */
+int zpx_qoi_encode_device(zpx_ctx *ctx, const uint8_t *d_pixels, const zpx_qoi_desc *desc, uint8_t *d_out,
+                          size_t out_cap, uint64_t *d_out_len, void *stream);
+
+/* zpix.fromBuffer / zpix.fromFilePath, src/root.zig:24-40: probes PNG, JPEG,
+ * QOI, BMP in that order; UnknownImageFormat otherwise. */
 int zpx_from_buffer(zpx_ctx *ctx, const zpx_allocator *al, const uint8_t *buf, size_t len,
                     zpx_image *out);
 int zpx_from_file_path(zpx_ctx *ctx, const zpx_allocator *al, const char *path, zpx_image *out);

@@ -115,7 +115,16 @@ double zo_png_unfilter_seconds(void)
     X(InvalidImageDimensions)                                                  \
     X(OutOfMemory)                                                             \
     X(Unsupported)                                                             \
-    X(Panic)
+    X(Panic)                                                                   \
+    X(InvalidSignature)                                                        \
+    X(UnsupportedHeader)                                                       \
+    X(UnsupportedDimensions)                                                   \
+    X(UnsupportedCompression)                                                  \
+    X(UnsupportedBPP)                                                          \
+    X(UnsupportedPaletteSize)                                                  \
+    X(UnsupportedColorOffset)                                                  \
+    X(InvalidQoiData)                                                          \
+    X(InvalidQoiHeader)
 
 enum zo_err {
 #define X(n) E_##n,
@@ -2129,4 +2138,298 @@ fail:
     if (d.have_img) zo_image_free(&d.img);
     free(d.palette);
     return e;
+}
+
+/* ======================================================================== */
+/* BMP                                                                       */
+/* ======================================================================== */
+
+static uint32_t le32(const uint8_t *b) { return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24; }
+static uint32_t le16(const uint8_t *b) { return (uint32_t)b[0] | (uint32_t)b[1] << 8; }
+
+/* bmp Decoder.decode (src/bmp/decoder.zig:25-40), readHeader (:42-158),
+ * decodePaletted (:160-229), decodeRGB (:231-270), decodeNRGBA (:272-307).
+ * The reader is a fixed buffer: every short read is EndOfStream. */
+int zo_bmp_decode(const uint8_t *buf, size_t len, zo_image *out)
+{
+    memset(out, 0, sizeof(*out));
+    size_t pos = 0;
+#define BMP_READ(n)                                                            \
+    do {                                                                       \
+        if (len - pos < (size_t)(n)) return E_EndOfStream;                     \
+    } while (0)
+    BMP_READ(18);
+    const uint8_t *b = buf;
+    if (!(b[0] == 'B' && b[1] == 'M')) return E_InvalidSignature;
+    const uint32_t pixel_off = le32(b + 10), info_len = le32(b + 14);
+    if (info_len != 40 && info_len != 108 && info_len != 124) return E_UnsupportedHeader;
+    pos = 18;
+    BMP_READ(14 + info_len - 18);
+    pos = 14 + info_len;
+    const int32_t w = (int32_t)le32(b + 18);
+    int32_t hh = (int32_t)le32(b + 22);
+    int top_down = 0;
+    if (hh < 0) {
+        if (hh == INT32_MIN) return E_UnsupportedDimensions; /* Zig would trap on the negation */
+        hh = -hh;
+        top_down = 1;
+    }
+    if (w < 0) return E_UnsupportedDimensions;
+    const uint32_t planes = le16(b + 26), bpp = le16(b + 28);
+    uint32_t compression = le32(b + 30);
+    if (compression == 3 && info_len > 40) { /* :77-86 */
+        if (le32(b + 54) == 0xff0000 && le32(b + 58) == 0x00ff00 && le32(b + 62) == 0x0000ff &&
+            le32(b + 66) == 0xff000000u)
+            compression = 0;
+    }
+    if (planes != 1 || compression != 0) return E_UnsupportedCompression;
+    const uint32_t width = (uint32_t)w, height = (uint32_t)hh;
+    const int allow_alpha = info_len > 40;
+    uint32_t ncol = 0;
+    uint8_t pal[256 * 5];
+    if (bpp == 1 || bpp == 2 || bpp == 4 || bpp == 8) {
+        ncol = le32(b + 46);
+        if (ncol == 0) ncol = 1u << bpp;
+        else if (ncol > (1u << bpp)) return E_UnsupportedPaletteSize;
+        if (pixel_off != 14 + info_len + ncol * 4) return E_UnsupportedColorOffset;
+        BMP_READ((size_t)ncol * 4);
+        for (uint32_t i = 0; i < ncol; i++) { /* B,G,R,pad -> .rgba, A=0xff */
+            pal[5 * i + 0] = b[pos + 4 * i + 2];
+            pal[5 * i + 1] = b[pos + 4 * i + 1];
+            pal[5 * i + 2] = b[pos + 4 * i + 0];
+            pal[5 * i + 3] = 0xff;
+            pal[5 * i + 4] = 0;
+        }
+        pos += (size_t)ncol * 4;
+    } else if (bpp == 24 || bpp == 32) {
+        if (pixel_off != 14 + info_len) return E_UnsupportedColorOffset;
+    } else {
+        return E_UnsupportedBPP;
+    }
+
+    if (ncol) {
+        /* Paletted; an empty image has rect (0,0,0,0) (:163-172) */
+        const int empty = width == 0 || height == 0;
+        out->kind = ZO_PALETTED;
+        out->max_x = empty ? 0 : (int32_t)width;
+        out->max_y = empty ? 0 : (int32_t)height;
+        out->stride = empty ? 0 : width;
+        out->pixels_len = out->stride * (empty ? 0 : height);
+        out->palette = (uint8_t *)calloc(256, 5); /* oracle images carry 256 entries */
+        out->pixels = (uint8_t *)calloc(out->pixels_len ? out->pixels_len : 1, 1);
+        if (!out->palette || !out->pixels) {
+            zo_image_free(out);
+            return E_OutOfMemory;
+        }
+        memcpy(out->palette, pal, ncol * 5);
+        out->palette_len = (int32_t)ncol;
+        if (empty) return 0;
+        const uint32_t ppb = 8 / bpp, mask = (1u << bpp) - 1;
+        const size_t row = ((((size_t)width + ppb - 1) / ppb) + 3) & ~(size_t)3;
+        for (uint32_t r = 0; r < height; r++) {
+            if (len - pos < row) {
+                zo_image_free(out);
+                return E_EndOfStream;
+            }
+            const uint32_t y = top_down ? r : height - 1 - r;
+            uint8_t *p = out->pixels + (size_t)y * out->stride;
+            size_t bi = 0;
+            int bit = 8;
+            for (uint32_t x = 0; x < width; x++) {
+                bit -= (int)bpp;
+                p[x] = (uint8_t)((buf[pos + bi] >> bit) & mask);
+                if (bit == 0) {
+                    bi++;
+                    bit = 8;
+                }
+            }
+            pos += row;
+        }
+        return 0;
+    }
+    out->kind = bpp == 24 ? ZO_RGBA : ZO_NRGBA;
+    out->max_x = (int32_t)width;
+    out->max_y = (int32_t)height;
+    out->stride = (size_t)width * 4;
+    out->pixels_len = out->stride * height;
+    out->pixels = (uint8_t *)calloc(out->pixels_len ? out->pixels_len : 1, 1);
+    if (!out->pixels) return E_OutOfMemory;
+    if (width == 0 || height == 0) return 0;
+    const size_t row = bpp == 24 ? ((size_t)width * 3 + 3) & ~(size_t)3 : (size_t)width * 4;
+    for (uint32_t r = 0; r < height; r++) {
+        if (len - pos < row) {
+            zo_image_free(out);
+            return E_EndOfStream;
+        }
+        const uint32_t y = top_down ? r : height - 1 - r;
+        uint8_t *p = out->pixels + (size_t)y * out->stride;
+        const uint8_t *s = buf + pos;
+        for (uint32_t x = 0; x < width; x++) {
+            if (bpp == 24) {
+                p[4 * x + 0] = s[3 * x + 2];
+                p[4 * x + 1] = s[3 * x + 1];
+                p[4 * x + 2] = s[3 * x + 0];
+                p[4 * x + 3] = 0xff;
+            } else {
+                p[4 * x + 0] = s[4 * x + 2];
+                p[4 * x + 1] = s[4 * x + 1];
+                p[4 * x + 2] = s[4 * x + 0];
+                p[4 * x + 3] = allow_alpha ? s[4 * x + 3] : 0xff;
+            }
+        }
+        pos += row;
+    }
+    return 0;
+#undef BMP_READ
+}
+
+/* ======================================================================== */
+/* QOI                                                                       */
+/* ======================================================================== */
+
+#define QOI_PIXELS_MAX 400000000u
+static unsigned qoi_hash(const uint8_t *px) { return (px[0] * 3u + px[1] * 5u + px[2] * 7u + px[3] * 11u) & 63u; }
+
+/* qoi decodeFromBuffer, src/qoi/decoder.zig:28-130 -> .RGBA image.
+ * DIFF/LUMA steps that leave 0..255 trap in the reference's @intCast
+ * (:97-114, safety-checked builds); here they wrap mod 256 as the QOI
+ * specification (and a ReleaseFast build's truncation) has them.  The
+ * reference's own encoder never emits such steps (encoder.zig:97-101). */
+int zo_qoi_decode(const uint8_t *data, size_t len, zo_image *out)
+{
+    memset(out, 0, sizeof(*out));
+    if (len < 14 + 8) return E_InvalidQoiData;
+    if (be32(data) != 0x716F6966u) return E_InvalidQoiHeader;
+    const uint32_t width = be32(data + 4), height = be32(data + 8);
+    const uint8_t channels = data[12], colorspace = data[13];
+    if (width == 0 || height == 0 || (channels != 3 && channels != 4) || colorspace > 1 ||
+        height >= QOI_PIXELS_MAX / width)
+        return E_InvalidQoiHeader;
+    const size_t n = (size_t)width * height, chunks_len = len - 8;
+    out->kind = ZO_RGBA;
+    out->max_x = (int32_t)width;
+    out->max_y = (int32_t)height;
+    out->stride = (size_t)width * 4;
+    out->pixels_len = n * 4;
+    out->pixels = (uint8_t *)malloc(n * 4);
+    if (!out->pixels) return E_OutOfMemory;
+    uint8_t index[64][4];
+    memset(index, 0, sizeof(index));
+    uint8_t px[4] = {0, 0, 0, 255};
+    size_t p = 14, run = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (run > 0) {
+            run--;
+        } else if (p < chunks_len) {
+            /* payload bytes are read without the chunks_len check (:71-82):
+             * within the 8 padding bytes they are read as they are, past the
+             * end of the buffer the reference's bounds check panics */
+            const uint8_t b1 = data[p++];
+            const size_t need = b1 == 0xfe ? 3 : b1 == 0xff ? 4 : (b1 & 0xc0) == 0x80 ? 1 : 0;
+            if (p + need > len) {
+                zo_image_free(out);
+                return E_Panic;
+            }
+            if (b1 == 0xfe) {
+                px[0] = data[p]; px[1] = data[p + 1]; px[2] = data[p + 2];
+                p += 3;
+            } else if (b1 == 0xff) {
+                px[0] = data[p]; px[1] = data[p + 1]; px[2] = data[p + 2]; px[3] = data[p + 3];
+                p += 4;
+            } else if ((b1 & 0xc0) == 0x00) {
+                memcpy(px, index[b1 & 0x3f], 4);
+            } else if ((b1 & 0xc0) == 0x40) {
+                px[0] = (uint8_t)(px[0] + ((b1 >> 4) & 3) - 2);
+                px[1] = (uint8_t)(px[1] + ((b1 >> 2) & 3) - 2);
+                px[2] = (uint8_t)(px[2] + (b1 & 3) - 2);
+            } else if ((b1 & 0xc0) == 0x80) {
+                const uint8_t b2 = data[p];
+                p += 1;
+                const int dg = (b1 & 0x3f) - 32;
+                px[0] = (uint8_t)(px[0] + dg + ((b2 >> 4) & 0xf) - 8);
+                px[1] = (uint8_t)(px[1] + dg);
+                px[2] = (uint8_t)(px[2] + dg + (b2 & 0xf) - 8);
+            } else {
+                run = b1 & 0x3f;
+            }
+            memcpy(index[qoi_hash(px)], px, 4);
+        }
+        memcpy(out->pixels + 4 * i, px, 4);
+    }
+    return 0;
+}
+
+/* qoi encode, src/qoi/encoder.zig:29-132.  *out is malloc'd; returns 0 or
+ * InvalidQoiHeader. */
+int zo_qoi_encode(const uint8_t *pixels, uint32_t width, uint32_t height, uint8_t channels, uint8_t colorspace,
+                  uint8_t **out, size_t *out_len)
+{
+    *out = NULL;
+    *out_len = 0;
+    if (width == 0 || height == 0 || channels < 3 || channels > 4 || colorspace > 1 ||
+        height >= QOI_PIXELS_MAX / width)
+        return E_InvalidQoiHeader;
+    const size_t px_len = (size_t)width * height * channels;
+    uint8_t *o = (uint8_t *)malloc((size_t)width * height * (channels + 1) + 14 + 8);
+    if (!o) return E_OutOfMemory;
+    size_t n = 0;
+    const uint32_t hdr[3] = {0x716F6966u, width, height};
+    for (int k = 0; k < 3; k++)
+        for (int s = 24; s >= 0; s -= 8) o[n++] = (uint8_t)(hdr[k] >> s);
+    o[n++] = channels;
+    o[n++] = colorspace;
+    uint8_t index[64][4];
+    memset(index, 0, sizeof(index));
+    uint8_t prev[4] = {0, 0, 0, 255}, px[4] = {0, 0, 0, 255};
+    uint32_t run = 0;
+    for (size_t i = 0; i < px_len; i += channels) {
+        px[0] = pixels[i];
+        px[1] = pixels[i + 1];
+        px[2] = pixels[i + 2];
+        if (channels == 4) px[3] = pixels[i + 3];
+        if (!memcmp(px, prev, 4)) {
+            run++;
+            if (run == 62 || i + channels == px_len) {
+                o[n++] = (uint8_t)(0xc0 | (run - 1));
+                run = 0;
+            }
+        } else {
+            if (run > 0) {
+                o[n++] = (uint8_t)(0xc0 | (run - 1));
+                run = 0;
+            }
+            const unsigned h = qoi_hash(px);
+            if (!memcmp(index[h], px, 4)) {
+                o[n++] = (uint8_t)h;
+            } else {
+                memcpy(index[h], px, 4);
+                if (px[3] == prev[3]) {
+                    const int vr = px[0] - prev[0], vg = px[1] - prev[1], vb = px[2] - prev[2];
+                    const int vgr = vr - vg, vgb = vb - vg;
+                    if (vr > -3 && vr < 2 && vg > -3 && vg < 2 && vb > -3 && vb < 2) {
+                        o[n++] = (uint8_t)(0x40 | (vr + 2) << 4 | (vg + 2) << 2 | (vb + 2));
+                    } else if (vgr > -9 && vgr < 8 && vg > -33 && vg < 32 && vgb > -9 && vgb < 8) {
+                        o[n++] = (uint8_t)(0x80 | (vg + 32));
+                        o[n++] = (uint8_t)((vgr + 8) << 4 | (vgb + 8));
+                    } else {
+                        o[n++] = 0xfe;
+                        o[n++] = px[0];
+                        o[n++] = px[1];
+                        o[n++] = px[2];
+                    }
+                } else {
+                    o[n++] = 0xff;
+                    memcpy(o + n, px, 4);
+                    n += 4;
+                }
+            }
+        }
+        memcpy(prev, px, 4);
+    }
+    static const uint8_t pad[8] = {0, 0, 0, 0, 0, 0, 0, 1};
+    memcpy(o + n, pad, 8);
+    n += 8;
+    *out = o;
+    *out_len = n;
+    return 0;
 }

@@ -70,6 +70,14 @@ const char *zo_error_name(int code);
 int zo_jpeg_decode(const uint8_t *buf, size_t len, zo_image *out);
 /* png.decode (src/png/decoder.zig:143-221) over an in-memory buffer. */
 int zo_png_decode(const uint8_t *buf, size_t len, zo_image *out);
+/* bmp.decode (src/bmp/decoder.zig:25-307): .Paletted, .RGBA (24 bpp) or
+ * .NRGBA (32 bpp). */
+int zo_bmp_decode(const uint8_t *buf, size_t len, zo_image *out);
+/* qoi.decode (src/qoi/decoder.zig:28-130): .RGBA. */
+int zo_qoi_decode(const uint8_t *buf, size_t len, zo_image *out);
+/* qoi.encode (src/qoi/encoder.zig:29-132): *out malloc'd, free() it. */
+int zo_qoi_encode(const uint8_t *pixels, uint32_t width, uint32_t height, uint8_t channels,
+                  uint8_t colorspace, uint8_t **out, size_t *out_len);
 /* Image.rgbaPixels (src/image/image.zig:103-130): out has 4*dX*dY bytes. */
 int zo_rgba_pixels(const zo_image *img, uint8_t *out);
 /* Image.at(x,y).toRGBA() (16-bit premultiplied), src/image/image.zig:54-66 */

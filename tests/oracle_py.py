@@ -77,7 +77,7 @@ def lib():
         L = C.CDLL(ORACLE_SO)
         L.zo_error_name.restype = C.c_char_p
         L.zo_error_name.argtypes = [C.c_int]
-        for fn in (L.zo_jpeg_decode, L.zo_png_decode):
+        for fn in (L.zo_jpeg_decode, L.zo_png_decode, L.zo_bmp_decode, L.zo_qoi_decode):
             fn.restype = C.c_int
             fn.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(ZoImage)]
         L.zo_rgba_pixels.restype = C.c_int
@@ -93,6 +93,10 @@ def lib():
             C.c_int32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
             C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
         ]
+        L.zo_qoi_encode.restype = C.c_int
+        L.zo_qoi_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_uint8,
+                                    C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_size_t)]
+        L.free.argtypes = [C.c_void_p]
         L.zo_png_unfilter_seconds.restype = C.c_double
         L.zo_png_unfilter_seconds.argtypes = []
         _lib = L
@@ -196,10 +200,48 @@ def png_decode(data: bytes) -> OImage:
     return _wrap(raw)
 
 
+def bmp_decode(data: bytes) -> OImage:
+    raw = ZoImage()
+    e = lib().zo_bmp_decode(data, len(data), C.byref(raw))
+    if e:
+        raise OracleError(error_name(e))
+    return _wrap(raw)
+
+
+def qoi_decode(data: bytes) -> OImage:
+    raw = ZoImage()
+    e = lib().zo_qoi_decode(data, len(data), C.byref(raw))
+    if e:
+        raise OracleError(error_name(e))
+    return _wrap(raw)
+
+
+def qoi_encode(pixels, width: int, height: int, channels: int, colorspace: int = 0) -> bytes:
+    """qoi.encode (src/qoi/encoder.zig:29-132) through the oracle."""
+    px = np.ascontiguousarray(np.asarray(pixels, np.uint8).reshape(-1))
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_size_t(0)
+    e = lib().zo_qoi_encode(px.ctypes.data if px.size else None, width, height, channels, colorspace,
+                            C.byref(out), C.byref(n))
+    if e:
+        raise OracleError(error_name(e))
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        lib().free(out)
+
+
 def decode(data: bytes) -> OImage:
+    """zpix.fromBuffer (src/root.zig:34-40): PNG, JPEG, QOI, BMP in that order."""
     if data[:8] == b"\x89PNG\r\n\x1a\n":
         return png_decode(data)
-    return jpeg_decode(data)
+    if data[:2] == b"\xff\xd8":
+        return jpeg_decode(data)
+    if data[:4] == b"qoif":
+        return qoi_decode(data)
+    if data[:2] == b"BM":
+        return bmp_decode(data)
+    raise OracleError("UnknownImageFormat")
 
 
 def idct(block) -> np.ndarray:

@@ -394,3 +394,65 @@ def test_inflate_matches_zlib(level, strategy):
         except _lib.ZpixError as e:
             got = e.name
         assert got == want, (k, got, want)
+
+
+def _raw_qoi_decode(data: bytes):
+    import ctypes as C
+
+    from zpix_amd.image import Image
+
+    raw = _lib.zpx_image()
+    code = _lib.lib().zpx_qoi_decode(None, None, data, len(data), C.byref(raw))
+    if code:
+        return _lib.error_name(code), None
+    return "Ok", Image._from_c(raw)
+
+
+def test_qoi_decode_host_matches_oracle():
+    """qoi.decode is a host loop (no context needed): same pixels and errors as the oracle."""
+    import io
+
+    from PIL import Image as PI
+
+    rng = np.random.default_rng(0)
+    for k, (w, h, ch) in enumerate([(1, 1, 4), (5, 3, 3), (64, 17, 4), (130, 40, 3)]):
+        px = np.clip(128 + np.cumsum(rng.integers(-3, 3, (h, w, ch)), axis=1), 0, 255).astype(np.uint8)
+        px[: h // 2, : w // 2] = px[0, 0]
+        b = io.BytesIO()
+        PI.fromarray(px, "RGBA" if ch == 4 else "RGB").save(b, format="QOI")
+        for data in (O.qoi_encode(px, w, h, ch, 0), b.getvalue()):
+            name, img = _raw_qoi_decode(data)
+            want = O.qoi_decode(data)
+            assert name == "Ok" and img.kind == "RGBA" and tuple(img.rect) == want.rect
+            assert np.array_equal(img.pixels, want.pixels)
+            # truncations: header errors, payload past the end (Panic) or a short image
+            for cut in (0, 13, 21, 22, len(data) - 9, len(data) - 1):
+                name, img = _raw_qoi_decode(data[:cut])
+                try:
+                    want = O.qoi_decode(data[:cut])
+                    assert name == "Ok" and np.array_equal(img.pixels, want.pixels), cut
+                except O.OracleError as e:
+                    assert name == e.name, cut
+
+
+def test_bmp_header_errors_match_oracle():
+    """bmp readHeader's errors (src/bmp/decoder.zig:42-158) come from the host
+    parse, before any device work, so they are checked without a GPU."""
+    import ctypes as C
+
+    from tools import synthetic as S
+
+    good, _ = S.bmp_bytes(1, 9, 4, 4, header=108)
+    variants = [b"", b"BM", b"XM" + good[2:], good[:30]]
+    for off, val in [(14, 12), (26, 2), (28, 16), (30, 1), (46, 17), (10, 99), (22, 0x80)]:
+        v = bytearray(good)
+        v[off] = val
+        if off == 22:
+            v[22:26] = (0x80000000).to_bytes(4, "little")
+        variants.append(bytes(v))
+    for data in variants:
+        raw = _lib.zpx_image()
+        code = _lib.lib().zpx_bmp_decode(None, None, data, len(data), C.byref(raw))
+        with pytest.raises(O.OracleError) as e:
+            O.bmp_decode(data)
+        assert _lib.error_name(code) == e.value.name, data[:32]

@@ -2,8 +2,13 @@
 
 - PNG: 35 PngSuite files vs .sng goldens (src/png/decoder_test.zig:8-129),
   bit-exact, with the silent-exit-on-failure bug removed (a load failure fails).
-- PNG Avg filter + rgbaPixels: BMP parity pairs (src/bmp/decoder_test.zig:24-61);
-  Pillow's BMP reader stands in for zpix's bmp decoder (out of scope here).
+- PNG Avg filter + rgbaPixels: BMP parity pairs (src/bmp/decoder_test.zig:24-61),
+  through the oracle's bmp.decode restatement, with Pillow's BMP reader as a
+  second, independent reader of the same .bmp files.
+- QOI (src/qoi/encoder.zig, decoder.zig): the reference holds no QOI fixture,
+  so the restatement is pinned against Pillow's independent QOI codec (the
+  published qoi.h algorithm): identical chunk bytes from the encoder, identical
+  pixels from the decoder.
 - JPEG: baseline == progressive planes for 10 pairs (src/jpeg/decoder.zig:1843-1920),
   assorted decodes (:1922-1940) and the error cases (:1942-2279).
 """
@@ -58,6 +63,77 @@ def test_png_bmp_parity(name):
     img = O.png_decode(read("testdata", name + ".png"))
     rgba = img.rgba_pixels().reshape(img.height, img.width, 4)
     assert np.array_equal(rgba, bmp_rgba_premultiplied(golden("testdata", name + ".bmp")))
+
+
+@pytest.mark.parametrize("name", BMP_PAIRS)
+def test_bmp_decode_parity_with_png(name):
+    """bmp: decode parity with png (src/bmp/decoder_test.zig:24-61)."""
+    b = O.bmp_decode(read("testdata", name + ".bmp"))
+    p = O.png_decode(read("testdata", name + ".png"))
+    assert b.rect == p.rect
+    assert np.array_equal(b.rgba_pixels(), p.rgba_pixels())
+
+
+def test_bmp_empty_input_is_end_of_stream():
+    """bmp: empty input returns eof (src/bmp/decoder_test.zig:63-69)."""
+    with pytest.raises(O.OracleError) as e:
+        O.bmp_decode(b"")
+    assert e.value.name == "EndOfStream"
+
+
+def _qoi_pixels(seed, w, h, ch):
+    rng = np.random.default_rng(seed)
+    # runs, index hits, small diffs, luma diffs and literals all occur
+    base = rng.integers(0, 4, (h, w, ch)) * 63
+    walk = np.cumsum(rng.integers(-2, 2, (h, w, ch)), axis=1)
+    # clipped so no channel step exceeds 207: the reference takes differences
+    # in i16 without wrapping (encoder.zig:97-101) while qoi.h/Pillow wrap them
+    # mod 256, and the two agree whenever no wrapped step is small
+    px = np.where(rng.random((h, w, 1)) < 0.5, base, np.clip(128 + walk, 48, 207)).astype(np.uint8)
+    px[:, : w // 3] = px[:, :1]  # long runs (>62)
+    return px
+
+
+@pytest.mark.parametrize("ch", [3, 4])
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (61, 5), (200, 31)])
+def test_qoi_encode_matches_pillow(shape, ch):
+    from PIL import Image
+    import io
+
+    w, h = shape
+    px = _qoi_pixels(w * h + ch, w, h, ch)
+    ours = O.qoi_encode(px, w, h, ch, 0)
+    buf = io.BytesIO()
+    Image.fromarray(px, "RGBA" if ch == 4 else "RGB").save(buf, format="QOI")
+    theirs = buf.getvalue()
+    assert ours[:13] == theirs[:13] and ours[13] == 0  # Pillow writes colorspace 1
+    assert ours[14:] == theirs[14:]
+    img = O.qoi_decode(ours)
+    assert img.kind == "RGBA" and img.rect == (0, 0, w, h)
+    want = px if ch == 4 else np.concatenate([px, np.full((h, w, 1), 255, np.uint8)], -1)
+    assert np.array_equal(img.pixels.reshape(h, w, 4), want)
+    assert np.array_equal(np.asarray(Image.open(io.BytesIO(ours)).convert("RGBA")), want)
+
+
+def test_qoi_encode_diffs_do_not_wrap():
+    """255 -> 0 is a 4-byte QOI_OP_RGB in the reference (i16 differences,
+    encoder.zig:97-113), not the 1-byte wrapped QOI_OP_DIFF of qoi.h."""
+    px = np.array([[[255, 10, 10, 255], [0, 10, 10, 255]]], np.uint8)
+    out = O.qoi_encode(px, 2, 1, 4)
+    assert out[14:] == bytes([0xFE, 255, 10, 10, 0xFE, 0, 10, 10]) + bytes(7) + b"\x01"
+    assert np.array_equal(O.qoi_decode(out).pixels.reshape(1, 2, 4), px)
+
+
+def test_qoi_errors():
+    with pytest.raises(O.OracleError) as e:
+        O.qoi_encode(np.zeros(4, np.uint8), 0, 1, 4)
+    assert e.value.name == "InvalidQoiHeader"
+    with pytest.raises(O.OracleError) as e:
+        O.qoi_decode(b"qoif" + bytes(10))
+    assert e.value.name == "InvalidQoiData"
+    with pytest.raises(O.OracleError) as e:
+        O.qoi_decode(b"qoix" + bytes(30))
+    assert e.value.name == "InvalidQoiHeader"
 
 
 def _check_blocks(bounds, p0, p1, s0, s1):
@@ -152,3 +228,26 @@ def test_jpeg_vs_png_sanity():
     a = O.jpeg_decode(read("testdata", "video-001.jpeg")).rgba_pixels().astype(int)
     p = O.png_decode(read("testdata", "video-001.png")).rgba_pixels().astype(int)
     assert np.abs(a - p).max() <= 4
+
+
+@pytest.mark.parametrize("bpp", [1, 2, 4, 8, 24, 32])
+@pytest.mark.parametrize("header", [40, 124])
+def test_bmp_synthetic_vs_pillow(bpp, header):
+    """The oracle's bmp.decode on generated files agrees with Pillow's reader
+    (rgbaPixels premultiplies; Pillow keeps straight alpha)."""
+    from PIL import Image
+    import io
+    from tools import synthetic as S
+
+    for w, h, td in [(1, 1, False), (5, 3, True), (67, 9, False)]:
+        data, _ = S.bmp_bytes(w + bpp, w, h, bpp, top_down=td, header=header,
+                              bitfields=header > 40 and bpp == 32)
+        try:
+            ref = np.asarray(Image.open(io.BytesIO(data)).convert("RGBA"))
+        except Exception:
+            pytest.skip(f"Pillow does not read {bpp} bpp")
+        img = O.bmp_decode(data)
+        a = ref[..., 3:4].astype(np.uint32)
+        pm = ((ref[..., :3].astype(np.uint32) * 0x101 * a) // 0xFF) >> 8
+        want = np.concatenate([pm.astype(np.uint8), ref[..., 3:4]], -1)
+        assert np.array_equal(img.rgba_pixels().reshape(h, w, 4), want), (w, h, td)

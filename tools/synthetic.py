@@ -169,3 +169,28 @@ def png_generic(seed: int, w: int, h: int, depth: int, color_type: int, interlac
 
 def png_rgba16_adam7(seed: int, w: int, h: int) -> bytes:
     return png_generic(seed, w, h, 16, 6, interlace=1)
+
+
+def bmp_bytes(seed: int, w: int, h: int, bpp: int, top_down: bool = False, header: int = 40,
+              ncol: int = 0, bitfields: bool = False) -> tuple[bytes, np.ndarray]:
+    """An uncompressed BMP (the layouts src/bmp/decoder.zig:42-307 accepts) with
+    random pixel data; returns (file bytes, raw row data as stored)."""
+    rng = np.random.default_rng(seed)
+    if bpp <= 8:
+        ppb = 8 // bpp
+        row = ((w + ppb - 1) // ppb + 3) & ~3
+        ncol_eff = ncol or (1 << bpp)
+        pal = rng.integers(0, 256, (ncol_eff, 4), dtype=np.uint8).tobytes()
+    else:
+        row = (w * 3 + 3) & ~3 if bpp == 24 else w * 4
+        ncol_eff, pal = 0, b""
+    rows = rng.integers(0, 256, (h, row), dtype=np.uint8)
+    info = bytearray(header)
+    struct.pack_into("<IiiHHI", info, 0, header, w, -h if top_down else h, 1, bpp, 3 if bitfields else 0)
+    struct.pack_into("<I", info, 32, ncol)
+    if header > 40:
+        struct.pack_into("<IIII", info, 40, 0xFF0000, 0x00FF00, 0x0000FF, 0xFF000000)
+    off = 14 + header + len(pal)
+    data = rows.tobytes()
+    fh = b"BM" + struct.pack("<IHHI", off + len(data), 0, 0, off)
+    return fh + bytes(info) + pal + data, rows

@@ -131,6 +131,11 @@ class zpx_batch_stats(C.Structure):
     ]
 
 
+class zpx_qoi_desc(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("channels", C.c_uint8), ("colorspace", C.c_uint8),
+                ("pad", C.c_uint8 * 2)]
+
+
 class zpx_gather_stats(C.Structure):
     _fields_ = [("decode_s", C.c_double), ("gather_s", C.c_double), ("gather_bytes", C.c_double),
                 ("ndev", C.c_int32), ("pad", C.c_int32)]
@@ -148,6 +153,8 @@ EXPORTS = [
     "zpx_png_stream_data", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
     "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config", "zpx_plan_status",
     "zpx_batch_decode_sharded", "zpx_debug_png_stall", "zpx_debug_jpeg_parallel_scans",
+    "zpx_bmp_decode", "zpx_bmp_load", "zpx_bmp_probe_buffer", "zpx_qoi_decode", "zpx_qoi_load",
+    "zpx_qoi_probe_buffer", "zpx_qoi_encode", "zpx_qoi_encode_bound", "zpx_qoi_encode_device",
 ]
 
 _lib = None
@@ -210,6 +217,15 @@ def lib():
                                            C.POINTER(zpx_gather_stats)]),
         "zpx_debug_png_stall": (i32, [vp, C.c_uint32, C.POINTER(C.c_double)]),
         "zpx_debug_jpeg_parallel_scans": (C.c_int64, []),
+        "zpx_bmp_decode": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(zpx_image)]),
+        "zpx_bmp_load": (i32, [vp, vp, C.c_char_p, C.POINTER(zpx_image)]),
+        "zpx_bmp_probe_buffer": (i32, [C.c_char_p, sz]),
+        "zpx_qoi_decode": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(zpx_image)]),
+        "zpx_qoi_load": (i32, [vp, vp, C.c_char_p, C.POINTER(zpx_image)]),
+        "zpx_qoi_probe_buffer": (i32, [C.c_char_p, sz]),
+        "zpx_qoi_encode": (i32, [vp, vp, vp, sz, C.POINTER(zpx_qoi_desc), C.POINTER(u8p), C.POINTER(sz)]),
+        "zpx_qoi_encode_bound": (sz, [C.POINTER(zpx_qoi_desc)]),
+        "zpx_qoi_encode_device": (i32, [vp, vp, C.POINTER(zpx_qoi_desc), vp, sz, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -217,6 +233,11 @@ def lib():
         fn.argtypes = args
     _lib = L
     return L
+
+
+def libc_free(p) -> None:
+    """free() for buffers the library returned from the default (NULL) allocator."""
+    C.CDLL(None).free(C.cast(p, C.c_void_p))
 
 
 def error_name(code: int) -> str:

@@ -17,6 +17,11 @@ struct zpx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string last_error;
+    // grow-only device scratch for stream-ordered work that needs no host
+    // round trip (the QOI encoder's tables and slots); used on `stream` or a
+    // caller stream, one call at a time per context
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
 };
 
 namespace zpx {
@@ -76,6 +81,51 @@ inline void al_free(const zpx_allocator *al, void *p, size_t n)
     if (!p) return;
     if (al && al->free) al->free(al->user, p, n);
     else free(p);
+}
+
+// Runs an entry point's body so that no C++ exception crosses the C-ABI
+// (include/zpix_amd.h: "No exception or abort crosses the ABI").
+template <typename F> int guarded(F &&f) noexcept
+{
+    try {
+        return f();
+    } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+}
+
+inline int read_file(const char *path, std::vector<uint8_t> &out)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) return ZPX_E_FILE_NOT_FOUND;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    if (n < 0) {
+        fclose(f);
+        return ZPX_E_READ_FAILED;
+    }
+    out.resize(static_cast<size_t>(n));
+    size_t got = n ? fread(out.data(), 1, static_cast<size_t>(n), f) : 0;
+    fclose(f);
+    return got == static_cast<size_t>(n) ? 0 : ZPX_E_READ_FAILED;
+}
+
+// ctx->scratch grown to at least n bytes (synchronises the device only when it grows)
+inline hipError_t ctx_scratch(zpx_ctx *ctx, size_t n)
+{
+    if (ctx->scratch && ctx->scratch_bytes >= n) return hipSuccess;
+    if (ctx->scratch) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return e;
+        (void)hipFree(ctx->scratch);
+        ctx->scratch = nullptr;
+        ctx->scratch_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&ctx->scratch, n ? n : 1);
+    if (e == hipSuccess) ctx->scratch_bytes = n;
+    else ctx->scratch = nullptr;
+    return e;
 }
 
 struct CtxScope { // make ctx->device current for this call

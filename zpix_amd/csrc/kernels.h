@@ -50,4 +50,28 @@ int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s)
 int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,
                      uint8_t *out, hipStream_t s);
 
+// bmp_kernels.hip: the pixel loop of bmp.decode over the file's row data
+// (bpp 1/2/4/8 -> palette indices, 24 -> RGBA, 32 -> NRGBA)
+int launch_bmp_rows(int bpp, bool allow_alpha, const uint8_t *src, uint64_t row_bytes, uint8_t *dst,
+                    uint64_t dst_stride, uint32_t width, uint32_t height, int top_down, hipStream_t s);
+
+// qoi_kernels.hip: qoi.encode as a segmented scan (see the file header)
+struct QoiEncodeArgs {
+    const uint8_t *pixels = nullptr; // device, width*height*channels bytes
+    uint64_t n = 0;                  // pixels
+    uint32_t S = 0, nseg = 0, slot_words = 0;
+    uint32_t width = 0, height = 0, colorspace = 0;
+    uint8_t *out = nullptr;          // device, >= qoi bound bytes
+    uint64_t *out_len = nullptr;     // device
+    uint32_t *seg_tbl = nullptr, *seg_run = nullptr, *seg_cnt = nullptr;
+    uint64_t *seg_mask = nullptr;
+    uint32_t *blk_tbl = nullptr, *blk_run = nullptr, *pre_tbl = nullptr, *pre_run = nullptr;
+    uint64_t *blk_mask = nullptr, *blk_cnt = nullptr, *blk_off = nullptr;
+    uint32_t *slots = nullptr;
+};
+// scratch bytes for n pixels in segments of S; with base != nullptr also
+// points a's scratch fields into base
+size_t qoi_scratch_layout(uint64_t n, uint32_t S, QoiEncodeArgs *a, uint8_t *base);
+int launch_qoi_encode(int channels, const QoiEncodeArgs &a, hipStream_t st);
+
 } // namespace zpx

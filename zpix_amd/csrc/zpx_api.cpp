@@ -40,38 +40,6 @@ extern "C" const char *zpx_error_name(int code)
 
 extern "C" const char *zpx_last_error(const zpx_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
-namespace {
-
-// Runs an entry point's body so that no C++ exception crosses the C-ABI
-// (include/zpix_amd.h: "No exception or abort crosses the ABI").
-template <typename F> int guarded(F &&f) noexcept
-{
-    try {
-        return f();
-    } catch (...) {
-        return ZPX_E_OUT_OF_MEMORY;
-    }
-}
-
-int read_file(const char *path, std::vector<uint8_t> &out)
-{
-    FILE *f = fopen(path, "rb");
-    if (!f) return ZPX_E_FILE_NOT_FOUND;
-    fseek(f, 0, SEEK_END);
-    long n = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    if (n < 0) {
-        fclose(f);
-        return ZPX_E_READ_FAILED;
-    }
-    out.resize(static_cast<size_t>(n));
-    size_t got = n ? fread(out.data(), 1, static_cast<size_t>(n), f) : 0;
-    fclose(f);
-    return got == static_cast<size_t>(n) ? 0 : ZPX_E_READ_FAILED;
-}
-
-} // namespace
-
 // ------------------------------------------------------------------ context
 static int zpx_ctx_create_impl(int device, zpx_ctx **out)
 {
@@ -98,6 +66,7 @@ extern "C" void zpx_ctx_destroy(zpx_ctx *ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
     delete ctx;
 }
 
@@ -1093,8 +1062,8 @@ extern "C" int zpx_from_buffer(zpx_ctx *ctx, const zpx_allocator *al, const uint
 {
     if (zpx_png_probe_buffer(buf, len)) return zpx_png_decode(ctx, al, buf, len, out);
     if (zpx_jpeg_probe_buffer(buf, len)) return zpx_jpeg_decode(ctx, al, buf, len, out);
-    if (buf && len >= 4 && memcmp(buf, "qoif", 4) == 0) return ZPX_E_UNSUPPORTED; // QOI: out of scope
-    if (buf && len >= 2 && buf[0] == 'B' && buf[1] == 'M') return ZPX_E_UNSUPPORTED; // BMP: out of scope
+    if (zpx_qoi_probe_buffer(buf, len)) return zpx_qoi_decode(ctx, al, buf, len, out);
+    if (zpx_bmp_probe_buffer(buf, len)) return zpx_bmp_decode(ctx, al, buf, len, out);
     return ZPX_E_UNKNOWN_IMAGE_FORMAT;
 }
 
