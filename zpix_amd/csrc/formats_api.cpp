@@ -217,7 +217,7 @@ uint32_t qoi_segment()
     static const uint32_t seg = [] {
         const char *e = getenv("ZPX_QOI_SEGMENT");
         const long v = e ? strtol(e, nullptr, 10) : 0;
-        return v >= 16 && v <= 4096 ? static_cast<uint32_t>(v) & ~3u : 128u;
+        return v >= 16 && v <= 4096 ? static_cast<uint32_t>(v) & ~15u : 128u; // whole load groups
     }();
     return seg;
 }

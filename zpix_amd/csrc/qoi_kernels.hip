@@ -54,49 +54,55 @@ template <int CH> __device__ __forceinline__ uint32_t load_px(const uint8_t *px,
     }
 }
 
-// four consecutive pixels starting at i (a multiple of 4, all < n)
-template <int CH> __device__ __forceinline__ void load_px4(const uint8_t *px, uint64_t i, uint32_t o[4])
+constexpr int kGroup = 16; // pixels per load group of one lane (64 B of RGBA)
+
+// kGroup consecutive pixels starting at i (16-byte aligned, all < n)
+template <int CH> __device__ __forceinline__ void load_group(const uint8_t *px, uint64_t i, uint32_t o[kGroup])
 {
+    const uint4 *v = reinterpret_cast<const uint4 *>(px + CH * i);
+    uint32_t w[kGroup * CH / 4 + 1];
+#pragma unroll
+    for (int k = 0; k < kGroup * CH / 16; k++) {
+        const uint4 t = v[k];
+        w[4 * k] = t.x;
+        w[4 * k + 1] = t.y;
+        w[4 * k + 2] = t.z;
+        w[4 * k + 3] = t.w;
+    }
     if constexpr (CH == 4) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(px + 4 * i);
-        o[0] = v.x;
-        o[1] = v.y;
-        o[2] = v.z;
-        o[3] = v.w;
+#pragma unroll
+        for (int j = 0; j < kGroup; j++) o[j] = w[j];
     } else {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(px + 3 * i); // 12-byte aligned
-        const uint32_t a = w[0], b = w[1], c = w[2];
-        o[0] = a | kInit;
-        o[1] = (a >> 24 | b << 8) | kInit;
-        o[2] = (b >> 16 | c << 16) | kInit;
-        o[3] = (c >> 8) | kInit;
+        w[kGroup * 3 / 4] = 0;
+#pragma unroll
+        for (int j = 0; j < kGroup; j++)
+            o[j] = (__builtin_amdgcn_alignbyte(w[3 * j / 4 + 1], w[3 * j / 4], (3 * j) % 4) & 0xffffffu) | kInit;
     }
 }
 
-// Calls f(p) for the pixels [start, end) of one lane, four at a time where the
-// buffer alignment allows it, with the next two groups' loads in flight (a
-// lane's work is a serial chain, so the wave cannot hide a load behind other
-// work of its own).  Prefetch addresses are clamped to the lane's last group.
+// Calls f(p, i) for the pixels [start, end) of one lane: whole groups with the
+// next two groups' loads in flight (a lane's work is a serial chain, so the
+// wave cannot hide a load behind other work of its own; a group spans whole
+// 64-byte pieces, so each line is fetched once per lane), then the tail.
+// Prefetch addresses are clamped to the lane's last whole group.
 template <int CH, typename F>
 __device__ __forceinline__ void for_pixels(const uint8_t *px, uint64_t start, uint64_t end, F &&f)
 {
     uint64_t i = start;
-    const bool vec = CH == 4 ? (reinterpret_cast<uintptr_t>(px) & 15) == 0 : (reinterpret_cast<uintptr_t>(px) & 3) == 0;
-    if (vec && start + 4 <= end) {
-        const uint64_t last = end - 4;
-        uint32_t q0[4], q1[4], q2[4];
-        load_px4<CH>(px, i, q0);
-        load_px4<CH>(px, min(i + 4, last), q1);
-        for (; i + 4 <= end; i += 4) {
-            load_px4<CH>(px, min(i + 8, last), q2);
-            f(q0[0], i);
-            f(q0[1], i + 1);
-            f(q0[2], i + 2);
-            f(q0[3], i + 3);
+    const bool vec = (reinterpret_cast<uintptr_t>(px) & 15) == 0 && (start % kGroup) == 0;
+    if (vec && start + kGroup <= end) {
+        const uint64_t last = end - kGroup - (end - start) % kGroup;
+        uint32_t q0[kGroup], q1[kGroup], q2[kGroup];
+        load_group<CH>(px, i, q0);
+        load_group<CH>(px, min(i + kGroup, last), q1);
+        for (; i + kGroup <= end; i += kGroup) {
+            load_group<CH>(px, min(i + 2 * kGroup, last), q2);
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                q0[k] = q1[k];
-                q1[k] = q2[k];
+            for (int j = 0; j < kGroup; j++) f(q0[j], i + j);
+#pragma unroll
+            for (int j = 0; j < kGroup; j++) {
+                q0[j] = q1[j];
+                q1[j] = q2[j];
             }
         }
     }
@@ -205,8 +211,9 @@ __global__ __launch_bounds__(1024) void qoi_block_scan_kernel(uint64_t n, uint32
         const uint64_t m = live ? blk_mask[b] : 0;
         const uint32_t r = live ? blk_run[b] : 1u << 31;
         uint32_t v[64];
+        const uint32_t bl = min(b, nblk - 1); // dead lanes load a live entry, masked out by m = 0
 #pragma unroll
-        for (int h = 0; h < 64; h++) v[h] = live ? blk_tbl[uint64_t(h) * nblk + b] : 0;
+        for (int h = 0; h < 64; h++) v[h] = blk_tbl[uint64_t(h) * nblk + bl];
 #pragma unroll
         for (int h = 0; h < 64; h++) {
             const uint64_t bits = __ballot(m >> h & 1);
@@ -248,8 +255,9 @@ __global__ __launch_bounds__(1024) void qoi_block_scan_kernel(uint64_t n, uint32
         const uint64_t m = live ? blk_mask[b] : 0;
         const uint32_t r = live ? blk_run[b] : 1u << 31;
         uint32_t v[64];
+        const uint32_t bl = min(b, nblk - 1); // dead lanes load a live entry, masked out by m = 0
 #pragma unroll
-        for (int h = 0; h < 64; h++) v[h] = live ? blk_tbl[uint64_t(h) * nblk + b] : 0;
+        for (int h = 0; h < 64; h++) v[h] = blk_tbl[uint64_t(h) * nblk + bl];
         uint32_t next_v = carry_v;
 #pragma unroll
         for (int h = 0; h < 64; h++) {
@@ -280,21 +288,34 @@ __global__ __launch_bounds__(1024) void qoi_block_scan_kernel(uint64_t n, uint32
     }
 }
 
-// byte queue of one lane: < 4 bytes pending in acc between calls
+// Byte queue of one lane: < 4 bytes pending in acc between calls, whole
+// dwords staged in four registers and stored 16 bytes at a time (the slot is
+// 16-byte aligned and has a spare 16 bytes).
 struct ByteOut {
-    uint32_t *slot;
+    uint4 *slot;
     uint32_t words = 0, pend = 0;
     uint64_t acc = 0;
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    __device__ __forceinline__ void push(uint32_t v)
+    {
+        const uint32_t k = words & 3;
+        w0 = k == 0 ? v : w0;
+        w1 = k == 1 ? v : w1;
+        w2 = k == 2 ? v : w2;
+        w3 = k == 3 ? v : w3;
+        words++;
+        if ((words & 3) == 0) slot[(words >> 2) - 1] = make_uint4(w0, w1, w2, w3);
+    }
     __device__ __forceinline__ void put(uint64_t bytes, uint32_t nb)
     {
-        acc |= bytes << (8 * pend);
+        acc |= (bytes & ((uint64_t(1) << (8 * nb)) - 1)) << (8 * pend);
         pend += nb;
         if (pend >= 4) {
-            slot[words++] = uint32_t(acc);
+            push(uint32_t(acc));
             acc >>= 32;
             pend -= 4;
             if (pend >= 4) {
-                slot[words++] = uint32_t(acc);
+                push(uint32_t(acc));
                 acc >>= 32;
                 pend -= 4;
             }
@@ -302,8 +323,10 @@ struct ByteOut {
     }
     __device__ __forceinline__ uint32_t finish()
     {
-        if (pend) slot[words] = uint32_t(acc);
-        return 4 * words + pend;
+        const uint32_t n = 4 * words + pend;
+        if (pend) push(uint32_t(acc));
+        if (words & 3) slot[words >> 2] = make_uint4(w0, w1, w2, w3);
+        return n;
     }
 };
 
@@ -354,7 +377,7 @@ __global__ __launch_bounds__(64) void qoi_encode_kernel(const uint8_t *__restric
     }
     uint32_t run = c % 62;
 
-    ByteOut out{slots + uint64_t(s) * slot_words};
+    ByteOut out{reinterpret_cast<uint4 *>(slots + uint64_t(s) * slot_words)};
     uint32_t prev = start > 0 ? load_px<CH>(px, start - 1) : kInit;
     for_pixels<CH>(px, start, end, [&](uint32_t p, uint64_t i) __attribute__((always_inline)) {
         // encoder.zig:70-124 with selects instead of branches (lanes would
@@ -433,11 +456,11 @@ __global__ __launch_bounds__(1024) void qoi_offsets_kernel(uint32_t nblk, const 
 }
 
 // One workgroup per block: the block's 64 slots are one contiguous run of
-// output bytes at out + 14 + blk_off[b].  Threads stride over the aligned
-// destination dwords; each finds its source segment by binary search over the
-// slot offsets in LDS and gathers 4 bytes (two aligned loads + alignbyte when
-// they come from one slot).  Dwords shared with a neighbouring block are
-// written bytewise.
+// output bytes at out + 14 + blk_off[b].  Each wave copies 16 of the slots:
+// the aligned destination dwords of a slot take two aligned source loads and
+// an alignbyte per lane (256 bytes per wave instruction); the at most 3 + 3
+// bytes at its ends, which share dwords with the neighbouring slots, are
+// stored bytewise.
 __global__ __launch_bounds__(256) void qoi_compact_kernel(uint32_t nseg, uint32_t slot_words,
                                                           const uint32_t *__restrict__ slots,
                                                           const uint32_t *__restrict__ seg_cnt,
@@ -445,7 +468,7 @@ __global__ __launch_bounds__(256) void qoi_compact_kernel(uint32_t nseg, uint32_
                                                           uint8_t *__restrict__ out)
 {
     __shared__ uint32_t offs[65];
-    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t < 64) {
         const uint32_t s = b * 64 + t;
         const uint32_t cnt = s < nseg ? seg_cnt[s] : 0;
@@ -458,43 +481,28 @@ __global__ __launch_bounds__(256) void qoi_compact_kernel(uint32_t nseg, uint32_
         if (t == 0) offs[0] = 0;
     }
     __syncthreads();
-    const uint32_t total = offs[64];
-    if (!total) return;
-    const uint8_t *slot0 = reinterpret_cast<const uint8_t *>(slots + uint64_t(b) * 64 * slot_words);
-    const uint64_t slot_bytes = uint64_t(slot_words) * 4;
-    auto seg_of = [&](uint32_t p) __attribute__((always_inline)) { // first k with offs[k+1] > p
-        uint32_t lo = 0, hi = 63;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (offs[mid + 1] > p) hi = mid;
-            else lo = mid + 1;
-        }
-        return lo;
-    };
-    auto byte_at = [&](uint32_t p) __attribute__((always_inline)) {
-        const uint32_t k = seg_of(p);
-        return slot0[k * slot_bytes + (p - offs[k])];
-    };
-    const uintptr_t d0 = reinterpret_cast<uintptr_t>(out) + 14 + blk_off[b];
-    const uintptr_t q0 = d0 & ~uintptr_t(3), q1 = (d0 + total + 3) & ~uintptr_t(3);
-    for (uintptr_t q = q0 + 4 * uintptr_t(t); q < q1; q += 4 * 256) {
-        if (q >= d0 && q + 4 <= d0 + total) {
-            const uint32_t p = static_cast<uint32_t>(q - d0);
-            const uint32_t k = seg_of(p);
-            uint32_t v;
-            if (p + 4 <= offs[k + 1]) {
-                const uint8_t *src = slot0 + k * slot_bytes + (p - offs[k]);
-                const uint32_t *w = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
-                v = __builtin_amdgcn_alignbyte(w[1], w[0], static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 3));
-            } else {
-                v = byte_at(p) | uint32_t(byte_at(p + 1)) << 8 | uint32_t(byte_at(p + 2)) << 16 |
-                    uint32_t(byte_at(p + 3)) << 24;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(out) + 14 + blk_off[b];
+    for (uint32_t k = w; k < 64; k += 4) {
+        const uint32_t o0 = offs[k], cnt = offs[k + 1] - o0;
+        if (!cnt) continue;
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(slots + uint64_t(b * 64 + k) * slot_words);
+        const uintptr_t d = base + o0, e = d + cnt;
+        const uintptr_t qa = (d + 3) & ~uintptr_t(3), qb = e & ~uintptr_t(3);
+        if (qb > qa) {
+            for (uintptr_t q = qa + 4 * uintptr_t(lane); q < qb; q += 4 * 64) {
+                const uintptr_t sa = reinterpret_cast<uintptr_t>(src) + (q - d);
+                const uint32_t *sw = reinterpret_cast<const uint32_t *>(sa & ~uintptr_t(3));
+                *reinterpret_cast<uint32_t *>(q) = __builtin_amdgcn_alignbyte(sw[1], sw[0], static_cast<uint32_t>(sa & 3));
             }
-            *reinterpret_cast<uint32_t *>(q) = v;
-        } else {
-            for (uint32_t i = 0; i < 4; i++)
-                if (q + i >= d0 && q + i < d0 + total)
-                    *reinterpret_cast<uint8_t *>(q + i) = byte_at(static_cast<uint32_t>(q + i - d0));
+        }
+        // head [d, min(qa, e)) and tail [max(qa, qb), e): at most 3 bytes each
+        const uintptr_t head_end = qa < e ? qa : e, tail_start = qb > qa ? qb : qa;
+        if (lane < 3) {
+            const uintptr_t x = d + lane;
+            if (x < head_end) *reinterpret_cast<uint8_t *>(x) = src[x - d];
+        } else if (lane < 6) {
+            const uintptr_t x = tail_start + (lane - 3);
+            if (x < e && x >= head_end) *reinterpret_cast<uint8_t *>(x) = src[x - d];
         }
     }
 }
@@ -522,7 +530,7 @@ int launch_qoi_t(const QoiEncodeArgs &a, hipStream_t st)
 size_t qoi_scratch_layout(uint64_t n, uint32_t S, QoiEncodeArgs *a, uint8_t *base)
 {
     const uint32_t nseg = static_cast<uint32_t>((n + S - 1) / S), nblk = (nseg + 63) / 64;
-    const uint32_t slot_words = (5 * S + 1 + 3) / 4 + 1;
+    const uint32_t slot_words = ((5 * S + 1 + 3) / 4 + 4 + 3) & ~3u; // 16-byte slots with a spare 16 bytes
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
