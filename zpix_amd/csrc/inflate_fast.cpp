@@ -66,9 +66,29 @@ uint32_t result(Kind k, int s)
     }
 }
 
+// bit-reversed bytes, for the MSB-first codes of an LSB-first stream
+struct Rev8 {
+    uint8_t v[256];
+    constexpr Rev8() : v()
+    {
+        for (int i = 0; i < 256; i++) {
+            int r = 0;
+            for (int k = 0; k < 8; k++) r |= ((i >> k) & 1) << (7 - k);
+            v[i] = static_cast<uint8_t>(r);
+        }
+    }
+};
+constexpr Rev8 kRev8;
+inline uint32_t reverse(uint32_t code, int len)
+{
+    return (uint32_t(kRev8.v[code & 0xff]) << 8 | kRev8.v[(code >> 8) & 0xff]) >> (16 - len);
+}
+
 // Builds a two-level canonical Huffman table (root `root` bits); false on an
 // over-subscribed or incomplete set (zlib allows a lone length-1 distance
-// code: we reject it and let zlib handle that stream).
+// code: we reject it and let zlib handle that stream).  Runs once per
+// dynamic block (~3,000 per 4K image), so it avoids per-call clears: the
+// subtable-size scratch is kept zero between calls.
 bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind)
 {
     uint16_t count[16] = {};
@@ -87,34 +107,35 @@ bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind
         code = static_cast<uint16_t>((code + count[l - 1]) << 1);
         next[l] = code;
     }
-    // codes are stored MSB-first in an LSB-first bit stream: index by the reversed code
     uint16_t rev[320];
-    int len_of[320];
-    uint8_t sub_bits[1 << kLitBits] = {}; // per root index: bits of its subtable
+    static thread_local uint8_t sub_bits[1 << 12]; // zero between calls
+    uint16_t longp[320];
+    int nlong = 0;
     for (int s = 0; s < n; s++) {
         const int l = lens[s];
-        len_of[s] = l;
         if (!l) continue;
-        const uint16_t c = next[l]++;
-        uint32_t r = 0;
-        for (int k = 0; k < l; k++) r |= ((c >> k) & 1u) << (l - 1 - k);
+        const uint32_t r = reverse(next[l]++, l);
         rev[s] = static_cast<uint16_t>(r);
         if (l > root) {
             const uint32_t p = r & ((1u << root) - 1);
+            if (!sub_bits[p]) longp[nlong++] = static_cast<uint16_t>(p);
             if (l - root > sub_bits[p]) sub_bits[p] = static_cast<uint8_t>(l - root);
         }
     }
     const int nroot = 1 << root;
     int used = nroot;
-    for (int p = 0; p < nroot; p++) {
-        if (!sub_bits[p]) continue;
+    bool fits = true;
+    for (int i = 0; i < nlong; i++) {
+        const int p = longp[i];
         const int size = 1 << sub_bits[p];
-        if (used + size > cap) return false;
-        t[p] = kSub | uint32_t(used) << 16 | uint32_t(sub_bits[p]) << 5 | uint32_t(root);
+        if (used + size > cap) fits = false;
+        else t[p] = kSub | uint32_t(used) << 16 | uint32_t(sub_bits[p]) << 5 | uint32_t(root);
         used += size;
     }
+    for (int i = 0; i < nlong; i++) sub_bits[longp[i]] = 0;
+    if (!fits) return false;
     for (int s = 0; s < n; s++) {
-        const int l = len_of[s];
+        const int l = lens[s];
         if (!l) continue;
         const uint32_t r = rev[s];
         if (l <= root) {
