@@ -529,6 +529,12 @@ int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds);
  * parallel in this process (tests: the parallel path ran, not its serial
  * fallback).  Host-only. */
 int64_t zpx_debug_jpeg_parallel_scans(void);
+/* Test hook: decodes a baseline 3-component interleaved JPEG into the sparse
+ * coefficient records the batch pipeline uploads and expands
+ * them on the host into int32 grids (component after component, blocks x 64,
+ * natural order).  Returns the record count, 0 if the frame took grids, or
+ * -(status). */
+int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, int32_t *grids, size_t grid_elems);
 
 #ifdef __cplusplus
 }

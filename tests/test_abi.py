@@ -456,3 +456,45 @@ def test_bmp_header_errors_match_oracle():
         with pytest.raises(O.OracleError) as e:
             O.bmp_decode(data)
         assert _lib.error_name(code) == e.value.name, data[:32]
+
+
+def _sparse_grids(data: bytes):
+    import ctypes as C
+
+    cap = 1 << 22
+    out = np.zeros(cap, np.int32)
+    n = _lib.lib().zpx_debug_jpeg_sparse_grids(data, len(data), out.ctypes.data, cap)
+    return n, out
+
+
+@pytest.mark.parametrize("sub", [0, 1, 2])
+def test_jpeg_sparse_records_match_oracle_grids(sub):
+    """The batch pipeline's sparse coefficient upload: the
+    records a baseline interleaved scan emits, expanded with the device
+    kernel's record -> block mapping, equal the oracle's coefficient grids."""
+    from tools import synthetic as S
+
+    for seed, (w, h) in enumerate([(8, 8), (37, 21), (129, 67), (256, 200)]):
+        data = S.jpeg_subsampled(seed, w, h, sub)
+        n, flat = _sparse_grids(data)
+        assert n > 0, (sub, w, h)
+        c = O.jpeg_coefficients(data)
+        off = 0
+        for i, g in enumerate(c.grids):
+            g = np.asarray(g, np.int32).reshape(-1)
+            assert np.array_equal(flat[off:off + g.size], g), (sub, w, h, i)
+            off += g.size
+
+
+def test_jpeg_sparse_records_fall_back_to_grids():
+    """Progressive, gray, non-interleaved and DRI-parallel frames take grids."""
+    from tools import synthetic as S
+
+    for data in (S.jpeg_progressive_444(1, 64, 48), S.jpeg_gray(2, 40, 40),
+                 read("testdata", "video-001.progressive.jpeg")):
+        n, _ = _sparse_grids(data)
+        assert n == 0
+    # a truncated file reports the reference's error, as the grid decoder does
+    data = S.jpeg_420(3, 64, 64)
+    n, _ = _sparse_grids(data[: len(data) // 2])
+    assert n < 0

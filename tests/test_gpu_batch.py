@@ -212,3 +212,35 @@ def test_plan_status_ok_and_stall_times_out_once():
     # the stall did not poison later launches of other plans
     pb.launch()
     pb.status()
+
+
+def test_batch_sparse_coefficient_upload():
+    """Baseline 3-component JPEGs travel as sparse coefficient records
+    (SURVEY §8(f)1), expanded on the device: bit-exact results and fewer H2D
+    bytes than the dense int8 grids."""
+    bufs = [S.jpeg_420(20 + i, 256 + 8 * i, 192) for i in range(4)] + [S.jpeg_subsampled(30, 200, 120, 0),
+                                                                       S.jpeg_subsampled(31, 96, 64, 1)]
+    res, st = batch.decode_rgba(bufs, host_threads=2, with_stats=True)
+    check_results(bufs, res)
+    dense = 0
+    for data in bufs:
+        c = O.jpeg_coefficients(data)
+        dense += sum(np.asarray(g).size for g in c.grids if g is not None)  # int8 bytes
+    assert 0 < st.h2d_bytes < 0.8 * dense, (st.h2d_bytes, dense)
+
+
+def test_batch_dense_coefficient_upload_subprocess():
+    """ZPX_JPEG_SPARSE=0 keeps the dense-grid upload; same pixels."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path[:0]=['tests','.']\n"
+        "from test_gpu_batch import mixed_buffers, check_results\n"
+        "from zpix_amd import batch\n"
+        "bufs = mixed_buffers(); check_results(bufs, batch.decode_rgba(bufs, host_threads=3)); print('OK')\n"
+    )
+    env = dict(os.environ, ZPX_JPEG_SPARSE="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]

@@ -73,16 +73,27 @@ struct Decoded {
 };
 
 struct Slot {
-    DevBuf din, dout, dimg, ddesc, dctl, dbound;
+    DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid;
     HostBuf hdesc, hstatus; // pinned descriptor staging, PNG status word
     hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
     std::unique_ptr<Decoded> dec;
     bool busy = false;
     bool check_png = false;
     bool failed = false; // the image failed after its slot was bound (status already set)
+    DevJpegSparse sparse_args; // the slot's sparse expand launch (issue_jpeg)
 };
 
 bool host_reserve(HostBuf &b, size_t n) { return b.bytes >= n || b.alloc(n, false); }
+
+// ZPX_JPEG_SPARSE=0 uploads dense coefficient grids instead of records
+bool jpeg_sparse_upload()
+{
+    static const bool on = [] {
+        const char *e = getenv("ZPX_JPEG_SPARSE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 class Pipeline {
   public:
@@ -103,6 +114,7 @@ class Pipeline {
     int setup();
     int issue(Slot &s, bool &sync_done);
     int issue_jpeg(Slot &s, bool &sync_done);
+    int upload_sparse(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f);
     int issue_png(Slot &s);
     int finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32_t W, uint32_t H, hipStream_t producer);
     void retire(Slot &s);
@@ -179,7 +191,8 @@ void Pipeline::worker()
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
             // spare pool threads (fewer images than threads) split restart intervals
-            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, std::max(1, threads_ / std::max(1, n_)));
+            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, std::max(1, threads_ / std::max(1, n_)),
+                                            jpeg_sparse_upload());
         } else if (it.buf && it.len >= 4 && (memcmp(it.buf, "qoif", 4) == 0 || (it.buf[0] == 'B' && it.buf[1] == 'M'))) {
             d->status = ZPX_E_UNSUPPORTED; // QOI / BMP: out of scope (zpx_from_buffer)
         } else {
@@ -253,6 +266,63 @@ int Pipeline::finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32
     return ZPX_OK;
 }
 
+// The records of a sparse frame (JpegSparse): H2D of counts, group offsets
+// and record bytes on the copy stream, device grids sized for the width the
+// values need; the expand kernel is launched on the compute stream once the
+// copy has landed (issue_jpeg).  f's coefficient pointers, width and narrow
+// flag are those of the expanded grids.
+int Pipeline::upload_sparse(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f)
+{
+    const JpegSparse &sp = jc.sparse;
+    int32_t m = 0;
+    int64_t mq = 0;
+    for (int k = 0; k < sp.ns; k++) {
+        const int c = sp.scan_comp[k];
+        m = std::max(m, sp.max_abs[c]);
+        mq = std::max<int64_t>(mq, int64_t(sp.max_abs[c]) * jc.max_q[c]);
+    }
+    const int bits = m > 127 ? 16 : 8;
+    f.coeff_bits = bits;
+    f.narrow = mq <= 16384 ? 1 : 0;
+    const size_t nc = align_up(sp.nrec), ng = align_up(sp.groups_bytes());
+    HIPCHK(ctx_, s.din.reserve(nc + ng + sp.bytes + 16));
+    uint8_t *dc = s.din.as<uint8_t>(), *dg = dc + nc, *dd = dg + ng;
+    HIPCHK(ctx_, hipMemcpyAsync(dc, sp.counts.ptr, sp.nrec, hipMemcpyHostToDevice, h2d_));
+    HIPCHK(ctx_, hipMemcpyAsync(dg, sp.groups.ptr, sp.groups_bytes(), hipMemcpyHostToDevice, h2d_));
+    if (sp.bytes) HIPCHK(ctx_, hipMemcpyAsync(dd, sp.data.ptr, sp.bytes, hipMemcpyHostToDevice, h2d_));
+    h2d_bytes_ += double(sp.nrec + sp.groups_bytes() + sp.bytes);
+    size_t gbytes[4] = {}, total = 0;
+    for (int c = 0; c < jc.n_comp; c++) {
+        gbytes[c] = size_t(jc.mxx) * jc.myy * jc.comp[c].h * jc.comp[c].v * 64 * (bits / 8);
+        total += align_up(gbytes[c]);
+    }
+    HIPCHK(ctx_, s.dgrid.reserve(total));
+    DevJpegSparse &a = s.sparse_args;
+    a = DevJpegSparse{};
+    a.counts = dc;
+    a.groups = reinterpret_cast<const uint32_t *>(dg);
+    a.data = dd;
+    a.nrec = sp.nrec;
+    a.mxx = jc.mxx;
+    a.ns = sp.ns;
+    size_t off = 0;
+    uint8_t *grid[4] = {};
+    for (int c = 0; c < jc.n_comp; c++) {
+        grid[c] = s.dgrid.as<uint8_t>() + off;
+        off += align_up(gbytes[c]);
+        f.coeffs[c] = grid[c];
+    }
+    for (int k = 0; k < sp.ns; k++) {
+        const int c = sp.scan_comp[k];
+        a.h[k] = jc.comp[c].h;
+        a.v[k] = jc.comp[c].v;
+        a.gw[k] = jc.mxx * jc.comp[c].h;
+        a.grid[k] = grid[c];
+        a.bpm += a.h[k] * a.v[k];
+    }
+    return ZPX_OK;
+}
+
 int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
 {
     Decoded &d = *s.dec;
@@ -270,20 +340,26 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
         return ZPX_OK;
     }
     // fused dequant + IDCT + upsample + colour straight into the destination
-    size_t total = 0;
-    for (int c = 0; c < 4; c++) total += f.coeffs[c] ? align_up(cb[c]) : 0;
-    HIPCHK(ctx_, s.din.reserve(total));
-    size_t off = 0;
-    for (int c = 0; c < 4; c++) {
-        if (!f.coeffs[c]) continue;
-        uint8_t *dst = s.din.as<uint8_t>() + off;
-        HIPCHK(ctx_, hipMemcpyAsync(dst, f.coeffs[c], cb[c], hipMemcpyHostToDevice, h2d_));
-        f.coeffs[c] = dst;
-        off += align_up(cb[c]);
-        h2d_bytes_ += double(cb[c]);
+    if (d.jc.sparse.valid) {
+        if (int e = upload_sparse(s, d.jc, f)) return e;
+    } else {
+        size_t total = 0;
+        for (int c = 0; c < 4; c++) total += f.coeffs[c] ? align_up(cb[c]) : 0;
+        HIPCHK(ctx_, s.din.reserve(total));
+        size_t off = 0;
+        for (int c = 0; c < 4; c++) {
+            if (!f.coeffs[c]) continue;
+            uint8_t *dst = s.din.as<uint8_t>() + off;
+            HIPCHK(ctx_, hipMemcpyAsync(dst, f.coeffs[c], cb[c], hipMemcpyHostToDevice, h2d_));
+            f.coeffs[c] = dst;
+            off += align_up(cb[c]);
+            h2d_bytes_ += double(cb[c]);
+        }
     }
     HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
     HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
+    if (d.jc.sparse.valid && launch_jpeg_sparse_expand(s.sparse_args, f.coeff_bits, ctx_->stream))
+        return hip_fail(ctx_, hipGetLastError(), "batch: jpeg sparse expand");
     if (!fused) {
         // planes + colour pass from the coefficients this worker already
         // decoded (no second entropy decode, no host sync): CMYK, Adobe RGB

@@ -129,12 +129,12 @@ void HostBuf::release()
 }
 
 // ---------------------------------------------------------------- CoeffGrid
-bool CoeffGrid::init(size_t blocks)
+bool CoeffGrid::init(size_t blocks, bool zero)
 {
     blocks_ = blocks;
     bits_ = 8;
     max_abs_ = 0;
-    return buf_.alloc(blocks * 64 * sizeof(int8_t), true);
+    return buf_.alloc(blocks * 64 * sizeof(int8_t), zero);
 }
 
 void CoeffGrid::load(size_t blk, int32_t *b) const
@@ -268,6 +268,10 @@ struct Huff { // HuffTable.zig
     int32_t min_codes[16] = {}, max_codes[16] = {}, vals_indices[16] = {};
 };
 
+// internal status: the frame does not fit the sparse records (jpeg_entropy_decode
+// then decodes it again into grids); never returned to a caller
+constexpr int kSparseAbort = 1 << 20;
+
 #define ZTRY(e)                                                                \
     do {                                                                       \
         int e_ = (e);                                                          \
@@ -276,8 +280,9 @@ struct Huff { // HuffTable.zig
 
 class Decoder {
   public:
-    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out, bool config_only = false, int threads = 1)
-        : src_(p), len_(n), o_(out), config_only_(config_only), threads_(threads)
+    Decoder(const uint8_t *p, size_t n, JpegCoeffs &out, bool config_only = false, int threads = 1,
+            bool sparse = false)
+        : src_(p), len_(n), o_(out), config_only_(config_only), threads_(threads), sparse_ok_(sparse)
     {
     }
     int run();
@@ -474,6 +479,29 @@ class Decoder {
             return o.grid[ci].store_sparse(blk, b, pos, n) ? 0 : ZPX_E_OUT_OF_MEMORY;
         }
     };
+    // appends a block's record to o.sparse (see JpegSparse)
+    struct RecordSink {
+        JpegSparse &sp;
+        int put(int ci, size_t, int32_t *b, const uint8_t *pos, int n)
+        {
+            if (sp.bytes + 3 * size_t(n) > sp.cap) return kSparseAbort;
+            uint8_t *d = static_cast<uint8_t *>(sp.data.ptr) + sp.bytes;
+            static_cast<uint8_t *>(sp.counts.ptr)[sp.nrec++] = static_cast<uint8_t>(n);
+            int32_t m = sp.max_abs[ci];
+            for (int i = 0; i < n; i++) {
+                const int32_t v = b[pos[i]];
+                const int32_t a = v < 0 ? -v : v;
+                if (a > 32767 || v == INT32_MIN) return kSparseAbort;
+                m = a > m ? a : m;
+                d[i] = pos[i];
+                d[n + 2 * i] = static_cast<uint8_t>(v);
+                d[n + 2 * i + 1] = static_cast<uint8_t>(v >> 8);
+            }
+            sp.max_abs[ci] = m;
+            sp.bytes += 3 * size_t(n);
+            return 0;
+        }
+    };
     struct FixedSink {
         JpegCoeffs &o;
         int32_t max_abs[4] = {0, 0, 0, 0};
@@ -511,6 +539,7 @@ class Decoder {
     bool config_only_ = false;
     bool interleaved_[4] = {}, noninterleaved_[4] = {};
     int threads_ = 1; // restart-interval-parallel Huffman (baseline scans with DRI)
+    bool sparse_ok_ = false; // emit JpegSparse records for a single interleaved baseline scan
 };
 
 int Decoder::sof(int32_t n)
@@ -762,14 +791,37 @@ int Decoder::sos(int32_t n)
     const int32_t myy = (static_cast<int32_t>(o_.height) + 8 * v0 - 1) / (8 * v0);
     o_.mxx = mxx;
     o_.myy = myy;
+    if (o_.sparse.valid) return kSparseAbort; // a second scan after a record scan: redo with grids
+    const bool records = sparse_ok_ && !seen_sos_ && !o_.progressive && ns == 3 && o_.n_comp == 3 &&
+                         !(threads_ > 1 && restart_interval_ > 0);
     seen_sos_ = true;
+    if (records) {
+        JpegSparse &sp = o_.sparse;
+        int32_t bpm = 0;
+        for (int k = 0; k < ns; k++) bpm += o_.comp[scan[k].id].h * o_.comp[scan[k].id].v;
+        const size_t nrec = size_t(mxx) * size_t(myy) * size_t(bpm);
+        // every coefficient costs at least two bits of entropy-coded data, plus
+        // one DC entry per block; never more than dense int16
+        const size_t bound = std::min(3 * (4 * len_ + nrec), nrec * (64 * 3));
+        if (!sp.counts.alloc(nrec, false) || !sp.data.alloc(bound, false)) return ZPX_E_OUT_OF_MEMORY;
+        sp.cap = bound;
+        sp.nrec = sp.bytes = 0;
+        sp.ns = ns;
+        for (int k = 0; k < ns; k++) sp.scan_comp[k] = scan[k].id;
+        sp.valid = true;
+    }
     // Grids: like progressive_coefficients, allocated for scan[i].id over
-    // i < n_comp (:1269-1282; slots past ns read component 0).
-    for (int i = 0; i < o_.n_comp; i++) {
+    // i < n_comp (:1269-1282; slots past ns read component 0).  A baseline
+    // scan interleaving several components writes every block of every MCU,
+    // so its grids need no clearing.
+    const bool full_cover = !o_.progressive && ns > 1;
+    for (int i = 0; i < o_.n_comp && !records; i++) {
         const int ci = scan[i].id;
         if (!o_.has_grid[ci]) {
             const size_t nb = size_t(mxx) * size_t(myy) * size_t(o_.comp[ci].h * o_.comp[ci].v);
-            if (!o_.grid[ci].init(nb)) return ZPX_E_OUT_OF_MEMORY;
+            bool in_scan = false;
+            for (int k = 0; k < ns; k++) in_scan |= scan[k].id == ci;
+            if (!o_.grid[ci].init(nb, !(full_cover && in_scan))) return ZPX_E_OUT_OF_MEMORY;
             o_.has_grid[ci] = true;
         }
     }
@@ -792,7 +844,7 @@ int Decoder::sos(int32_t n)
     ba_ = bm_ = 0;
     bn_ = 0;
     bool done = false;
-    ZTRY(restart_parallel(sc, done));
+    if (!records) ZTRY(restart_parallel(sc, done));
     if (!done) {
         int32_t mcu_i = 0, block_count = 0;
         uint8_t expected_rst = 0xd0;
@@ -800,10 +852,12 @@ int Decoder::sos(int32_t n)
         int32_t b[64];
         uint8_t nzpos[64];
         memset(b, 0, sizeof(b));
-        SerialSink sink{o_};
+        SerialSink serial{o_};
+        RecordSink rec{o_.sparse};
         for (int32_t my = 0; my < myy; my++) {
             for (int32_t mx = 0; mx < mxx; mx++) {
-                ZTRY(mcu(sc, my, mx, block_count, dc, b, nzpos, sink));
+                ZTRY(records ? mcu(sc, my, mx, block_count, dc, b, nzpos, rec)
+                             : mcu(sc, my, mx, block_count, dc, b, nzpos, serial));
                 mcu_i++;
                 if (restart_interval_ > 0 && mcu_i % restart_interval_ == 0 && mcu_i < mxx * myy) {
                     ZTRY(full(tmp_, 2));
@@ -1115,11 +1169,32 @@ int Decoder::run()
 
 } // namespace
 
-int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads)
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads, bool sparse)
 {
     try { // no exception crosses the ABI
-        Decoder d(buf, len, out, false, threads);
-        if (int e = d.run()) return e;
+        int e;
+        {
+            Decoder d(buf, len, out, false, threads, sparse);
+            e = d.run();
+        }
+        if (e == kSparseAbort) { // records could not hold this frame: grids from the start
+            out = JpegCoeffs{};
+            Decoder d(buf, len, out, false, threads, false);
+            e = d.run();
+        }
+        if (e) return e;
+        if (out.sparse.valid) { // byte offset of every 64th record
+            JpegSparse &sp = out.sparse;
+            if (!sp.groups.alloc(sp.groups_bytes(), false)) return ZPX_E_OUT_OF_MEMORY;
+            const uint8_t *cnt = static_cast<const uint8_t *>(sp.counts.ptr);
+            uint32_t *g = static_cast<uint32_t *>(sp.groups.ptr);
+            size_t off = 0;
+            for (size_t r = 0; r < sp.nrec; r++) {
+                if (r % 64 == 0) g[r / 64] = static_cast<uint32_t>(off);
+                off += 3 * size_t(cnt[r]);
+            }
+            return ZPX_OK;
+        }
         // one width per frame (the kernels take one coefficient type per frame)
         int bits = 8;
         for (int i = 0; i < 4; i++)

@@ -45,7 +45,7 @@ class CoeffGrid {
     // int8 and is widened (copied) the first time a value does not fit.
     // Conforming 8-bit streams never need int32; the bench's q75 frames fit
     // int8, natural photos usually need int16 (iceberg.jpg: max |AC| 157).
-    bool init(size_t blocks);
+    bool init(size_t blocks, bool zero = true); // zero = false: every block will be stored
     int bits() const { return bits_; }
     bool wide() const { return bits_ == 32; }
     size_t blocks() const { return blocks_; }
@@ -74,6 +74,21 @@ class CoeffGrid {
     int32_t max_abs_ = 0;
 };
 
+// Sparse coefficient records: the batch pipeline's H2D form of a baseline
+// interleaved scan.  One record per block in decode (MCU)
+// order -- n natural-order positions (u8), then n values (i16 little endian)
+// -- and a u8 count per record; `groups` holds the byte offset of every 64th
+// record.  Expanded into dense grids on the device (launch_jpeg_sparse_expand).
+struct JpegSparse {
+    bool valid = false;
+    HostBuf counts, data, groups;
+    size_t nrec = 0, bytes = 0, cap = 0;
+    int32_t max_abs[4] = {0, 0, 0, 0};
+    int ns = 0;
+    int scan_comp[4] = {0, 0, 0, 0}; // component of each scan slot (record order within an MCU)
+    size_t groups_bytes() const { return ((nrec + 63) / 64) * sizeof(uint32_t); }
+};
+
 struct JpegCoeffs {
     uint32_t width = 0, height = 0;
     int n_comp = 0;
@@ -88,6 +103,7 @@ struct JpegCoeffs {
     // quant table each component is reconstructed with, natural order
     int32_t qt_natural[4][64] = {};
     int32_t max_q[4] = {0, 0, 0, 0};
+    JpegSparse sparse; // valid: the scan's coefficients are records, not grids
 };
 
 // Decode `buf` into coefficient grids.  Returns ZPX_E_* (ZPX_E_OK on success),
@@ -97,7 +113,10 @@ struct JpegCoeffs {
 // threads > 1: baseline scans with a restart interval decode their restart
 // segments in parallel (identical result; anything irregular falls back to
 // the serial loop).
-int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads = 1);
+// sparse: a baseline frame whose one scan interleaves every component (and is
+// not split by restart intervals over threads) is decoded into out.sparse
+// records instead of grids; anything else decodes into grids as usual.
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads = 1, bool sparse = false);
 // default thread count of the single-image entry points: ZPX_HUFF_THREADS,
 // else min(8, hardware threads)
 int jpeg_huff_threads();

@@ -50,6 +50,18 @@ int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s)
 int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,
                      uint8_t *out, hipStream_t s);
 
+// jpeg_sparse_kernels.hip: JpegSparse records -> dense coefficient grids
+struct DevJpegSparse {
+    const uint8_t *counts = nullptr;   // device: u8 per record
+    const uint32_t *groups = nullptr;  // device: byte offset of every 64th record
+    const uint8_t *data = nullptr;     // device: record bytes
+    uint64_t nrec = 0;
+    int32_t mxx = 0, ns = 0, bpm = 0;  // MCU columns, scan slots, blocks per MCU
+    int32_t h[4] = {}, v[4] = {}, gw[4] = {}; // per scan slot: sampling, grid blocks per row
+    void *grid[4] = {};                // per scan slot: the component's dense grid
+};
+int launch_jpeg_sparse_expand(const DevJpegSparse &a, int coeff_bits, hipStream_t s);
+
 // bmp_kernels.hip: the pixel loop of bmp.decode over the file's row data
 // (bpp 1/2/4/8 -> palette indices, 24 -> RGBA, 32 -> NRGBA)
 int launch_bmp_rows(int bpp, bool allow_alpha, const uint8_t *src, uint64_t row_bytes, uint8_t *dst,

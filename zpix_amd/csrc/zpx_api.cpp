@@ -1162,3 +1162,49 @@ extern "C" int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *se
 }
 
 extern "C" int64_t zpx_debug_jpeg_parallel_scans(void) { return jpeg_parallel_scans(); }
+
+// Test hook for the sparse coefficient records (JpegSparse): decodes `buf` in
+// record mode and expands the records on the host with the mapping of
+// jpeg_sparse_expand_kernel, into int32 grids laid out component after
+// component (blocks x 64, natural order).  Returns the number of records, 0
+// when the frame was decoded into grids instead, or -(error code).
+extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, int32_t *grids, size_t grid_elems)
+{
+    return guarded([&]() -> int64_t {
+        JpegCoeffs c;
+        if (int e = jpeg_entropy_decode(buf, len, c, 1, true)) return -int64_t(e);
+        const JpegSparse &sp = c.sparse;
+        if (!sp.valid) return 0;
+        size_t base[4] = {}, total = 0;
+        for (int i = 0; i < c.n_comp; i++) {
+            base[i] = total;
+            total += size_t(c.mxx) * c.myy * c.comp[i].h * c.comp[i].v * 64;
+        }
+        if (total > grid_elems) return -int64_t(ZPX_E_INVALID_ARGUMENT);
+        memset(grids, 0, total * sizeof(int32_t));
+        int bpm = 0;
+        for (int k = 0; k < sp.ns; k++) bpm += c.comp[sp.scan_comp[k]].h * c.comp[sp.scan_comp[k]].v;
+        const uint8_t *cnt = static_cast<const uint8_t *>(sp.counts.ptr);
+        const uint8_t *data = static_cast<const uint8_t *>(sp.data.ptr);
+        const uint32_t *groups = static_cast<const uint32_t *>(sp.groups.ptr);
+        size_t off = 0;
+        for (size_t r = 0; r < sp.nrec; r++) {
+            if (r % 64 == 0 && groups[r / 64] != off) return -int64_t(ZPX_E_PANIC);
+            const size_t mcu = r / bpm;
+            int t = static_cast<int>(r % bpm), k = 0;
+            while (k + 1 < sp.ns && t >= c.comp[sp.scan_comp[k]].h * c.comp[sp.scan_comp[k]].v) {
+                t -= c.comp[sp.scan_comp[k]].h * c.comp[sp.scan_comp[k]].v;
+                k++;
+            }
+            const int ci = sp.scan_comp[k], h = c.comp[ci].h, v = c.comp[ci].v;
+            const size_t my = mcu / c.mxx, mx = mcu % c.mxx;
+            const size_t bx = h * mx + t % h, by = v * my + t / h;
+            int32_t *blk = grids + base[ci] + (by * size_t(c.mxx * h) + bx) * 64;
+            const uint8_t *d = data + off;
+            const int n = cnt[r];
+            for (int i = 0; i < n; i++) blk[d[i]] = static_cast<int16_t>(d[n + 2 * i] | d[n + 2 * i + 1] << 8);
+            off += 3 * size_t(n);
+        }
+        return off == sp.bytes ? int64_t(sp.nrec) : -int64_t(ZPX_E_PANIC);
+    });
+}
