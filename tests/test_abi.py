@@ -498,3 +498,44 @@ def test_jpeg_sparse_records_fall_back_to_grids():
     data = S.jpeg_420(3, 64, 64)
     n, _ = _sparse_grids(data[: len(data) // 2])
     assert n < 0
+
+
+def _zstream(raw: bytes, level: int, strategy: int = 0, wbits: int = 15) -> bytes:
+    c = zlib.compressobj(level, zlib.DEFLATED, wbits, 8, strategy)
+    return c.compress(raw) + c.flush()
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8])
+def test_parallel_inflate_matches_zlib(threads):
+    """The speculative multi-threaded inflate returns zlib's
+    bytes whenever it accepts a stream; it accepts the usual PNG streams."""
+    import ctypes as C
+
+    rng = np.random.default_rng(threads)
+    noise = (128 + rng.normal(0, 12, 3_000_000)).clip(0, 255).astype(np.uint8).tobytes()
+    smooth = np.repeat(rng.integers(0, 256, 40_000, dtype=np.uint8), 60).tobytes()
+    mixed = b"".join(noise[i:i + 50_000] + smooth[i:i + 70_000] for i in range(0, 2_000_000, 120_000))
+    cases = [(noise, 6, 0), (smooth, 6, 0), (mixed, 9, 0), (mixed, 1, 0), (noise, 6, zlib.Z_FIXED),
+             (mixed, 0, 0), (mixed, 6, zlib.Z_HUFFMAN_ONLY), (mixed, 6, zlib.Z_RLE)]
+    accepted = 0
+    for raw, level, strategy in cases:
+        z = _zstream(raw, level, strategy)
+        for want in (len(raw), len(raw) // 3):
+            out = np.zeros(want + 64, np.uint8)
+            ok = _lib.lib().zpx_debug_inflate_parallel(z, len(z), out.ctypes.data, want, threads)
+            if ok:
+                accepted += 1
+                assert out[:want].tobytes() == raw[:want], (level, strategy, want)
+        # a corrupted stream is never accepted with wrong bytes
+        bad = bytearray(z)
+        bad[len(z) // 2] ^= 0x55
+        out = np.zeros(len(raw) + 64, np.uint8)
+        if _lib.lib().zpx_debug_inflate_parallel(bytes(bad), len(bad), out.ctypes.data, len(raw), threads):
+            # like the serial path, only the bytes the PNG reads are checked (no
+            # Adler-32: the reader stops at the last byte it needs)
+            try:
+                ref = zlib.decompressobj(-15).decompress(bytes(bad[2:]))  # raw DEFLATE, no Adler-32
+            except zlib.error:
+                pytest.fail("accepted a stream whose first bytes zlib rejects")
+            assert len(ref) >= len(raw) and out[:len(raw)].tobytes() == ref[:len(raw)]
+    assert accepted >= 8  # dynamic-block streams decode in parallel

@@ -155,7 +155,7 @@ EXPORTS = [
     "zpx_batch_decode_sharded", "zpx_debug_png_stall", "zpx_debug_jpeg_parallel_scans",
     "zpx_bmp_decode", "zpx_bmp_load", "zpx_bmp_probe_buffer", "zpx_qoi_decode", "zpx_qoi_load",
     "zpx_qoi_probe_buffer", "zpx_qoi_encode", "zpx_qoi_encode_bound", "zpx_qoi_encode_device",
-    "zpx_debug_jpeg_sparse_grids",
+    "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel",
 ]
 
 _lib = None
@@ -228,6 +228,7 @@ def lib():
         "zpx_qoi_encode_bound": (sz, [C.POINTER(zpx_qoi_desc)]),
         "zpx_qoi_encode_device": (i32, [vp, vp, C.POINTER(zpx_qoi_desc), vp, sz, vp, vp]),
         "zpx_debug_jpeg_sparse_grids": (C.c_int64, [C.c_char_p, sz, vp, sz]),
+        "zpx_debug_inflate_parallel": (i32, [C.c_char_p, sz, vp, sz, i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

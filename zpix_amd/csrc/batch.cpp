@@ -187,7 +187,7 @@ void Pipeline::worker()
         const double t0 = now_s();
         if (zpx_png_probe_buffer(it.buf, it.len)) {
             d->fmt = 2;
-            d->status = png_parse(it.buf, it.len, d->ps);
+            d->status = png_parse(it.buf, it.len, d->ps, std::max(1, threads_ / std::max(1, n_)));
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
             // spare pool threads (fewer images than threads) split restart intervals

@@ -19,7 +19,11 @@
 // literal needs an end-of-input or end-of-output check.
 #include "inflate_fast.h"
 
+#include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 namespace zpx {
 namespace {
@@ -186,6 +190,8 @@ struct Bits {
         pos += take;
         cnt += take * 8;
     }
+    // input bit position of the next unconsumed bit
+    inline uint64_t bitpos() const { return uint64_t(pos) * 8 + uint64_t(pad) - uint64_t(cnt); }
     // true once a consumed bit lay past the end of the input
     inline bool overrun() const { return cnt < pad; }
     inline uint32_t peek(int n) const { return static_cast<uint32_t>(buf & ((uint64_t(1) << n) - 1)); }
@@ -214,13 +220,14 @@ inline uint32_t decode(Bits &b, const uint32_t *t, int root)
     return e;
 }
 
-// match copy of n bytes from distance d (d <= bytes already written)
-inline void copy_match(uint8_t *dst, size_t d, size_t n)
+// match copy of n elements from distance d (d <= elements already written)
+template <typename T> inline void copy_match(T *dst, size_t d, size_t n)
 {
-    const uint8_t *src = dst - d;
-    if (d >= 8) {
+    const T *src = dst - d;
+    if (d * sizeof(T) >= 8) {
         size_t k = 0;
-        for (; k + 8 <= n; k += 8) { // with d >= 8 a chunk never reads bytes it writes
+        constexpr size_t kStep = 8 / sizeof(T);
+        for (; k + kStep <= n; k += kStep) { // with d >= 8 bytes a chunk never reads what it writes
             uint64_t w;
             memcpy(&w, src + k, 8);
             memcpy(dst + k, &w, 8);
@@ -231,26 +238,91 @@ inline void copy_match(uint8_t *dst, size_t d, size_t n)
     }
 }
 
-} // namespace
+// Output of one decode run: a fixed buffer (capacity = the bytes wanted) or
+// a growable one (the parallel path's speculative chunks).
+template <typename T> struct Out {
+    T *p = nullptr;
+    size_t o = 0, cap = 0;
+    std::vector<T> *grow = nullptr;
+    bool room(size_t n)
+    {
+        if (o + n <= cap) return true;
+        if (!grow) return false;
+        const size_t nc = std::max(2 * cap, o + n + (size_t(1) << 20));
+        grow->resize(nc);
+        p = grow->data();
+        cap = nc;
+        return true;
+    }
+};
 
-bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced)
+// The dynamic block header (RFC 1951 3.2.7) after BTYPE: both tables.
+bool read_dynamic(Bits &b, uint32_t *lit, uint32_t *dist)
 {
-    *produced = 0;
-    if (in_len < 2) return false;
-    const uint32_t cmf = in[0], flg = in[1];
-    if ((cmf & 15) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) return false;
-    Bits b;
-    b.in = in + 2;
-    b.len = in_len - 2;
-    size_t o = 0;
-    static thread_local uint32_t lit[kLitEntries], dist[kDistEntries];
-    bool last = false;
-    while (!last && o < want) {
+    b.refill();
+    const int hlit = static_cast<int>(b.take(5)) + 257;
+    const int hdist = static_cast<int>(b.take(5)) + 1;
+    const int hclen = static_cast<int>(b.take(4)) + 4;
+    if (hlit > 286 || hdist > 30) return false;
+    static const uint8_t kOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    uint8_t cl[19] = {};
+    for (int i = 0; i < hclen; i++) {
         b.refill();
-        last = b.take(1) != 0;
+        cl[kOrd[i]] = static_cast<uint8_t>(b.take(3));
+    }
+    uint32_t clt[1 << 7];
+    if (!build(clt, 1 << 7, cl, 19, 7, Kind::CodeLen)) return false;
+    uint8_t lens[320];
+    int n = 0;
+    while (n < hlit + hdist) {
+        b.refill();
+        const int sym = static_cast<int>(payload(decode(b, clt, 7)));
+        if (b.overrun()) return false;
+        if (sym < 16) {
+            lens[n++] = static_cast<uint8_t>(sym);
+        } else {
+            int rep;
+            uint8_t v = 0;
+            if (sym == 16) {
+                if (n == 0) return false;
+                v = lens[n - 1];
+                rep = 3 + static_cast<int>(b.take(2));
+            } else if (sym == 17) {
+                rep = 3 + static_cast<int>(b.take(3));
+            } else {
+                rep = 11 + static_cast<int>(b.take(7));
+            }
+            if (n + rep > hlit + hdist) return false;
+            while (rep--) lens[n++] = v;
+        }
+    }
+    if (lens[256] == 0) return false; // no end-of-block code
+    if (!build(lit, kLitEntries, lens, hlit, kLitBits, Kind::LitLen)) return false;
+    if (!build(dist, kDistEntries, lens + hlit, hdist, kDistBits, Kind::Dist)) return false;
+    return !b.overrun();
+}
+
+enum class Run { Want, Final, AtStop, Error };
+
+// Decodes blocks from b's position into out until out.o reaches `want`
+// (Want), the final block ends (Final), or a block header is about to start
+// at bit `stop` (AtStop; nothing of it consumed).  A block header past `stop`
+// sets `overshot` (the caller then moves the stop on).  `floor` is how far
+// back a distance may reach before out.p[0] (the speculative window).
+template <typename T>
+Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &overshot, size_t floor)
+{
+    static thread_local uint32_t lit[kLitEntries], dist[kDistEntries];
+    for (;;) {
+        if (out.o >= want) return Run::Want;
+        const uint64_t at = b.bitpos();
+        if (at == stop) return Run::AtStop;
+        if (at > stop) overshot = true;
+        b.refill();
+        const bool last = b.take(1) != 0;
         const uint32_t type = b.take(2);
         if (type == 0) { // stored
-            if (b.overrun()) return false;
+            if (b.overrun()) return Run::Error;
             b.drop((b.cnt - b.pad) & 7);
             // re-sync the byte position to the bit buffer (whole real bytes
             // still buffered go back to the input)
@@ -260,16 +332,19 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
             b.cnt = 0;
             b.pad = 0;
             b.pos = p;
-            if (p + 4 > b.len) return false;
+            if (p + 4 > b.len) return Run::Error;
             const uint32_t len = b.in[p] | uint32_t(b.in[p + 1]) << 8;
             const uint32_t nlen = b.in[p + 2] | uint32_t(b.in[p + 3]) << 8;
-            if ((len ^ 0xffffu) != nlen) return false;
+            if ((len ^ 0xffffu) != nlen) return Run::Error;
             p += 4;
-            if (p + len > b.len) return false;
-            const size_t n = len < want - o ? len : want - o;
-            memcpy(out + o, b.in + p, n);
-            o += n;
+            if (p + len > b.len) return Run::Error;
+            size_t n = len;
+            if (!out.room(n)) n = std::min<size_t>(n, out.cap - out.o);
+            n = std::min(n, want - out.o);
+            for (size_t k = 0; k < n; k++) out.p[out.o + k] = b.in[p + k];
+            out.o += n;
             b.pos = p + len;
+            if (last) return out.o >= want ? Run::Want : Run::Final;
             continue;
         }
         if (type == 1) { // fixed codes
@@ -279,77 +354,41 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
             for (int i = 256; i < 280; i++) l[i] = 7;
             for (int i = 280; i < 288; i++) l[i] = 8;
             // zlib's fixed table has 288 literal/length symbols (286, 287 invalid when used)
-            if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen)) return false;
+            if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen)) return Run::Error;
             uint8_t d[32];
             for (int i = 0; i < 32; i++) d[i] = 5;
-            if (!build(dist, kDistEntries, d, 32, kDistBits, Kind::Dist)) return false;
+            if (!build(dist, kDistEntries, d, 32, kDistBits, Kind::Dist)) return Run::Error;
         } else if (type == 2) { // dynamic
-            b.refill();
-            const int hlit = static_cast<int>(b.take(5)) + 257;
-            const int hdist = static_cast<int>(b.take(5)) + 1;
-            const int hclen = static_cast<int>(b.take(4)) + 4;
-            if (hlit > 286 || hdist > 30) return false;
-            static const uint8_t kOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-            uint8_t cl[19] = {};
-            for (int i = 0; i < hclen; i++) {
-                b.refill();
-                cl[kOrd[i]] = static_cast<uint8_t>(b.take(3));
-            }
-            static thread_local uint32_t clt[1 << 7];
-            if (!build(clt, 1 << 7, cl, 19, 7, Kind::CodeLen)) return false;
-            uint8_t lens[320];
-            int n = 0;
-            while (n < hlit + hdist) {
-                b.refill();
-                const int sym = static_cast<int>(payload(decode(b, clt, 7)));
-                if (b.overrun()) return false;
-                if (sym < 16) {
-                    lens[n++] = static_cast<uint8_t>(sym);
-                } else {
-                    int rep;
-                    uint8_t v = 0;
-                    if (sym == 16) {
-                        if (n == 0) return false;
-                        v = lens[n - 1];
-                        rep = 3 + static_cast<int>(b.take(2));
-                    } else if (sym == 17) {
-                        rep = 3 + static_cast<int>(b.take(3));
-                    } else {
-                        rep = 11 + static_cast<int>(b.take(7));
-                    }
-                    if (n + rep > hlit + hdist) return false;
-                    while (rep--) lens[n++] = v;
-                }
-            }
-            if (lens[256] == 0) return false; // no end-of-block code
-            if (!build(lit, kLitEntries, lens, hlit, kLitBits, Kind::LitLen)) return false;
-            if (!build(dist, kDistEntries, lens + hlit, hdist, kDistBits, Kind::Dist)) return false;
+            if (!read_dynamic(b, lit, dist)) return Run::Error;
         } else {
-            return false;
+            return Run::Error;
         }
-        if (b.overrun()) return false;
+        if (b.overrun()) return Run::Error;
         // ---- the block's symbols
+        T *o = out.p + out.o;
         for (;;) {
             uint32_t e;
-            if (b.pos + 32 <= b.len && o + 258 + 8 <= want) {
+            size_t done = static_cast<size_t>(o - out.p);
+            if (b.pos + 32 <= b.len && done + 258 + 8 <= want && (done + 258 + 8 <= out.cap || out.room(1 << 16))) {
+                o = out.p + done; // the buffer may have moved
                 // fast zone: real input bytes behind every bit and room for a
                 // whole match -- no end checks per symbol
                 b.refill_fast();
                 e = decode(b, lit, kLitBits);
                 if (e & kLiteral) {
-                    out[o++] = static_cast<uint8_t>(payload(e));
+                    *o++ = static_cast<T>(payload(e));
                     e = decode(b, lit, kLitBits);
                     if (e & kLiteral) {
-                        out[o++] = static_cast<uint8_t>(payload(e));
+                        *o++ = static_cast<T>(payload(e));
                         e = decode(b, lit, kLitBits);
                         if (e & kLiteral) {
-                            out[o++] = static_cast<uint8_t>(payload(e));
+                            *o++ = static_cast<T>(payload(e));
                             continue;
                         }
                     }
                 }
                 if (e & (kEob | kInvalid)) {
-                    if (e & kInvalid) return false;
+                    if (e & kInvalid) return Run::Error;
                     break;
                 }
                 // a length: its extra bits, then the distance (one refill covers
@@ -357,20 +396,23 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
                 b.refill_fast();
                 const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
                 const uint32_t de = decode(b, dist, kDistBits);
-                if (de & kInvalid) return false;
+                if (de & kInvalid) return Run::Error;
                 const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
-                if (d > o) return false; // distance past the start of the output
-                copy_match(out + o, d, len);
+                if (d > size_t(o - out.p) + floor) return Run::Error; // before the start of the output
+                copy_match(o, d, len);
                 o += len;
                 continue;
             }
             // careful path near the end of the input or the output
+            o = out.p + done;
             b.refill();
             e = decode(b, lit, kLitBits);
-            if (b.overrun() || (e & kInvalid)) return false;
+            if (b.overrun() || (e & kInvalid)) return Run::Error;
             if (e & kLiteral) {
-                if (o >= want) break;
-                out[o++] = static_cast<uint8_t>(payload(e));
+                if (done >= want) break;
+                if (!out.room(1)) return Run::Error;
+                out.p[done] = static_cast<T>(payload(e));
+                o = out.p + done + 1;
                 continue;
             }
             if (e & kEob) break;
@@ -378,18 +420,230 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
             const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
             b.refill();
             const uint32_t de = decode(b, dist, kDistBits);
-            if (de & kInvalid) return false;
+            if (de & kInvalid) return Run::Error;
             const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
-            if (b.overrun()) return false;
-            if (d > o) return false;
-            const size_t n = len < want - o ? len : want - o;
-            copy_match(out + o, d, n);
-            o += n;
-            if (o >= want) break;
+            if (b.overrun()) return Run::Error;
+            if (d > done + floor) return Run::Error;
+            size_t n = len < want - done ? len : want - done;
+            if (!out.room(n)) return Run::Error;
+            copy_match(out.p + done, d, n);
+            o = out.p + done + n;
+            if (done + n >= want) break;
         }
+        out.o = static_cast<size_t>(o - out.p);
+        if (out.o >= want) return Run::Want;
+        if (last) return Run::Final;
     }
-    *produced = o;
-    return o >= want; // anything short of the requested bytes: let zlib decide
+}
+
+bool zlib_header_ok(const uint8_t *in, size_t in_len)
+{
+    if (in_len < 2) return false;
+    const uint32_t cmf = in[0], flg = in[1];
+    return (cmf & 15) == 8 && (cmf >> 4) <= 7 && ((cmf << 8) | flg) % 31 == 0 && !(flg & 0x20);
+}
+
+inline Bits bits_at(const uint8_t *in, size_t len, uint64_t bit)
+{
+    Bits b;
+    b.in = in;
+    b.len = len;
+    b.pos = static_cast<size_t>(bit >> 3);
+    b.refill();
+    b.drop(static_cast<int>(bit & 7));
+    return b;
+}
+
+// A dynamic-Huffman block header could start at `bit`: BTYPE 2 and both
+// code sets complete (the speculative chunks' start search).
+bool plausible_block(const uint8_t *in, size_t len, uint64_t bit)
+{
+    const size_t byte = static_cast<size_t>(bit >> 3);
+    if (byte + 2 >= len) return false;
+    const uint32_t w = (in[byte] | uint32_t(in[byte + 1]) << 8 | uint32_t(in[byte + 2]) << 16) >> (bit & 7);
+    if ((w >> 1 & 3) != 2) return false;                  // BTYPE = dynamic
+    if ((w >> 3 & 31) > 29 || (w >> 8 & 31) > 29) return false; // HLIT, HDIST
+    Bits b = bits_at(in, len, bit + 3);
+    static thread_local uint32_t lit[kLitEntries], dist[kDistEntries];
+    return read_dynamic(b, lit, dist);
+}
+
+} // namespace
+
+bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced)
+{
+    *produced = 0;
+    if (!zlib_header_ok(in, in_len)) return false;
+    Bits b = bits_at(in, in_len, 16);
+    Out<uint8_t> o{out, 0, want, nullptr};
+    bool overshot = false;
+    const Run r = decode_blocks(b, o, want, ~uint64_t(0), overshot, 0);
+    *produced = o.o;
+    return r == Run::Want; // anything short of the requested bytes: let zlib decide
+}
+
+// Parallel inflate of one stream (the reference's single call
+// at src/png/decoder.zig:516-518).  DEFLATE blocks are not independent (a
+// match may reach 32 KiB back), so this is speculative, after the two-stage
+// scheme of parallel gzip decoders:
+//   1. the compressed bytes are cut into `threads` ranges; each range after
+//      the first searches forward for a bit position where a dynamic block
+//      header parses with complete code sets;
+//   2. chunk 0 decodes from the stream start into the output, every other
+//      chunk from its candidate into 16-bit symbols behind a 32 KiB window of
+//      markers (value 256 + i = "byte i of the 32 KiB before this chunk"), so
+//      matches that reach before the chunk copy markers.  A chunk stops at a
+//      block header exactly at the next chunk's candidate: landing on it
+//      proves the candidate a real block boundary; passing it moves the stop
+//      to the candidate after (the passed chunk is discarded);
+//   3. the chunks' last 32 KiB resolve in order (each only needs the previous
+//      output's last 32 KiB), then the rest of every chunk in parallel.
+// Anything irregular returns false and the caller runs the serial decoder,
+// so results are the serial path's by construction.
+bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced, int threads)
+{
+    *produced = 0;
+    constexpr size_t kWin = 32768;
+    if (threads < 2 || !zlib_header_ok(in, in_len)) return false;
+    const int T = threads;
+    std::vector<uint64_t> cand(T + 1, ~uint64_t(0));
+    cand[0] = 16;
+    const uint64_t total_bits = uint64_t(in_len) * 8;
+    std::vector<std::thread> pool;
+    // 1. candidate starts
+    auto search = [&](int i) {
+        const uint64_t lo = total_bits * uint64_t(i) / uint64_t(T);
+        const uint64_t hi = total_bits * uint64_t(i + 1) / uint64_t(T);
+        for (uint64_t p = lo; p < hi; p++)
+            if (plausible_block(in, in_len, p)) {
+                cand[i] = p;
+                return;
+            }
+    };
+    for (int i = 1; i < T; i++) pool.emplace_back(search, i);
+    for (auto &t : pool) t.join();
+    pool.clear();
+    // 2. speculative decode, chunk i from cand[i] to the next candidate it lands on
+    struct Chunk {
+        std::vector<uint16_t> sym;
+        size_t n = 0;       // output elements (without the window)
+        int next = -1;      // index of the candidate it landed on (T = the stream end)
+        bool ok = false;
+    };
+    std::vector<Chunk> ch(T);
+    auto run = [&](int i) {
+        Chunk &c = ch[i];
+        if (cand[i] == ~uint64_t(0)) return;
+        Bits b = bits_at(in, in_len, cand[i]);
+        int nx = i + 1;
+        while (nx < T && cand[nx] == ~uint64_t(0)) nx++;
+        if (i == 0) {
+            Out<uint8_t> o{out, 0, want, nullptr};
+            for (;;) {
+                bool over = false;
+                const Run r = decode_blocks(b, o, want, nx < T ? cand[nx] : ~uint64_t(0), over, 0);
+                if (r == Run::AtStop) {
+                    c.ok = true;
+                    c.next = nx;
+                    break;
+                }
+                if (r == Run::Want) {
+                    c.ok = true;
+                    c.next = T;
+                    break;
+                }
+                if (r != Run::Error && over && nx < T) { // passed a false candidate: aim at the next
+                    do nx++;
+                    while (nx < T && cand[nx] == ~uint64_t(0));
+                    continue;
+                }
+                break;
+            }
+            c.n = o.o;
+            return;
+        }
+        // the 32 KiB window of markers, then the chunk's symbols (growable)
+        c.sym.resize(kWin + (size_t(1) << 22));
+        for (size_t k = 0; k < kWin; k++) c.sym[k] = static_cast<uint16_t>(256 + k);
+        Out<uint16_t> o{c.sym.data(), kWin, c.sym.size(), &c.sym};
+        for (;;) {
+            bool over = false;
+            const Run r = decode_blocks(b, o, ~size_t(0) >> 1, nx < T ? cand[nx] : ~uint64_t(0), over, 0);
+            if (r == Run::AtStop) {
+                c.ok = true;
+                c.next = nx;
+                break;
+            }
+            if (r == Run::Final) {
+                c.ok = true;
+                c.next = T;
+                break;
+            }
+            if (r != Run::Error && over && nx < T) {
+                do nx++;
+                while (nx < T && cand[nx] == ~uint64_t(0));
+                continue;
+            }
+            break;
+        }
+        o.o -= kWin;
+        c.n = o.o;
+    };
+    for (int i = 1; i < T; i++) pool.emplace_back(run, i);
+    run(0);
+    for (auto &t : pool) t.join();
+    pool.clear();
+    // the chain of chunks that landed on each other, from chunk 0 to the end
+    std::vector<int> chain;
+    size_t total = 0;
+    for (int i = 0; i < T;) {
+        if (!ch[i].ok) return false;
+        chain.push_back(i);
+        total += ch[i].n;
+        if (ch[i].next >= T) break;
+        i = ch[i].next;
+    }
+    if (ch[chain.back()].next < T) return false;
+    if (total < want) return false;
+    // 3. resolve: offsets, tails in order, then the bulk in parallel
+    std::vector<size_t> off(chain.size());
+    size_t acc = 0;
+    for (size_t k = 0; k < chain.size(); k++) {
+        off[k] = acc;
+        acc += ch[chain[k]].n;
+    }
+    auto resolve = [&](size_t k, size_t from, size_t to) -> bool {
+        const Chunk &c = ch[chain[k]];
+        const size_t base = off[k];
+        if (base < kWin) { // a marker would reach before the stream start
+            for (size_t j = from; j < to; j++)
+                if (c.sym[kWin + j] >= 256 && base + (c.sym[kWin + j] - 256) < kWin) return false;
+        }
+        const uint8_t *win = out + base - kWin; // only dereferenced for markers, which are in range
+        const size_t end = std::min(to, want - std::min(want, base));
+        for (size_t j = from; j < end; j++) {
+            const uint16_t s = c.sym[kWin + j];
+            out[base + j] = s < 256 ? static_cast<uint8_t>(s) : win[s - 256];
+        }
+        return true;
+    };
+    for (size_t k = 1; k < chain.size(); k++) {
+        const size_t n = ch[chain[k]].n;
+        if (off[k] >= want) break;
+        if (!resolve(k, n > kWin ? n - kWin : 0, n)) return false;
+    }
+    std::atomic<bool> bad{false};
+    for (size_t k = 1; k < chain.size(); k++) {
+        const size_t n = ch[chain[k]].n;
+        if (n > kWin && off[k] < want)
+            pool.emplace_back([&, k, n] {
+                if (!resolve(k, 0, n - kWin)) bad = true;
+            });
+    }
+    for (auto &t : pool) t.join();
+    if (bad) return false;
+    *produced = want;
+    return true;
 }
 
 } // namespace zpx

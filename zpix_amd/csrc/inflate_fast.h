@@ -9,4 +9,7 @@
 
 namespace zpx {
 bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced);
+// The same contract, decoded by `threads` threads (speculative chunks; false
+// on anything irregular, the caller then runs the serial decoder).
+bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced, int threads);
 }

@@ -11,7 +11,10 @@
 
 #include <zlib.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 namespace zpx {
@@ -73,7 +76,7 @@ int inflate_zlib(const std::vector<uint8_t> &z, uint8_t *dst, size_t total, size
 
 class Parser {
   public:
-    Parser(const uint8_t *p, size_t n, PngStream &o) : src_(p), len_(n), o_(o) {}
+    Parser(const uint8_t *p, size_t n, PngStream &o, int threads) : src_(p), len_(n), o_(o), threads_(threads) {}
     int run(bool header_only = false);
 
   private:
@@ -122,6 +125,7 @@ class Parser {
     int stage_ = 0; // start, ihdr, plte, trns, idat, iend
     bool have_image_ = false;
     PngStream &o_;
+    int threads_ = 1; // inflate threads (inflate_parallel)
 };
 
 int Parser::ihdr(uint32_t len)
@@ -262,7 +266,11 @@ int Parser::decode_image(const std::vector<uint8_t> &z)
     uint8_t *dst = static_cast<uint8_t *>(o_.data.ptr);
     size_t produced = 0;
     bool data_error = false;
-    if (!inflate_fast(z.data(), z.size(), dst, total, &produced)) {
+    // several threads for a large stream (speculative chunks, identical
+    // bytes), else / on anything irregular the serial fast decoder
+    const bool par = threads_ > 1 && total >= (size_t(4) << 20) &&
+                     inflate_parallel(z.data(), z.size(), dst, total, &produced, threads_);
+    if (!par && !inflate_fast(z.data(), z.size(), dst, total, &produced)) {
         produced = 0;
         if (int e = inflate_zlib(z, dst, total, produced, data_error)) return e;
     }
@@ -409,10 +417,20 @@ int Parser::run(bool header_only)
 
 } // namespace
 
-int png_parse(const uint8_t *buf, size_t len, PngStream &out)
+int png_inflate_threads()
+{
+    static const int n = [] {
+        if (const char *e = getenv("ZPX_INFLATE_THREADS")) return std::max(1, atoi(e));
+        const unsigned hw = std::thread::hardware_concurrency();
+        return static_cast<int>(std::min(8u, hw ? hw : 1u));
+    }();
+    return n;
+}
+
+int png_parse(const uint8_t *buf, size_t len, PngStream &out, int threads)
 {
     try { // no exception crosses the ABI (std::bad_alloc on a huge stream)
-        Parser p(buf, len, out);
+        Parser p(buf, len, out, threads);
         return p.run();
     } catch (...) {
         return ZPX_E_OUT_OF_MEMORY;
@@ -422,7 +440,7 @@ int png_parse(const uint8_t *buf, size_t len, PngStream &out)
 int png_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h)
 {
     PngStream s;
-    Parser p(buf, len, s);
+    Parser p(buf, len, s, 1);
     if (int e = p.run(true)) return e;
     w = s.width;
     h = s.height;

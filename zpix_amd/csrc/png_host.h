@@ -39,7 +39,11 @@ struct PngStream {
 // byte is valid; otherwise returns the reference's error for the first row
 // that would fail (EndOfStream / ReadFailed / InvalidFilterType) or the
 // chunk-level error.
-int png_parse(const uint8_t *buf, size_t len, PngStream &out);
+// threads > 1: a large stream inflates on that many threads (inflate_parallel)
+int png_parse(const uint8_t *buf, size_t len, PngStream &out, int threads = 1);
+// default inflate threads of the single-image entry points: ZPX_INFLATE_THREADS,
+// else min(8, hardware threads)
+int png_inflate_threads();
 
 // Signature + IHDR only (dimensions of the image png.decode would return).
 int png_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h);

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "api_internal.h"
+#include "inflate_fast.h"
 #include "device_types.h"
 #include "jpeg_host.h"
 #include "kernels.h"
@@ -689,7 +690,7 @@ static int zpx_png_inflate_impl(const uint8_t *buf, size_t len, zpx_png_stream *
     if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
     std::unique_ptr<zpx_png_stream> s(new zpx_png_stream);
-    if (int e = png_parse(buf, len, s->s)) return e;
+    if (int e = png_parse(buf, len, s->s, png_inflate_threads())) return e;
     *out = s.release();
     return ZPX_OK;
 }
@@ -919,7 +920,7 @@ static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint
     memset(out, 0, sizeof(*out));
     CtxScope s(ctx);
     PngStream ps;
-    if (int e = png_parse(buf, len, ps)) return e;
+    if (int e = png_parse(buf, len, ps, png_inflate_threads())) return e;
     const size_t out_len = size_t(ps.width) * ps.height * ps.out_bpp;
     DevBuf din, dout, dmax;
     HIPCHK(ctx, din.alloc(ps.data_len + ZPX_PNG_INPUT_PAD));
@@ -1206,5 +1207,16 @@ extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, i
             off += 3 * size_t(n);
         }
         return off == sp.bytes ? int64_t(sp.nrec) : -int64_t(ZPX_E_PANIC);
+    });
+}
+
+// Test hook for the speculative parallel inflate (inflate_parallel): 1 when it
+// decoded the first `want` bytes of the zlib stream `z` on `threads` threads,
+// 0 when it declined (the PNG path then decodes serially).
+extern "C" int zpx_debug_inflate_parallel(const uint8_t *z, size_t len, uint8_t *out, size_t want, int threads)
+{
+    return guarded([&] {
+        size_t produced = 0;
+        return inflate_parallel(z, len, out, want, &produced, threads) && produced == want ? 1 : 0;
     });
 }
