@@ -185,14 +185,16 @@ void Pipeline::worker()
         d->item = i;
         const zpx_batch_item &it = items_[i];
         const double t0 = now_s();
+        // threads this item may use: one while enough items remain to keep
+        // every worker busy; the batch's last items split the workers that
+        // are about to go idle (parallel inflate, restart-interval Huffman)
+        const int sub = std::max(1, threads_ / std::max(1, n_ - i));
         if (zpx_png_probe_buffer(it.buf, it.len)) {
             d->fmt = 2;
-            d->status = png_parse(it.buf, it.len, d->ps, std::max(1, threads_ / std::max(1, n_)));
+            d->status = png_parse(it.buf, it.len, d->ps, sub);
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
-            // spare pool threads (fewer images than threads) split restart intervals
-            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, std::max(1, threads_ / std::max(1, n_)),
-                                            jpeg_sparse_upload());
+            d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, sub, jpeg_sparse_upload());
         } else if (it.buf && it.len >= 4 && (memcmp(it.buf, "qoif", 4) == 0 || (it.buf[0] == 'B' && it.buf[1] == 'M'))) {
             d->status = ZPX_E_UNSUPPORTED; // QOI / BMP: out of scope (zpx_from_buffer)
         } else {
