@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=16.0, help="bound on the CPU baseline samples (JPEG + PNG)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the RCCL gather of the end-to-end batch's RGBA to rank 0")
+    ap.add_argument("--no-adam7", action="store_true", help="configs[4]: progressive JPEG line only (A/B runs)")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
     ap.add_argument("--no-e2e", action="store_true",
@@ -272,6 +273,8 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         "host_entropy_mpix_s": round(W * H / t_ent / 1e6, 1),
         "config": {"workload": f"{args.images}x {W}x{H} progressive 4:4:4 JPEG -> RGBA, configs[4]"}}
     del jb
+    if args.no_adam7:
+        return out
     pd = S.png_rgba16_adam7(2000 + rank, W, H)
     t0 = time.perf_counter()
     st = png.Stream(pd)

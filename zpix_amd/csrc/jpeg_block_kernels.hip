@@ -78,6 +78,12 @@ __device__ __forceinline__ void wave_lds_sync()
 #define ZPX_JPEGB_STORE_AUX 2 // cache policy of the RGBA stores (2 = nt; whole lines per instruction)
 #endif
 
+// Samples stay in the signed domain (sample - 128, the IDCT's clamp range
+// before its level shift): the +128 costs nothing folded into the colour
+// constants (luma) or a per-dword xor (packed bytes), instead of an add per
+// sample.
+constexpr uint32_t kBias4 = 0x80808080u; // four samples of value 0
+
 // The wave's LDS image of one pass's coefficients: 64 blocks as 16-byte
 // pieces (P per block: 4 int8, 8 int16).  DMA instruction k (of P) covers
 // blocks B*k .. B*k+B-1 (B = 64 / P; 1 KiB of the grid when the blocks are
@@ -165,37 +171,49 @@ __device__ __forceinline__ void idct_block(int32_t s[64])
         int32_t t[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
-        idct_col_clamp<NARROW>(t);
+        idct_col_clamp<NARROW, true>(t);
 #pragma unroll
         for (int i = 0; i < 8; i++) s[8 * i + c] = t[i];
     }
 }
 
-// four samples (0..255) -> one dword of bytes
+// four signed samples (-128..127) -> one dword of their low bytes (the
+// signed domain: xor kBias4 gives the samples' bytes)
 __device__ __forceinline__ uint32_t pack4(const int32_t *v)
 {
-    return static_cast<uint32_t>(v[0]) | static_cast<uint32_t>(v[1]) << 8 | static_cast<uint32_t>(v[2]) << 16 |
-           static_cast<uint32_t>(v[3]) << 24;
+    const uint32_t lo = __builtin_amdgcn_perm(static_cast<uint32_t>(v[1]), static_cast<uint32_t>(v[0]), 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm(static_cast<uint32_t>(v[3]), static_cast<uint32_t>(v[2]), 0x0c0c0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
-// The chroma terms of color.zig:95-106 for one (Cb, Cr) sample.
+// signed byte u (0..3) of a dword of packed signed samples
+__device__ __forceinline__ int32_t sbyte(uint32_t w, int u) { return static_cast<int32_t>(w << (24 - 8 * u)) >> 24; }
+
+// The chroma terms of color.zig:95-106 for one (Cb, Cr) sample, given as
+// cb1 = Cb - 128, cr1 = Cr - 128 (the signed domain), each with the luma
+// level shift 128 * 0x10101 folded in (so a pixel is mad24(Y - 128, 0x10101, t)).
 struct ChromaTerms {
     int32_t r, g, b;
 };
-__device__ __forceinline__ ChromaTerms chroma_terms(uint32_t cb, uint32_t cr)
+__device__ __forceinline__ ChromaTerms chroma_terms(int32_t cb1, int32_t cr1)
 {
-    const int32_t cb1 = static_cast<int32_t>(cb) - 128, cr1 = static_cast<int32_t>(cr) - 128;
-    return ChromaTerms{__mul24(91881, cr1), -(__mul24(22554, cb1) + __mul24(46802, cr1)), __mul24(116130, cb1)};
+    constexpr int32_t kY = 128 * 0x10101;
+    return ChromaTerms{__mul24(91881, cr1) + kY, kY - (__mul24(22554, cb1) + __mul24(46802, cr1)),
+                       __mul24(116130, cb1) + kY};
 }
 
-// One RGBA pixel (see P3b of jpeg_rgba_kernel for the clamp form).
+// One RGBA pixel from a signed-domain luma sample (see P3b of
+// jpeg_rgba_kernel for the clamp form); cb/cr are the signed-domain chroma
+// samples (RGB frames only).
 template <int COLOR>
-__device__ __forceinline__ uint32_t rgba_pixel(int32_t Yv, uint32_t cb, uint32_t cr, ChromaTerms t)
+__device__ __forceinline__ uint32_t rgba_pixel(int32_t Yv, int32_t cb, int32_t cr, ChromaTerms t)
 {
     if constexpr (COLOR == ZPX_JPEG_COLOR_GRAY) {
-        return static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
+        return static_cast<uint32_t>(__mul24(Yv, 0x010101) + 128 * 0x010101) | 0xff000000u;
     } else if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
-        return static_cast<uint32_t>(Yv) | cb << 8 | cr << 16 | 0xff000000u;
+        const uint32_t rgb = __builtin_amdgcn_perm(static_cast<uint32_t>(cr), __builtin_amdgcn_perm(static_cast<uint32_t>(cb),
+                                                   static_cast<uint32_t>(Yv), 0x0c0c0400u), 0x0c040100u);
+        return (rgb ^ 0x808080u) | 0xff000000u;
     } else {
         const int32_t r = __mul24(Yv, 0x10101) + t.r;
         const int32_t g = __mul24(Yv, 0x10101) + t.g;
@@ -453,29 +471,29 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 // chroma block -> tile (never-scanned component: samples 0)
                 const PassBlock b = pass_block(P, lane);
                 const bool present = (b.comp == 1 ? ts.g[1] : ts.g[2]) != nullptr;
-                const uint32_t pm = present ? 0xffffffffu : 0u;
                 uint8_t *t = &ctile[b.comp - 1][(b.cy * 8) * CPX + b.cx * 8];
                 if (b.ok) {
 #pragma unroll
                     for (int r = 0; r < 8; r++)
-                        *reinterpret_cast<u32x2 *>(t + r * CPX) = u32x2{pack4(s + 8 * r) & pm, pack4(s + 8 * r + 4) & pm};
+                        *reinterpret_cast<u32x2 *>(t + r * CPX) =
+                            present ? u32x2{pack4(s + 8 * r), pack4(s + 8 * r + 4)} : u32x2{kBias4, kBias4};
                 }
                 if constexpr (p == CP - 1) wave_lds_sync(); // tile complete before the luma passes
             } else if constexpr (kind(p) >= 2) {
                 // chroma block kept in this lane: 8 rows x 8 bytes
-                const uint32_t pm = ts.g[kind(p) - 1] != nullptr ? 0xffffffffu : 0u;
+                const bool present = ts.g[kind(p) - 1] != nullptr;
                 uint32_t *dst = kind(p) == 2 ? cbr : crr;
 #pragma unroll
                 for (int r = 0; r < 8; r++) {
-                    dst[2 * r] = pack4(s + 8 * r) & pm;
-                    dst[2 * r + 1] = pack4(s + 8 * r + 4) & pm;
+                    dst[2 * r] = present ? pack4(s + 8 * r) : kBias4;
+                    dst[2 * r + 1] = present ? pack4(s + 8 * r + 4) : kBias4;
                 }
             } else {
                 // luma block -> 8 rows of 8 RGBA pixels
                 constexpr int yr = yrow(p);
                 if (!y_present) { // never-scanned luma: samples 0
 #pragma unroll
-                    for (int i = 0; i < 64; i++) s[i] = 0;
+                    for (int i = 0; i < 64; i++) s[i] = -128;
                 }
                 uint32_t cs[kGray ? 1 : (NS + 3) / 4][2]; // this chroma row's samples, Cb / Cr
                 ChromaTerms ct[kGray ? 1 : NS];
@@ -510,8 +528,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                             if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) {
 #pragma unroll
                                 for (int u = 0; u < NS; u++)
-                                    ct[u] = chroma_terms((cs[u >> 2][0] >> (8 * (u & 3))) & 0xff,
-                                                         (cs[u >> 2][1] >> (8 * (u & 3))) & 0xff);
+                                    ct[u] = chroma_terms(sbyte(cs[u >> 2][0], u & 3), sbyte(cs[u >> 2][1], u & 3));
                             }
                         }
                     }
@@ -519,11 +536,11 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 #pragma unroll
                     for (int x = 0; x < 8; x++) {
                         const int u = x / RX;
-                        uint32_t cb = 0, cr = 0;
+                        int32_t cb = 0, cr = 0;
                         ChromaTerms t{0, 0, 0};
                         if constexpr (!kGray) {
-                            cb = (cs[u >> 2][0] >> (8 * (u & 3))) & 0xff;
-                            cr = (cs[u >> 2][1] >> (8 * (u & 3))) & 0xff;
+                            cb = sbyte(cs[u >> 2][0], u & 3);
+                            cr = sbyte(cs[u >> 2][1], u & 3);
                             if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) t = ct[u];
                         }
 #ifndef ZPX_JPEGB_TIMING_NO_COLOR

@@ -90,7 +90,10 @@ __device__ __forceinline__ void idct_row(int32_t s[8])
 
 // Vertical 1-D IDCT of one column (idct.zig:148-200) + level shift and clamp
 // (decoder.zig:1622-1628): c<-128 -> 0, c>127 -> 255, else c+128.
-template <bool NARROW>
+// SIGNED_OUT leaves the level shift out: the sample minus 128, clamp(c, -128,
+// 127), one instruction less per sample (callers fold the +128 into their
+// colour constants, or into a per-dword xor 0x80 of packed bytes).
+template <bool NARROW, bool SIGNED_OUT = false>
 __device__ __forceinline__ void idct_col_clamp(int32_t s[8])
 {
     int32_t y0 = shl(s[0], 8) + 8192, y1 = shl(s[4], 8), y2 = s[6], y3 = s[2];
@@ -125,7 +128,7 @@ __device__ __forceinline__ void idct_col_clamp(int32_t s[8])
     s[6] = (y3 - y2) >> 14;
     s[7] = (y7 - y1) >> 14;
 #pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = min(max(s[i], -128), 127) + 128;
+    for (int i = 0; i < 8; i++) s[i] = min(max(s[i], -128), 127) + (SIGNED_OUT ? 0 : 128);
 }
 
 
