@@ -6,6 +6,9 @@
 //   mode 1 "linear": per task 12 KiB read and 32 KiB written, both contiguous
 //   mode 2 "write":  mode 0's stores only
 //   mode 3 "task4k": tasks twice as wide (4 KiB row segments, 8 output rows)
+//   mode 4 "spread": mode 0 with VALU work (argv[5] x 64 multiply-adds)
+//                    before each row's two stores
+//   mode 5 "burst":  mode 4's VALU work, then all 32 stores together
 // Usage: mem_pattern <mode> <waves_per_cu> <nt 0|1> [xcd_remap 0|1]
 #include <hip/hip_runtime.h>
 
@@ -20,7 +23,7 @@ constexpr size_t kRgba = size_t(kW) * kH * 4, kYGrid = size_t(kW) * kH, kCGrid =
 
 template <int MODE, int NT>
 __global__ __launch_bounds__(64) void pattern(const unsigned char *__restrict__ coef, unsigned char *__restrict__ out,
-                                               int total_tasks, unsigned sink_mask, int remap)
+                                               int total_tasks, unsigned sink_mask, int remap, int work)
 {
     const int lane = threadIdx.x;
     int t0 = blockIdx.x;
@@ -32,7 +35,7 @@ __global__ __launch_bounds__(64) void pattern(const unsigned char *__restrict__ 
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7ffffff0, 0x00020000);
     u32x4 acc = {0, 0, 0, 0};
     for (int t = t0; t < total_tasks; t += gridDim.x) {
-        if constexpr (MODE == 0 || MODE == 2 || MODE == 3) {
+        if constexpr (MODE == 0 || MODE == 2 || MODE == 3 || MODE == 4 || MODE == 5) {
             constexpr int TW = MODE == 3 ? 2 : 1;          // task width in 2 KiB row segments
             constexpr int ROWS = MODE == 3 ? 8 : 16;       // output rows per task
             const int tasks_x = 8 / TW, per_frame = tasks_x * (kH / ROWS);
@@ -59,12 +62,30 @@ __global__ __launch_bounds__(64) void pattern(const unsigned char *__restrict__ 
             const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(
                 (uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(ob >> 32)) << 32 | (unsigned)__builtin_amdgcn_readfirstlane((unsigned)ob)),
                 0, 0x7ffffff0, 0x00020000);
-            const u32x4 v = acc & sink_mask;
+            u32x4 v = acc & sink_mask;
+            auto burn = [&]() {
+                // `work` x 64 independent multiply-adds (four chains), ~the fused kernel's VALU per row
+                unsigned a0 = v[0] | 1, a1 = v[1] | 3, a2 = v[2] | 5, a3 = v[3] | 7;
+                for (int i = 0; i < work; i++) {
 #pragma unroll
-            for (int rr = 0; rr < ROWS; rr++)
+                    for (int k = 0; k < 16; k++) {
+                        a0 = __mul24(a0, 0x10101) + a1;
+                        a1 = __mul24(a1, 0x10101) + a2;
+                        a2 = __mul24(a2, 0x10101) + a3;
+                        a3 = __mul24(a3, 0x10101) + a0;
+                    }
+                }
+                v[0] ^= (a0 ^ a1 ^ a2 ^ a3) & sink_mask;
+            };
+            if constexpr (MODE == 5)
+                for (int rr = 0; rr < ROWS; rr++) burn();
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++) {
+                if constexpr (MODE == 4) burn();
 #pragma unroll
                 for (int h = 0; h < 2 * TW; h++)
                     __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, rr * kW * 4 + h * 1024 + 16 * lane, 0, NT ? 2 : 0);
+            }
         } else {
             const unsigned char *c = coef + size_t(t) * 12288;
 #pragma unroll
@@ -92,15 +113,15 @@ __global__ __launch_bounds__(64) void pattern(const unsigned char *__restrict__ 
     } while (0)
 
 template <int MODE, int NT>
-void launch(int grid, const unsigned char *c, unsigned char *o, int tasks, int remap)
+void launch(int grid, const unsigned char *c, unsigned char *o, int tasks, int remap, int work)
 {
-    hipLaunchKernelGGL((pattern<MODE, NT>), dim3(grid), dim3(64), 0, 0, c, o, tasks, 0u, remap);
+    hipLaunchKernelGGL((pattern<MODE, NT>), dim3(grid), dim3(64), 0, 0, c, o, tasks, 0u, remap, work);
 }
 
 int main(int argc, char **argv)
 {
     const int mode = argc > 1 ? atoi(argv[1]) : 0, wpc = argc > 2 ? atoi(argv[2]) : 12, nt = argc > 3 ? atoi(argv[3]) : 1;
-    const int remap = argc > 4 ? atoi(argv[4]) : 0;
+    const int remap = argc > 4 ? atoi(argv[4]) : 0, work = argc > 5 ? atoi(argv[5]) : 4;
     const size_t cbytes = size_t(kFrames) * (kYGrid + 2 * kCGrid), obytes = size_t(kFrames) * kRgba;
     unsigned char *c = nullptr, *o = nullptr;
     CK(hipMalloc(&c, cbytes));
@@ -112,14 +133,18 @@ int main(int argc, char **argv)
     const int grid = cus * wpc;
     auto run = [&]() {
         switch (mode * 2 + (nt ? 1 : 0)) {
-        case 0: launch<0, 0>(grid, c, o, tasks, remap); break;
-        case 1: launch<0, 1>(grid, c, o, tasks, remap); break;
-        case 2: launch<1, 0>(grid, c, o, tasks, remap); break;
-        case 3: launch<1, 1>(grid, c, o, tasks, remap); break;
-        case 4: launch<2, 0>(grid, c, o, tasks, remap); break;
-        case 5: launch<2, 1>(grid, c, o, tasks, remap); break;
-        case 6: launch<3, 0>(grid, c, o, tasks, remap); break;
-        case 7: launch<3, 1>(grid, c, o, tasks, remap); break;
+        case 0: launch<0, 0>(grid, c, o, tasks, remap, work); break;
+        case 1: launch<0, 1>(grid, c, o, tasks, remap, work); break;
+        case 2: launch<1, 0>(grid, c, o, tasks, remap, work); break;
+        case 3: launch<1, 1>(grid, c, o, tasks, remap, work); break;
+        case 4: launch<2, 0>(grid, c, o, tasks, remap, work); break;
+        case 5: launch<2, 1>(grid, c, o, tasks, remap, work); break;
+        case 6: launch<3, 0>(grid, c, o, tasks, remap, work); break;
+        case 7: launch<3, 1>(grid, c, o, tasks, remap, work); break;
+        case 8: launch<4, 0>(grid, c, o, tasks, remap, work); break;
+        case 9: launch<4, 1>(grid, c, o, tasks, remap, work); break;
+        case 10: launch<5, 0>(grid, c, o, tasks, remap, work); break;
+        case 11: launch<5, 1>(grid, c, o, tasks, remap, work); break;
         }
     };
     for (int i = 0; i < 3; i++) run();
@@ -135,7 +160,7 @@ int main(int argc, char **argv)
     CK(hipEventElapsedTime(&ms, a, b));
     ms /= iters;
     const double bytes = double(obytes) + (mode == 2 ? 0.0 : double(cbytes));
-    printf("mode %d wpc %d nt %d remap %d: %.4f ms/launch, %.1f GB/s (%.3f of 8 TB/s)\n", mode, wpc, nt, remap, ms, bytes / ms / 1e6,
+    printf("mode %d wpc %d nt %d remap %d work %d: %.4f ms/launch, %.1f GB/s (%.3f of 8 TB/s)\n", mode, wpc, nt, remap, work, ms, bytes / ms / 1e6,
            bytes / ms / 1e6 / 8000.0);
     return 0;
 }

@@ -60,13 +60,14 @@ __device__ __forceinline__ void wave_lds_sync()
 #define ZPX_JPEGB_WAVES_PER_EU16 2 // int16 instances (at 3 they spill)
 #endif
 #ifndef ZPX_JPEGB_INLANE
-#define ZPX_JPEGB_INLANE 0 // 1: aligned chroma blocks stay in registers (costs 32 VGPRs)
+#define ZPX_JPEGB_INLANE 1 // aligned (4:4:4) chroma blocks stay in registers: 32 VGPRs, no LDS tile (0: through the tile)
 #endif
 #ifndef ZPX_JPEGB_DEPTH2
 #define ZPX_JPEGB_DEPTH2 0 // 1: int8 coefficient DMA two passes ahead (measured slower)
 #endif
 #ifndef ZPX_JPEGB_STORE_LDS
-#define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores)
+#define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores,
+                              // 2: a 1 KiB tile in two rounds per row)
 #endif
 #ifndef ZPX_JPEGB_DMA_NT
 #define ZPX_JPEGB_DMA_NT 0 // 1: non-temporal coefficient DMA (measured 0.8 % slower)
@@ -76,6 +77,10 @@ __device__ __forceinline__ void wave_lds_sync()
 #endif
 #ifndef ZPX_JPEGB_STORE_AUX
 #define ZPX_JPEGB_STORE_AUX 2 // cache policy of the RGBA stores (2 = nt; whole lines per instruction)
+#endif
+
+#ifndef ZPX_JPEGB_DOT2
+#define ZPX_JPEGB_DOT2 1 // row IDCT stages 1-2 as v_dot2 over packed (coef * q) pairs (0: 32-bit dequant + idct_row)
 #endif
 
 // Samples stay in the signed domain (sample - 128, the IDCT's clamp range
@@ -177,6 +182,129 @@ __device__ __forceinline__ void idct_block(int32_t s[64])
     }
 }
 
+// ---- row IDCT over packed pairs (ZPX_JPEGB_DOT2) -------------------------
+// Stages 1 and 2 of idct.zig's row pass (:99-120) are rotations of pairs of
+// dequantized coefficients: x4' = x8 + (W1-W7)x4 with x8 = W7(x4+x5) is
+// W1*x4 + W7*x5 exactly (no rounding between), and likewise for the other
+// six outputs; x0 +/- x1 is 2048(s0 +/- s4) + 128.  With the block's
+// coefficients dequantized as (i16, i16) pairs -- exact, |coef * q| <= 16384
+// on the block kernel's frames -- each output is one v_dot2_i32_i16 (the
+// exact sum, which equals the reference's wrap-around i32 value since it
+// fits), 8 per row instead of 18 multiply/add instructions.
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+
+// (inline asm: for the builtin hipcc picks v_dot2c, whose accumulator is the
+// destination, and spends a v_mov per product initialising it; the VOP3P
+// form takes the packed constant from an SGPR and an inline 0 or a VGPR)
+template <int32_t LO, int32_t HI>
+__device__ __forceinline__ int32_t dot2(uint32_t p)
+{
+    constexpr uint32_t k = (static_cast<uint32_t>(LO) & 0xffffu) | static_cast<uint32_t>(HI) << 16;
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(p), "s"(k));
+    return r;
+}
+template <int32_t LO, int32_t HI>
+__device__ __forceinline__ int32_t dot2(uint32_t p, int32_t acc)
+{
+    constexpr uint32_t k = (static_cast<uint32_t>(LO) & 0xffffu) | static_cast<uint32_t>(HI) << 16;
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(p), "s"(k), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_mul16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, a) * __builtin_bit_cast(v2u16, b));
+}
+
+// Quant-pair table of one component: per row r, four dwords holding
+// (q[r][1], q[r][7]), (q[r][5], q[r][3]), (q[r][2], q[r][6]), (q[r][0], q[r][4])
+// as u16 pairs (natural order; tables are at most 16-bit, decoder.zig:629-666).
+__device__ __forceinline__ uint32_t qpair(const int32_t *q, int i)
+{
+    constexpr int lo[4] = {1, 5, 2, 0}, hi[4] = {7, 3, 6, 4};
+    const int r = i >> 2, k = i & 3;
+    return (static_cast<uint32_t>(q[8 * r + lo[k]]) & 0xffffu) | static_cast<uint32_t>(q[8 * r + hi[k]]) << 16;
+}
+
+// The coefficient pairs of row r, in the qpair order, sign-extended to i16.
+// int8: a piece holds rows 2k and 2k+1 (natural order, 8 bytes a row); the
+// v_perm sign selectors reach the odd bytes of a dword, so the even
+// coefficients come from the row shifted up a byte.  int16: one row a piece.
+template <typename CoefT>
+__device__ __forceinline__ u32x4 row_coef_pairs(const u32x4 *raw, int r)
+{
+    if constexpr (sizeof(CoefT) == 1) {
+        const uint32_t w0 = raw[r >> 1][2 * (r & 1)], w1 = raw[r >> 1][2 * (r & 1) + 1];
+        const uint32_t w0s = w0 << 8, w1s = w1 << 8;
+        return u32x4{__builtin_amdgcn_perm(w1, w0, 0x0b070801u), __builtin_amdgcn_perm(w1, w0, 0x09030a05u),
+                     __builtin_amdgcn_perm(w1s, w0s, 0x0b070903u), __builtin_amdgcn_perm(w1s, w0s, 0x0a050801u)};
+    } else {
+        const u32x4 w = raw[r];
+        return u32x4{__builtin_amdgcn_perm(w[3], w[0], 0x07060302u), __builtin_amdgcn_perm(w[1], w[2], 0x07060302u),
+                     __builtin_amdgcn_perm(w[3], w[1], 0x05040100u), __builtin_amdgcn_perm(w[2], w[0], 0x05040100u)};
+    }
+}
+
+// Lane j's block from the LDS image into registers (all LDS reads of the
+// image issue here, so the caller's lgkmcnt(0) lets the next DMA refill it).
+template <typename CoefT>
+__device__ __forceinline__ void load_raw(const uint8_t *img, int j, u32x4 raw[CoefImage<CoefT>::P])
+{
+#pragma unroll
+    for (int pc = 0; pc < CoefImage<CoefT>::P; pc++)
+        raw[pc] = *reinterpret_cast<const u32x4 *>(img + 16 * CoefImage<CoefT>::slot(j, pc));
+}
+
+// Dequant + row pass (idct.zig:79-145) + column pass with clamp, as
+// idct_block, from the raw block and the component's quant-pair table.
+template <typename CoefT>
+__device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT>::P], const uint32_t *qp, int32_t s[64])
+{
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const u32x4 q = *reinterpret_cast<const u32x4 *>(qp + 4 * r);
+        const u32x4 c = row_coef_pairs<CoefT>(raw, r);
+        const uint32_t p17 = pk_mul16(c[0], q[0]), p53 = pk_mul16(c[1], q[1]);
+        const uint32_t p26 = pk_mul16(c[2], q[2]), p04 = pk_mul16(c[3], q[3]);
+        int32_t x4 = dot2<W1, W7>(p17), x5 = dot2<W7, -W1>(p17);
+        int32_t x6 = dot2<W5, W3>(p53), x7 = dot2<W3, -W5>(p53);
+        int32_t x8 = dot2<2048, 2048>(p04, 128), x0 = dot2<2048, -2048>(p04, 128);
+        int32_t x2 = dot2<W6, -W2>(p26), x3 = dot2<W2, W6>(p26);
+        int32_t x1 = x4 + x6;
+        x4 -= x6;
+        x6 = x5 + x7;
+        x5 -= x7;
+        x7 = x8 + x3;
+        x8 -= x3;
+        x3 = x0 + x2;
+        x0 -= x2;
+        x2 = (R2 * (x4 + x5) + 128) >> 8;
+        x4 = (R2 * (x4 - x5) + 128) >> 8;
+        int32_t *o = s + 8 * r;
+        o[0] = (x7 + x1) >> 8;
+        o[1] = (x3 + x2) >> 8;
+        o[2] = (x0 + x4) >> 8;
+        o[3] = (x8 + x6) >> 8;
+        o[4] = (x8 - x6) >> 8;
+        o[5] = (x0 - x4) >> 8;
+        o[6] = (x3 - x2) >> 8;
+        o[7] = (x7 - x1) >> 8;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        __builtin_amdgcn_sched_barrier(0);
+        int32_t t[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
+        idct_col_clamp<true, true>(t);
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[8 * i + c] = t[i];
+    }
+}
+
 // four signed samples (-128..127) -> one dword of their low bytes (the
 // signed domain: xor kBias4 gives the samples' bytes)
 __device__ __forceinline__ uint32_t pack4(const int32_t *v)
@@ -261,7 +389,11 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     };
     constexpr auto yrow = [](int p) { return kGray ? p : kInLane ? p / 3 : p - CP; };
 
+#if ZPX_JPEGB_DOT2
+    __shared__ __attribute__((aligned(16))) uint32_t qs[3][32]; // Y, Cb, Cr quant-pair tables (qpair)
+#else
     __shared__ __attribute__((aligned(16))) int32_t qs[3][64]; // Y, Cb, Cr (natural order)
+#endif
     // coefficient images: DEPTH passes in flight (int8: the DMA runs two
     // passes ahead, int16 one -- LDS per wave stays within the occupancy
     // the registers allow)
@@ -270,7 +402,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     __shared__ __attribute__((aligned(16))) uint8_t cimg[DEPTH * IMG];
     __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
 #if ZPX_JPEGB_STORE_LDS
-    __shared__ __attribute__((aligned(16))) uint8_t otile[2048]; // one output row of the task (512 RGBA px)
+    __shared__ __attribute__((aligned(16))) uint8_t otile[ZPX_JPEGB_STORE_LDS == 2 ? 1024 : 2048]; // one output row of the task (512 RGBA px)
 #endif
     const int lane = threadIdx.x;
 
@@ -339,8 +471,13 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     };
     auto load_q = [&](int f) __attribute__((always_inline)) {
         const DevJpegFrame &fr = frames[f];
+#if ZPX_JPEGB_DOT2
+#pragma unroll
+        for (int i = lane; i < 3 * 32; i += 64) qs[i >> 5][i & 31] = qpair(fr.qt[i >> 5], i & 31);
+#else
 #pragma unroll
         for (int i = lane; i < 3 * 64; i += 64) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
+#endif
         wave_lds_sync();
     };
 
@@ -450,7 +587,12 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             // previous pass's stores only (16 after a luma pass)
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(vm_wait(p)) : "memory");
             uint8_t *const img = cimg + (DEPTH == 2 ? cur * IMG : 0);
+#if ZPX_JPEGB_DOT2
+            u32x4 raw[CoefImage<CoefT>::P];
+            load_raw<CoefT>(img, lane, raw);
+#else
             dequant_block<CoefT>(img, lane, &qs[pass_block(P, lane).comp][0], s);
+#endif
             // every lane's reads of the image are done before the DMA refills it
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             // pass p + DEPTH's coefficients load while this pass (and the next) computes
@@ -461,7 +603,12 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 issue_pass(tsn, myn, mxn, std::integral_constant<int, pn - NP>{}, img);
             if constexpr (DEPTH == 2) cur ^= 1;
 #ifndef ZPX_JPEGB_TIMING_NO_IDCT // timing-only builds (wrong pixels): cost breakdown
+#if ZPX_JPEGB_DOT2
+            static_assert(NARROW, "the pair IDCT needs |coef * q| <= 16384");
+            idct_block_pairs<CoefT>(raw, &qs[pass_block(P, lane).comp][0], s);
+#else
             idct_block<NARROW>(s);
+#endif
 #else
 #pragma unroll
             for (int i = 0; i < 64; i++) s[i] &= 0xff;
@@ -552,7 +699,22 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
                     // (the host sends only frames with 16-byte aligned rows and
                     // W % 4 == 0: a 4-pixel piece is wholly inside or outside)
-#if ZPX_JPEGB_STORE_LDS
+#if ZPX_JPEGB_STORE_LDS == 2
+                    // the row's 512 pixels in two rounds of 256 through a 1 KiB tile
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        if ((lane >> 5) == h) {
+                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane & 31)) = u32x4{px[0], px[1], px[2], px[3]};
+                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane & 31) + 16) = u32x4{px[4], px[5], px[6], px[7]};
+                        }
+                        wave_lds_sync();
+                        const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + 16 * lane);
+                        wave_lds_sync();
+                        const int xa = mx0 * H0 * 8 + 256 * h + 4 * lane;
+                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
+                                                               0, ZPX_JPEGB_STORE_AUX);
+                    }
+#elif ZPX_JPEGB_STORE_LDS
                     // the row's 512 pixels through a 2 KiB LDS row tile: each
                     // store instruction then writes 1 KiB contiguous (whole lines)
                     *reinterpret_cast<u32x4 *>(otile + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
