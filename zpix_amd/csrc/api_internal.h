@@ -161,20 +161,30 @@ inline bool png_band_fits(uint32_t max_row_bytes, uint32_t band_rows = 128)
     return uint64_t(band_rows) * (uint64_t(max_row_bytes) + 1) + ZPX_PNG_INPUT_PAD + 4 < 0x7ffffff0ull;
 }
 
-// PNG band schedule (the ticket order of png_unfilter_kernel). Bands are
-// ordered by the first output row they write, then by pass: band b of a pass
-// still precedes band b+1 of it (the kernel's no-deadlock rule), and for
-// Adam7 the passes that fill the same output lines run close together, so a
-// line's partial writes from passes 1/2/4/6 meet in L2 instead of reaching
-// HBM one pass at a time. Without interlacing this is band-major order.
+// PNG band schedule (the ticket order of png_unfilter_kernel / png_pair_kernel).
+// Longest bands first (LPT: a band's steps are its row's chunks), then by band
+// index, then pass: band b of a pass still precedes band b+1 of it (the
+// kernels' no-deadlock rule: a band's predecessor holds a lower ticket, so it
+// is running or done).  With Adam7 the bands differ 8x in length (pass 1: 512
+// pixels a row, pass 7: 4096); in output-row order the last tickets are the
+// bottom bands of passes 6-7, and every wave but those idles for up to 2048
+// steps (simulated over 64 x 4K RGBA16: makespan 5,160 steps against 4,096 of
+// work a wave; longest-first: 4,372).  ZPX_PNG_SCHED=row restores the
+// output-row order (A/B: it lets the partial line writes of passes 1/2/4/6
+// meet in L2).  Without interlacing both are band-major order.
 inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passes, uint32_t band_rows)
 {
+    static const bool row_order = [] {
+        const char *e = getenv("ZPX_PNG_SCHED");
+        return e && e[0] == 'r';
+    }();
     std::vector<DevPngBand> sched;
     std::vector<uint64_t> key;
     for (size_t i = 0; i < passes.size(); i++)
         for (uint32_t b = 0; b < passes[i].nbands; b++) {
             sched.push_back(DevPngBand{static_cast<uint32_t>(i), b});
-            key.push_back(static_cast<uint64_t>(b) * band_rows * passes[i].yf + passes[i].yo);
+            key.push_back(row_order ? static_cast<uint64_t>(b) * band_rows * passes[i].yf + passes[i].yo
+                                    : (static_cast<uint64_t>(0xffffffffu - passes[i].row_bytes) << 32) | b);
         }
     std::vector<size_t> idx(sched.size());
     for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
