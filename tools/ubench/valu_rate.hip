@@ -47,6 +47,12 @@ DEF_KERNEL(k_min3, "v_min3_u32 %0, %0, %1, %1")
 DEF_KERNEL(k_bfe, "v_bfe_u32 %0, %0, %1, 8")
 DEF_KERNEL(k_dpp_wshr, "v_mov_b32_dpp %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf")
 DEF_KERNEL(k_dpp_rshr, "v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf")
+DEF_KERNEL(k_mul_lo, "v_mul_lo_u32 %0, %0, %1")
+DEF_KERNEL(k_mad24, "v_mad_i32_i24 %0, %0, %1, %1")
+DEF_KERNEL(k_lshl_add, "v_lshl_add_u32 %0, %0, 4, %1")
+DEF_KERNEL(k_dot2, "v_dot2_i32_i16 %0, %0, %1, 0")
+DEF_KERNEL(k_pk_mul, "v_pk_mul_lo_u16 %0, %0, %1")
+DEF_KERNEL(k_med3, "v_med3_i32 %0, %0, %1, %1")
 DEF_KERNEL(k_dpp_add_wshr, "v_add_u32_dpp %0, %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf")
 
 typedef void (*KFn)(uint32_t *, uint64_t *, int);
@@ -57,7 +63,8 @@ int main()
         {"v_perm_b32", k_perm}, {"v_lshl_or_b32", k_lshl_or}, {"v_and_or_b32", k_and_or},
         {"v_alignbit_b32", k_alignbit}, {"v_sad_u16", k_sad}, {"v_min3_u32", k_min3}, {"v_bfe_u32", k_bfe},
         {"v_mov_dpp wave_shr:1", k_dpp_wshr}, {"v_mov_dpp row_shr:1", k_dpp_rshr},
-        {"v_add_dpp wave_shr:1", k_dpp_add_wshr}};
+        {"v_add_dpp wave_shr:1", k_dpp_add_wshr}, {"v_mul_lo_u32", k_mul_lo}, {"v_mad_i32_i24", k_mad24},
+        {"v_lshl_add_u32", k_lshl_add}, {"v_dot2_i32_i16", k_dot2}, {"v_pk_mul_lo_u16", k_pk_mul}, {"v_med3_i32", k_med3}};
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int iters = 2000;

@@ -449,7 +449,11 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + (k & (kSlots - 1)) * 4]);
                 store(post, r * static_cast<int>(orow_bytes), k, v);
             };
+#ifndef ZPX_PNG_TIMING_NO_SCATTER // timing-only builds (wrong pixels): Adam7 passes stored as if contiguous
             if (ps.xf == 1) { // contiguous rows: one 16-byte store per chunk
+#else
+            if (true) {
+#endif
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     round(i, [&](bool post, int ro, int k, v4u v) {
