@@ -235,4 +235,64 @@ inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> 
 }
 
 
+// Adam7 through a staging area (png_adam7_kernels.hip): passes 1-6 of an
+// interlaced image on the paired-row kernel are unfiltered into contiguous
+// staging rows (whole-line stores), and the merge kernel then writes the
+// image's even rows whole; pass 7 (the odd rows) goes to the image directly.
+// ZPX_PNG_ADAM7_STAGE=0 keeps the in-kernel scatter (A/B).
+struct Adam7Stage {
+    std::vector<DevAdam7Merge> jobs; // stage[] relative to the staging base until png_adam7_rebase
+    std::vector<size_t> staged;      // the redirected passes (their `out` relative likewise)
+    size_t bytes = 0;                // staging bytes
+    uint32_t max_erows = 0;          // the largest image's even rows
+    int obpx = 0;                    // output bytes per pixel (one depth per group)
+};
+inline bool png_adam7_staging_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("ZPX_PNG_ADAM7_STAGE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// passes[first..] are frame f's, as png_frame_passes made them (Adam7 order,
+// empty passes skipped)
+inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPngPass> &passes, size_t first,
+                            Adam7Stage &st)
+{
+    static const uint32_t kA7[6][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4}, {0, 2, 2, 4}, {1, 0, 2, 2}};
+    DevAdam7Merge m{};
+    m.out = f.out;
+    m.out_stride = f.out_stride;
+    m.width = f.width;
+    m.height = f.height;
+    for (size_t i = first; i < passes.size(); i++) {
+        DevPngPass &d = passes[i];
+        int pno = -1;
+        for (int p = 0; p < 6; p++)
+            if (d.xo == kA7[p][0] && d.yo == kA7[p][1] && d.xf == kA7[p][2] && d.yf == kA7[p][3]) pno = p;
+        if (pno < 0) continue; // pass 7
+        const uint64_t sstride = (uint64_t(d.width) * obpx + 127) & ~uint64_t(127);
+        st.bytes = (st.bytes + 255) & ~size_t(255);
+        m.stage[pno] = reinterpret_cast<const uint8_t *>(static_cast<uintptr_t>(st.bytes));
+        m.sstride[pno] = static_cast<uint32_t>(sstride);
+        d.out = reinterpret_cast<uint8_t *>(static_cast<uintptr_t>(st.bytes));
+        d.out_stride = sstride;
+        d.xo = d.yo = 0;
+        d.xf = d.yf = 1;
+        st.staged.push_back(i);
+        st.bytes += sstride * d.rows;
+    }
+    st.jobs.push_back(m);
+    st.max_erows = std::max(st.max_erows, (f.height + 1) / 2);
+    st.obpx = obpx;
+}
+inline void png_adam7_rebase(std::vector<DevPngPass> &passes, Adam7Stage &st, uint8_t *base)
+{
+    for (size_t i : st.staged) passes[i].out = base + reinterpret_cast<uintptr_t>(passes[i].out);
+    for (auto &m : st.jobs)
+        for (int p = 0; p < 6; p++)
+            m.stage[p] = m.sstride[p] ? base + reinterpret_cast<uintptr_t>(m.stage[p]) : nullptr;
+}
+
 } // namespace zpx

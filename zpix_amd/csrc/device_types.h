@@ -37,6 +37,17 @@ struct DevPngPass {
     uint8_t pad;
 };
 
+// Adam7 merge job of one interlaced image (png_adam7_kernels.hip): passes
+// 1-6 unfiltered into staging rows (stage[p], sstride[p] bytes apart) are
+// gathered into the even rows of the image.
+struct DevAdam7Merge {
+    uint8_t *out;             // image base
+    uint64_t out_stride;      // bytes between image rows
+    uint32_t width, height;   // image size in pixels
+    const uint8_t *stage[6];  // passes 1-6 (null when empty)
+    uint32_t sstride[6];      // staging row stride of each pass
+};
+
 // A scheduled band: which pass and which band in it.  Bands are ordered so
 // that band b of a pass always precedes band b+1 of the same pass.
 struct DevPngBand {

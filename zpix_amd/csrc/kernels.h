@@ -45,6 +45,9 @@ int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPng
                     uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit = 0);
 
 // color_kernels.hip
+// Adam7 even rows from the staged passes 1-6 (obpx 4 or 8); max_erows =
+// the largest image's even rows
+int launch_png_adam7_merge(int obpx, const DevAdam7Merge *d_jobs, int njobs, uint32_t max_erows, hipStream_t s);
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);
 int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s);
 int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,

@@ -306,6 +306,9 @@ struct PngGroup {
     bool trns = false; // (pair kernel) the images carry a tRNS colour key
     DevBuf passes, sched, scratch, boundary;
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
+    DevBuf staging, merge_jobs; // Adam7 passes 1-6 and their merge jobs (Adam7Stage)
+    int merge_n = 0, merge_obpx = 0;
+    uint32_t merge_erows = 0;
     size_t scratch_zero_bytes = 0;
 };
 
@@ -517,10 +520,24 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
         g->trns = std::get<2>(kv.first);
         std::vector<DevPngPass> passes;
         std::vector<uint32_t> rowbytes;
+        Adam7Stage a7;
         for (int idx : kv.second) {
+            const size_t first = passes.size();
             png_frame_passes(frames[idx], passes, rowbytes, bytes);
-            bytes += uint64_t(frames[idx].width) * frames[idx].height *
-                     png_out_bpp(frames[idx].depth, frames[idx].use_transparent != 0);
+            const int obpx = png_out_bpp(frames[idx].depth, frames[idx].use_transparent != 0);
+            bytes += uint64_t(frames[idx].width) * frames[idx].height * obpx;
+            if (g->pair && frames[idx].interlace && png_adam7_staging_on())
+                png_adam7_stage(frames[idx], obpx, passes, first, a7);
+        }
+        if (!a7.jobs.empty()) {
+            HIPCHK(ctx, g->staging.alloc(a7.bytes));
+            png_adam7_rebase(passes, a7, g->staging.as<uint8_t>());
+            HIPCHK(ctx, g->merge_jobs.alloc(a7.jobs.size() * sizeof(DevAdam7Merge)));
+            HIPCHK(ctx, hipMemcpy(g->merge_jobs.ptr, a7.jobs.data(), a7.jobs.size() * sizeof(DevAdam7Merge),
+                                  hipMemcpyHostToDevice));
+            g->merge_n = static_cast<int>(a7.jobs.size());
+            g->merge_obpx = a7.obpx;
+            g->merge_erows = a7.max_erows;
         }
         if (int e = png_build_group(ctx, *g, passes, rowbytes)) return e;
         plan->png.push_back(std::move(g));
@@ -559,6 +576,9 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
                                                      g->nsched, g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(),
                                                      g->band_bytes, st);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
+        if (g->merge_n > 0 &&
+            launch_png_adam7_merge(g->merge_obpx, g->merge_jobs.as<DevAdam7Merge>(), g->merge_n, g->merge_erows, st))
+            return hip_fail(ctx, hipGetLastError(), "png adam7 merge launch");
     }
     return ZPX_OK;
 }
