@@ -40,7 +40,8 @@ def oracle_rgba(data):
 def mixed_buffers():
     bufs = [open(p, "rb").read() for p in FIXTURES]
     bufs += [S.jpeg_420(7, 333, 211), S.png_tc8_mixed(8, 301, 97), S.jpeg_progressive_444(9, 130, 77),
-             S.png_rgba16_adam7(10, 77, 45)]
+             S.png_rgba16_adam7(10, 77, 45), S.png_generic(11, 190, 123, 8, 2, interlace=1),
+             S.png_generic(12, 67, 90, 8, 6, interlace=1)]  # Adam7 through the staged passes (RGBA16, RGB8, RGBA8)
     bufs += [bufs[0][:len(bufs[0]) // 2], b"not an image at all", b""]  # malformed items
     return bufs
 

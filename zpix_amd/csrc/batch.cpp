@@ -73,7 +73,7 @@ struct Decoded {
 };
 
 struct Slot {
-    DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid;
+    DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid, dstage; // dstage: Adam7 passes 1-6 (Adam7Stage)
     HostBuf hdesc, hstatus; // pinned descriptor staging, PNG status word
     hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
     std::unique_ptr<Decoded> dec;
@@ -459,20 +459,28 @@ int Pipeline::issue_png(Slot &s)
     uint64_t bytes = 0;
     png_frame_passes(f, passes, rowbytes, bytes);
     const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W, img_stride);
+    Adam7Stage a7;
+    if (pair && ps.interlace && png_adam7_staging_on()) {
+        png_adam7_stage(f, static_cast<int>(ps.out_bpp), passes, 0, a7);
+        HIPCHK(ctx_, s.dstage.reserve(a7.bytes));
+        png_adam7_rebase(passes, a7, s.dstage.as<uint8_t>());
+    }
     const PngBandPlan bp = png_plan_bands(ps.depth, pair, passes, rowbytes);
     const std::vector<DevPngBand> &sched = bp.sched; // output-row order (api_internal.h)
     const uint32_t granules = bp.granules;
     const uint32_t base = bp.nbands;
-    // descriptor staging: passes | sched | palette (256 zpx_color)
+    // descriptor staging: passes | sched | palette (256 zpx_color) | Adam7 merge job
     const size_t pass_b = align_up(passes.size() * sizeof(DevPngPass));
     const size_t sched_b = align_up(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand));
-    const size_t pal_b = 256 * sizeof(zpx_color);
-    const size_t desc_b = pass_b + sched_b + pal_b;
+    const size_t pal_b = align_up(256 * sizeof(zpx_color));
+    const size_t merge_b = a7.jobs.size() * sizeof(DevAdam7Merge);
+    const size_t desc_b = pass_b + sched_b + pal_b + merge_b;
     if (!host_reserve(s.hdesc, desc_b)) return ZPX_E_OUT_OF_MEMORY;
     uint8_t *h = static_cast<uint8_t *>(s.hdesc.ptr);
     memcpy(h, passes.data(), passes.size() * sizeof(DevPngPass));
     if (!sched.empty()) memcpy(h + pass_b, sched.data(), sched.size() * sizeof(DevPngBand));
-    memcpy(h + pass_b + sched_b, ps.palette, pal_b);
+    memcpy(h + pass_b + sched_b, ps.palette, 256 * sizeof(zpx_color));
+    if (merge_b) memcpy(h + pass_b + sched_b + pal_b, a7.jobs.data(), merge_b);
     HIPCHK(ctx_, s.ddesc.reserve(desc_b));
     HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.ptr, h, desc_b, hipMemcpyHostToDevice, ctx_->stream));
     const size_t bound_b = std::max<size_t>(1, base) * granules * sizeof(uint64_t);
@@ -492,6 +500,10 @@ int Pipeline::issue_png(Slot &s)
                                                granules, ctx_->stream);
     if (lrc)
         return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
+    if (merge_b &&
+        launch_png_adam7_merge(a7.obpx, reinterpret_cast<const DevAdam7Merge *>(dd + pass_b + sched_b + pal_b), 1,
+                               a7.max_erows, ctx_->stream))
+        return hip_fail(ctx_, hipGetLastError(), "batch: png adam7 merge");
     HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, ctx_->stream));
     s.check_png = true;
     if (rgba_native) {
