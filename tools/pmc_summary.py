@@ -15,7 +15,8 @@ for p in sorted(os.listdir(base)):
         name = r["Kernel_Name"]
         short = ("jpeg_rgba" if "jpeg_rgba" in name else "jpeg_block" if "jpeg_block_kernel" in name
                  else "png_unfilter" if "png_unfilter" in name
-                 else "png_pair" if "png_pair_kernel" in name else None)
+                 else "png_pair" if "png_pair_kernel" in name
+                 else "png_adam7_merge" if "png_adam7_merge" in name else None)
         import re
         if short == "png_pair":  # one entry per depth template (tc8 vs the Adam7 RGBA16 line)
             m = re.search(r"png_pair_kernel<(\d+)", name)
