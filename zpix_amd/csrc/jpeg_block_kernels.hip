@@ -67,7 +67,7 @@ __device__ __forceinline__ void wave_lds_sync()
 #endif
 #ifndef ZPX_JPEGB_STORE_LDS
 #define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores,
-                              // 2: a 1 KiB tile in two rounds per row)
+                              // 2: a 1 KiB tile in two rounds per row, 3: two rows per round)
 #endif
 #ifndef ZPX_JPEGB_DMA_NT
 #define ZPX_JPEGB_DMA_NT 0 // 1: non-temporal coefficient DMA (measured 0.8 % slower)
@@ -402,7 +402,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     __shared__ __attribute__((aligned(16))) uint8_t cimg[DEPTH * IMG];
     __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
 #if ZPX_JPEGB_STORE_LDS
-    __shared__ __attribute__((aligned(16))) uint8_t otile[ZPX_JPEGB_STORE_LDS == 2 ? 1024 : 2048]; // one output row of the task (512 RGBA px)
+    __shared__ __attribute__((aligned(16))) uint8_t otile[ZPX_JPEGB_STORE_LDS == 2 ? 1024 : ZPX_JPEGB_STORE_LDS == 3 ? 4096 : 2048]; // output row(s) of the task (512 RGBA px each)
 #endif
     const int lane = threadIdx.x;
 
@@ -713,6 +713,25 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                         const int xa = mx0 * H0 * 8 + 256 * h + 4 * lane;
                         __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
                                                                0, ZPX_JPEGB_STORE_AUX);
+                    }
+#elif ZPX_JPEGB_STORE_LDS == 3
+                    // two rows through a 4 KiB tile: four 1 KiB stores a round
+                    *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
+                    *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
+                    if (y & 1) {
+                        wave_lds_sync();
+                        u32x4 v[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) v[i] = *reinterpret_cast<const u32x4 *>(otile + 1024 * i + 16 * lane);
+                        wave_lds_sync();
+                        const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int xx = (i & 1) ? xb : xa;
+                            const uint32_t ro = rowoff - ((i >> 1) ? 0u : ostride);
+                            __builtin_amdgcn_raw_buffer_store_b128(v[i], orsrc, xx < W ? ro + static_cast<uint32_t>(xx) * 4 : kDrop,
+                                                                   0, ZPX_JPEGB_STORE_AUX);
+                        }
                     }
 #elif ZPX_JPEGB_STORE_LDS
                     // the row's 512 pixels through a 2 KiB LDS row tile: each
