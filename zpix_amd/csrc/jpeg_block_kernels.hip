@@ -67,7 +67,11 @@ __device__ __forceinline__ void wave_lds_sync()
 #endif
 #ifndef ZPX_JPEGB_STORE_LDS
 #define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores,
-                              // 2: a 1 KiB tile in two rounds per row, 3: two rows per round)
+                              // 2: a 1 KiB tile in two rounds per row everywhere, 3: two rows per round)
+#endif
+#ifndef ZPX_JPEGB_ROUNDS16
+#define ZPX_JPEGB_ROUNDS16 1 // int16 instances: 4 = the row in 4 rounds through a 512-byte tile (their 8 KiB
+                             // coefficient image leaves room for 12 waves per CU only so): 2.07 ms against 1.47 at 8 waves
 #endif
 #ifndef ZPX_JPEGB_DMA_NT
 #define ZPX_JPEGB_DMA_NT 0 // 1: non-temporal coefficient DMA (measured 0.8 % slower)
@@ -372,6 +376,12 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
     constexpr int T = 64 / H0;                                  // MCUs per task
     constexpr bool kInLane = ZPX_JPEGB_INLANE && !kGray && HC == H0 && VC == V0; // chroma block (x, y) <-> luma block (x, y)
+    // rounds of the RGBA row tile (ZPX_JPEGB_STORE_LDS 1 / 2): 1 = the 2 KiB
+    // tile; int16 with an LDS chroma tile takes ZPX_JPEGB_ROUNDS16
+    constexpr int kRounds = ZPX_JPEGB_STORE_LDS == 2 ? 2
+                            : (ZPX_JPEGB_STORE_LDS == 1 && sizeof(CoefT) == 2 && !kGray && !kInLane) ? ZPX_JPEGB_ROUNDS16
+                                                                                                    : 1;
+    static_assert(kRounds == 1 || kRounds == 2 || kRounds == 4, "row tile rounds");
     constexpr int CBW = kGray ? 1 : T * HC;                     // chroma blocks across a task, per component
     constexpr int CBH = kGray ? 1 : VC;
     constexpr int NCB = kGray ? 0 : 2 * CBW * CBH;              // chroma blocks of a task
@@ -402,7 +412,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     __shared__ __attribute__((aligned(16))) uint8_t cimg[DEPTH * IMG];
     __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
 #if ZPX_JPEGB_STORE_LDS
-    __shared__ __attribute__((aligned(16))) uint8_t otile[ZPX_JPEGB_STORE_LDS == 2 ? 1024 : ZPX_JPEGB_STORE_LDS == 3 ? 4096 : 2048]; // output row(s) of the task (512 RGBA px each)
+    __shared__ __attribute__((aligned(16))) uint8_t otile[kRounds > 1 ? 2048 / kRounds : ZPX_JPEGB_STORE_LDS == 3 ? 4096 : 2048]; // output row(s) of the task (512 RGBA px each)
 #endif
     const int lane = threadIdx.x;
 
@@ -530,7 +540,8 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     // was issued DEPTH passes earlier, and at pass p's start the operations
     // issued after it are the intervening passes' stores and DMAs.
     constexpr int L = CoefImage<CoefT>::P;
-    constexpr auto S = [=](int p) { return kind(((p % NP) + NP) % NP) == 0 ? 16 : 0; };
+    constexpr int kRowStores = kRounds == 4 ? 4 : 2; // store instructions per pixel row
+    constexpr auto S = [=](int p) { return kind(((p % NP) + NP) % NP) == 0 ? 8 * kRowStores : 0; };
     constexpr auto vm_wait = [=](int p) { return DEPTH == 2 ? S(p - 2) + L + S(p - 1) : S(p - 1); };
     // the loop head expects the steady state: the first DEPTH images in
     // flight, each followed by the previous task's stores it would have seen
@@ -538,7 +549,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
     auto pad_stores = [&](int n) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 16; i++)
+        for (int i = 0; i < 32; i++)
             if (i < n) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, ZPX_JPEGB_STORE_AUX);
     };
     if constexpr (DEPTH == 2) {
@@ -699,22 +710,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
                     // (the host sends only frames with 16-byte aligned rows and
                     // W % 4 == 0: a 4-pixel piece is wholly inside or outside)
-#if ZPX_JPEGB_STORE_LDS == 2
-                    // the row's 512 pixels in two rounds of 256 through a 1 KiB tile
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        if ((lane >> 5) == h) {
-                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane & 31)) = u32x4{px[0], px[1], px[2], px[3]};
-                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane & 31) + 16) = u32x4{px[4], px[5], px[6], px[7]};
-                        }
-                        wave_lds_sync();
-                        const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + 16 * lane);
-                        wave_lds_sync();
-                        const int xa = mx0 * H0 * 8 + 256 * h + 4 * lane;
-                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
-                                                               0, ZPX_JPEGB_STORE_AUX);
-                    }
-#elif ZPX_JPEGB_STORE_LDS == 3
+#if ZPX_JPEGB_STORE_LDS == 3
                     // two rows through a 4 KiB tile: four 1 KiB stores a round
                     *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
                     *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
@@ -734,6 +730,25 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                         }
                     }
 #elif ZPX_JPEGB_STORE_LDS
+                    if constexpr (kRounds > 1) {
+                    // the row's 512 pixels in kRounds rounds through a 2048 / kRounds byte
+                    // tile: 64 / kRounds lanes write theirs, 128 / kRounds lanes store 16 B each
+                    constexpr int TB = 2048 / kRounds, LPR = 64 / kRounds;
+#pragma unroll
+                    for (int h = 0; h < kRounds; h++) {
+                        if (lane / LPR == h) {
+                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane % LPR)) = u32x4{px[0], px[1], px[2], px[3]};
+                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane % LPR) + 16) = u32x4{px[4], px[5], px[6], px[7]};
+                        }
+                        wave_lds_sync();
+                        const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + (16 * lane) % TB);
+                        wave_lds_sync();
+                        const int xa = mx0 * H0 * 8 + (512 / kRounds) * h + 4 * lane;
+                        const bool mine = 16 * lane < TB;
+                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, mine && xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
+                                                               0, ZPX_JPEGB_STORE_AUX);
+                    }
+                    } else {
                     // the row's 512 pixels through a 2 KiB LDS row tile: each
                     // store instruction then writes 1 KiB contiguous (whole lines)
                     *reinterpret_cast<u32x4 *>(otile + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
@@ -747,6 +762,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                                                            0, ZPX_JPEGB_STORE_AUX);
                     __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, xb < W ? rowoff + static_cast<uint32_t>(xb) * 4 : kDrop,
                                                            0, ZPX_JPEGB_STORE_AUX);
+                    }
 #else
                     const uint32_t o0 = xpix < W ? rowoff + static_cast<uint32_t>(xpix) * 4 : kDrop;
                     const uint32_t o1 = xpix + 4 < W ? rowoff + static_cast<uint32_t>(xpix) * 4 + 16 : kDrop;
