@@ -17,6 +17,8 @@ struct DevJpegFrame {
     int32_t rule[4];
     int32_t n_comp, color;
     int32_t qt[4][64];       // natural order
+    uint32_t qp[3][32];      // components 0-2: quant-pair tables of the block kernel's row pass
+                             // (per row r: (q1,q7), (q5,q3), (q2,q6), (q0,q4) as u16 pairs)
 };
 
 // One PNG unfilter job: a (pass of a) PNG image.  Rows are processed by the

@@ -69,6 +69,9 @@ __device__ __forceinline__ void wave_lds_sync()
 #define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores,
                               // 2: a 1 KiB tile in two rounds per row everywhere, 3: two rows per round)
 #endif
+#ifndef ZPX_JPEGB_QSGPR
+#define ZPX_JPEGB_QSGPR 1 // (dot2) quant-pair rows by scalar loads from the frame descriptor, no LDS table
+#endif
 #ifndef ZPX_JPEGB_ROUNDS16
 #define ZPX_JPEGB_ROUNDS16 1 // int16 instances: 4 = the row in 4 rounds through a 512-byte tile (their 8 KiB
                              // coefficient image leaves room for 12 waves per CU only so): 2.07 ms against 1.47 at 8 waves
@@ -263,12 +266,12 @@ __device__ __forceinline__ void load_raw(const uint8_t *img, int j, u32x4 raw[Co
 
 // Dequant + row pass (idct.zig:79-145) + column pass with clamp, as
 // idct_block, from the raw block and the component's quant-pair table.
-template <typename CoefT>
-__device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT>::P], const uint32_t *qp, int32_t s[64])
+template <typename CoefT, typename QRow>
+__device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT>::P], QRow &&qrow, int32_t s[64])
 {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const u32x4 q = *reinterpret_cast<const u32x4 *>(qp + 4 * r);
+        const u32x4 q = qrow(r);
         const u32x4 c = row_coef_pairs<CoefT>(raw, r);
         const uint32_t p17 = pk_mul16(c[0], q[0]), p53 = pk_mul16(c[1], q[1]);
         const uint32_t p26 = pk_mul16(c[2], q[2]), p04 = pk_mul16(c[3], q[3]);
@@ -399,7 +402,9 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     };
     constexpr auto yrow = [](int p) { return kGray ? p : kInLane ? p / 3 : p - CP; };
 
-#if ZPX_JPEGB_DOT2
+#if ZPX_JPEGB_DOT2 && ZPX_JPEGB_QSGPR
+    // (quant-pair tables come from the frame descriptor: DevJpegFrame::qp)
+#elif ZPX_JPEGB_DOT2
     __shared__ __attribute__((aligned(16))) uint32_t qs[3][32]; // Y, Cb, Cr quant-pair tables (qpair)
 #else
     __shared__ __attribute__((aligned(16))) int32_t qs[3][64]; // Y, Cb, Cr (natural order)
@@ -421,6 +426,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     // also wait for the stores in flight)
     struct TaskSrc {
         const CoefT *g[3];
+        uint64_t qp; // address of DevJpegFrame::qp[0] of the task's frame (uniform: scalar loads)
         uint8_t *rgba;
         int gwy, gwc, myy, width, height;
         uint32_t stride;
@@ -449,6 +455,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         s.width = static_cast<int>(u32(static_cast<uint32_t>(fr.width)));
         s.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
         s.stride = u32(static_cast<uint32_t>(fr.rgba_stride));
+        s.qp = reinterpret_cast<uint64_t>(ptr(&fr.qp[0][0]));
         return s;
     };
     auto coords = [&](int t, int &f, int &my, int &mx0) __attribute__((always_inline)) {
@@ -481,7 +488,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     };
     auto load_q = [&](int f) __attribute__((always_inline)) {
         const DevJpegFrame &fr = frames[f];
-#if ZPX_JPEGB_DOT2
+#if ZPX_JPEGB_DOT2 && ZPX_JPEGB_QSGPR
+        (void)fr;
+        return;
+#elif ZPX_JPEGB_DOT2
 #pragma unroll
         for (int i = lane; i < 3 * 32; i += 64) qs[i >> 5][i & 31] = qpair(fr.qt[i >> 5], i & 31);
 #else
@@ -616,7 +626,31 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 #ifndef ZPX_JPEGB_TIMING_NO_IDCT // timing-only builds (wrong pixels): cost breakdown
 #if ZPX_JPEGB_DOT2
             static_assert(NARROW, "the pair IDCT needs |coef * q| <= 16384");
-            idct_block_pairs<CoefT>(raw, &qs[pass_block(P, lane).comp][0], s);
+#if ZPX_JPEGB_QSGPR
+            {
+                // the pass's component(s): one for luma / in-lane passes, and
+                // for a chroma pass Cb in lanes < kCb, Cr above (4:2:0, 4:2:2)
+                constexpr int kCb = kind(p) == 1 ? (CBW * CBH - p * 64 < 0 ? 0 : CBW * CBH - p * 64) : 0;
+                constexpr int c0 = kind(p) == 0 ? 0 : kind(p) >= 2 ? kind(p) - 1 : (kCb > 0 ? 1 : 2);
+                // (constant address space: s_load, outside the vmcnt the kernel counts)
+                typedef const __attribute__((address_space(4))) u32x4 *cq;
+                const uint64_t q0 = ts.qp + 128 * c0, q2 = ts.qp + 256;
+                idct_block_pairs<CoefT>(raw, [&](int r) __attribute__((always_inline)) {
+                    const u32x4 a = *reinterpret_cast<cq>(q0 + 16 * r);
+                    if constexpr (kind(p) == 1 && kCb > 0 && kCb < 64) {
+                        const u32x4 b = *reinterpret_cast<cq>(q2 + 16 * r);
+                        return lane < kCb ? a : b;
+                    } else {
+                        (void)q2;
+                        return a;
+                    }
+                }, s);
+            }
+#else
+            idct_block_pairs<CoefT>(raw, [&](int r) __attribute__((always_inline)) {
+                return *reinterpret_cast<const u32x4 *>(&qs[pass_block(P, lane).comp][4 * r]);
+            }, s);
+#endif
 #else
             idct_block<NARROW>(s);
 #endif

@@ -175,6 +175,14 @@ DevJpegFrame zpx::dev_jpeg_frame(const zpx_jpeg_frame &f)
         d.rule[c] = c < f.n_comp ? f.rule[c] : ZPX_BLOCKS_NONE;
         memcpy(d.qt[c], f.qt[c], sizeof(d.qt[c]));
     }
+    // quant-pair tables (jpeg_block_kernels.hip, idct_block_pairs); tables are at most 16-bit
+    static const int kLo[4] = {1, 5, 2, 0}, kHi[4] = {7, 3, 6, 4};
+    for (int c = 0; c < 3; c++)
+        for (int i = 0; i < 32; i++) {
+            const int r = i >> 2, k = i & 3;
+            d.qp[c][i] = (static_cast<uint32_t>(f.qt[c][8 * r + kLo[k]]) & 0xffffu) |
+                         static_cast<uint32_t>(f.qt[c][8 * r + kHi[k]]) << 16;
+        }
     if (f.n_comp == 1) d.h[0] = d.v[0] = 1;
     d.rgba = f.rgba;
     d.rgba_stride = f.rgba_stride;
