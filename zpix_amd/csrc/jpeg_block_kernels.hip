@@ -435,8 +435,15 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     // vector loads, and a use of their results after the rare frame-change
     // branch would cost a vmcnt(0) -- a wait for every store in flight -- in
     // every task; this way the wait stays inside the branch)
+    // The descriptor is read through the constant address space: scalar
+    // loads (lgkmcnt).  Read as vector loads, its use after the loads cost a
+    // vmcnt(0) -- every store and DMA in flight -- and a wave's consecutive
+    // tasks lie in different frames (tstride waves > tasks per frame), so
+    // that drain hit every task.
+    typedef const __attribute__((address_space(4))) DevJpegFrame *CFrame;
     auto task_src = [&](int f) __attribute__((always_inline)) {
-        const DevJpegFrame &fr = frames[f];
+        const CFrame frp = reinterpret_cast<CFrame>(reinterpret_cast<uintptr_t>(frames)) + f;
+        const auto &fr = *frp;
         auto u32 = [](uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(x)); };
         auto ptr = [&](const void *p) {
             const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -455,7 +462,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         s.width = static_cast<int>(u32(static_cast<uint32_t>(fr.width)));
         s.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
         s.stride = u32(static_cast<uint32_t>(fr.rgba_stride));
-        s.qp = reinterpret_cast<uint64_t>(ptr(&fr.qp[0][0]));
+        s.qp = reinterpret_cast<uint64_t>(ptr(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(&fr.qp[0][0]))));
         return s;
     };
     auto coords = [&](int t, int &f, int &my, int &mx0) __attribute__((always_inline)) {

@@ -21,6 +21,9 @@
 namespace zpx {
 namespace {
 
+#ifndef ZPX_A7_NT
+#define ZPX_A7_NT 0 // 1: non-temporal stores of the merged rows
+#endif
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
@@ -85,7 +88,11 @@ __global__ __launch_bounds__(256) void png_adam7_merge_kernel(const DevAdam7Merg
 #pragma unroll
                 for (uint32_t k = 0; k < PPS; k++)
                     copy_px<OBPX>(m, x0 + k, y, reinterpret_cast<uint8_t *>(v) + k * OBPX);
-                *reinterpret_cast<v4u *>(d) = v4u{v[0], v[1], v[2], v[3]};
+    #if ZPX_A7_NT
+            __builtin_nontemporal_store(v4u{v[0], v[1], v[2], v[3]}, reinterpret_cast<v4u *>(d));
+#else
+            *reinterpret_cast<v4u *>(d) = v4u{v[0], v[1], v[2], v[3]};
+#endif
             } else { // ragged right edge or unaligned rows: pixel stores
                 for (uint32_t k = 0; k < PPS && x0 + k < width; k++) copy_px<OBPX>(m, x0 + k, y, d + k * OBPX);
             }
