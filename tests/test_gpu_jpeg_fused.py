@@ -200,3 +200,31 @@ def test_fused_padded_stride():
     frames = [_frame_data(rng, GEOMS["420"], YCBCR, 200, 40, 8, True)]
     for fd, got in zip(frames, _run(frames, stride_pad=48)):
         assert np.array_equal(got, _expected(fd))
+
+
+@pytest.mark.parametrize("bits", [8, 16])
+@pytest.mark.parametrize("geom", ["420", "444"])
+def test_fused_narrow_limit_pairs(bits, geom):
+    """The block kernel's packed-pair row pass at the narrow certificate's
+    edge: 16-bit quant values up to 16384 with coefficients in {-1, 0, 1},
+    and |coef * q| = 16384 exactly (64 * 256 int8, 128 * 128 int16) -- the
+    v_pk_mul_lo_u16 products and v_dot2_i32_i16 sums at their largest."""
+    rng = np.random.default_rng(97 + bits)
+    fd = _frame_data(rng, GEOMS[geom], YCBCR, 264, 40, bits, True)
+    lim = 64 if bits == 8 else 128
+    for c in range(fd["n_comp"]):
+        q = rng.integers(8192, 16385, 64).astype(np.int32)  # zigzag order
+        q[rng.random(64) < 0.3] = 16384
+        q[rng.random(64) < 0.5] = 16384 // lim
+        fd["qz"][c] = q
+        qn = np.zeros(64, np.int32)
+        qn[UNZIG] = q
+        g = rng.integers(-1, 2, fd["grids"][c].shape).astype(np.int32)
+        blk = rng.random(g.shape[0]) < 0.25  # these blocks: +-lim wherever q = 16384 / lim
+        big = rng.choice(np.array([-lim, lim], np.int32), size=g.shape)
+        sel = blk[:, None] & (qn == 16384 // lim)[None, :]
+        g[sel] = big[sel]
+        fd["grids"][c] = g
+        assert np.abs(g.astype(np.int64) * qn[None, :]).max() == 16384  # the certificate's bound, reached
+    got = _run([fd])[0]
+    assert np.array_equal(got, _expected(fd))
