@@ -77,7 +77,8 @@ __device__ __forceinline__ void wave_lds_sync()
                              // coefficient image leaves room for 12 waves per CU only so): 2.07 ms against 1.47 at 8 waves
 #endif
 #ifndef ZPX_JPEGB_DMA_NT
-#define ZPX_JPEGB_DMA_NT 0 // 1: non-temporal coefficient DMA (measured 0.8 % slower)
+#define ZPX_JPEGB_DMA_NT 2 // non-temporal coefficient DMA: 0 never, 1 always, 2 for the in-lane (4:4:4)
+                           // instances (4:4:4 1.90 -> 1.85 ms; 4:2:0 int8 0.3 % slower with it)
 #endif
 #ifndef ZPX_JPEGB_XCD_REMAP
 #define ZPX_JPEGB_XCD_REMAP 1 // consecutive tasks on one XCD (0: round-robin)
@@ -120,18 +121,18 @@ struct CoefImage {
 // (the asm is absent from hipcc's s_waitcnt bookkeeping, which can only make
 // hipcc's own waits longer, never shorter).  M0 is set and restored inside the
 // statement (hipcc reserves it).
+template <bool NT>
 __device__ __forceinline__ void glds16(const void *src, const void *lds_base)
 {
     const uint32_t dst = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
         (const __attribute__((address_space(3))) void *)lds_base));
     uint32_t keep;
-#if ZPX_JPEGB_DMA_NT
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-#else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-#endif
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
 }
 
 // s[k] = coef[k] * q[k] (natural order), lane j's block from the LDS image
@@ -549,7 +550,8 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             const int last = row_ok ? gw - 1 : 0;
             const int bx = min(mx0_ * hh + b0.cx + lane % I::B, last);
             const int q = (lane / I::B + I::P - (I::P == 8 ? k : 0)) % I::P;
-            glds16(row + static_cast<uint32_t>(bx * BYTES + 16 * q), img + 1024 * k);
+            glds16<ZPX_JPEGB_DMA_NT == 1 || (ZPX_JPEGB_DMA_NT == 2 && kInLane)>(row + static_cast<uint32_t>(bx * BYTES + 16 * q),
+                                                                           img + 1024 * k);
         }
     };
     // vmcnt bookkeeping (the DMA is inline asm, so the kernel counts it):
