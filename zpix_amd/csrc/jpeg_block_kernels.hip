@@ -78,7 +78,8 @@ __device__ __forceinline__ void wave_lds_sync()
 #endif
 #ifndef ZPX_JPEGB_DMA_NT
 #define ZPX_JPEGB_DMA_NT 2 // non-temporal coefficient DMA: 0 never, 1 always, 2 for the in-lane (4:4:4)
-                           // instances (4:4:4 1.90 -> 1.85 ms; 4:2:0 int8 0.3 % slower with it)
+                           // and int16 instances (alternating A/B: 4:4:4 1.90 -> 1.85 ms, int16
+                           // 1.398 -> 1.378; int8 4:2:0 1% slower with it)
 #endif
 #ifndef ZPX_JPEGB_XCD_REMAP
 #define ZPX_JPEGB_XCD_REMAP 1 // consecutive tasks on one XCD (0: round-robin)
@@ -550,7 +551,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             const int last = row_ok ? gw - 1 : 0;
             const int bx = min(mx0_ * hh + b0.cx + lane % I::B, last);
             const int q = (lane / I::B + I::P - (I::P == 8 ? k : 0)) % I::P;
-            glds16<ZPX_JPEGB_DMA_NT == 1 || (ZPX_JPEGB_DMA_NT == 2 && kInLane)>(row + static_cast<uint32_t>(bx * BYTES + 16 * q),
+            glds16<ZPX_JPEGB_DMA_NT == 1 || (ZPX_JPEGB_DMA_NT == 2 && (kInLane || sizeof(CoefT) == 2))>(row + static_cast<uint32_t>(bx * BYTES + 16 * q),
                                                                            img + 1024 * k);
         }
     };
