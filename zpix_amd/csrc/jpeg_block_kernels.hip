@@ -28,6 +28,24 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef ZPX_JPEGB_LDS_INORDER
+#define ZPX_JPEGB_LDS_INORDER 1
+#endif
+// Ordering between LDS instructions of one wave (LDS -> LDS only; not for the
+// LDS-DMA, which is a vector-memory operation): the LDS unit executes a wave's
+// LDS instructions in issue order, all lanes of one before the next, so a
+// compiler fence is enough -- no wait for the writes to complete
+// (ZPX_JPEGB_LDS_INORDER=0: lgkmcnt(0) as wave_lds_sync).
+__device__ __forceinline__ void wave_lds_order()
+{
+#if ZPX_JPEGB_LDS_INORDER
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#else
+    wave_lds_sync();
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Fused RGBA kernel, one 8x8 block per lane (jpeg_block_kernel).
 //
@@ -507,7 +525,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 #pragma unroll
         for (int i = lane; i < 3 * 64; i += 64) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
 #endif
-        wave_lds_sync();
+        wave_lds_order();
     };
 
 #if ZPX_JPEGB_XCD_REMAP
@@ -680,7 +698,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                         *reinterpret_cast<u32x2 *>(t + r * CPX) =
                             present ? u32x2{pack4(s + 8 * r), pack4(s + 8 * r + 4)} : u32x2{kBias4, kBias4};
                 }
-                if constexpr (p == CP - 1) wave_lds_sync(); // tile complete before the luma passes
+                if constexpr (p == CP - 1) wave_lds_order(); // tile complete before the luma passes
             } else if constexpr (kind(p) >= 2) {
                 // chroma block kept in this lane: 8 rows x 8 bytes
                 const bool present = ts.g[kind(p) - 1] != nullptr;
@@ -759,11 +777,11 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
                     *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
                     if (y & 1) {
-                        wave_lds_sync();
+                        wave_lds_order();
                         u32x4 v[4];
 #pragma unroll
                         for (int i = 0; i < 4; i++) v[i] = *reinterpret_cast<const u32x4 *>(otile + 1024 * i + 16 * lane);
-                        wave_lds_sync();
+                        wave_lds_order();
                         const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
@@ -784,9 +802,9 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                             *reinterpret_cast<u32x4 *>(otile + 32 * (lane % LPR)) = u32x4{px[0], px[1], px[2], px[3]};
                             *reinterpret_cast<u32x4 *>(otile + 32 * (lane % LPR) + 16) = u32x4{px[4], px[5], px[6], px[7]};
                         }
-                        wave_lds_sync();
+                        wave_lds_order();
                         const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + (16 * lane) % TB);
-                        wave_lds_sync();
+                        wave_lds_order();
                         const int xa = mx0 * H0 * 8 + (512 / kRounds) * h + 4 * lane;
                         const bool mine = 16 * lane < TB;
                         __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, mine && xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
@@ -797,10 +815,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     // store instruction then writes 1 KiB contiguous (whole lines)
                     *reinterpret_cast<u32x4 *>(otile + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
                     *reinterpret_cast<u32x4 *>(otile + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
-                    wave_lds_sync(); // (cross-lane: keep hipcc from reordering around it)
+                    wave_lds_order(); // (cross-lane: keep hipcc from reordering around it)
                     const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + 16 * lane);
                     const u32x4 vb = *reinterpret_cast<const u32x4 *>(otile + 1024 + 16 * lane);
-                    wave_lds_sync();
+                    wave_lds_order();
                     const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
                     __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
                                                            0, ZPX_JPEGB_STORE_AUX);
@@ -820,10 +838,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         });
         if (!more) break;
         if (fn != f) {
-            wave_lds_sync(); // every dequant of this task has read qs
+            wave_lds_order(); // every dequant of this task has read qs
             load_q(fn);
         }
-        if constexpr (CP > 0) wave_lds_sync(); // the tile's reads precede the next task's writes
+        if constexpr (CP > 0) wave_lds_order(); // the tile's reads precede the next task's writes
         task = tn;
         f = fn;
         my = myn;
