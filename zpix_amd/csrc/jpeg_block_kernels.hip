@@ -90,6 +90,15 @@ __device__ __forceinline__ void wave_lds_order()
 #ifndef ZPX_JPEGB_QSGPR
 #define ZPX_JPEGB_QSGPR 1 // (dot2) quant-pair rows by scalar loads from the frame descriptor, no LDS table
 #endif
+#ifndef ZPX_JPEGB_SCHED
+#define ZPX_JPEGB_SCHED 0 // 1: scheduling barriers between the 1-D transforms of the pair IDCT (at 116 VGPRs
+                          // they no longer pay: without, 107 VGPRs and 0.6 % faster int8, A/B x3)
+#endif
+#if ZPX_JPEGB_SCHED
+#define ZPX_JPEGB_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define ZPX_JPEGB_SCHED_BARRIER() ((void)0)
+#endif
 #ifndef ZPX_JPEGB_ROUNDS16
 #define ZPX_JPEGB_ROUNDS16 1 // int16 instances: 4 = the row in 4 rounds through a 512-byte tile (their 8 KiB
                              // coefficient image leaves room for 12 waves per CU only so): 2.07 ms against 1.47 at 8 waves
@@ -318,11 +327,11 @@ __device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT
         o[5] = (x0 - x4) >> 8;
         o[6] = (x3 - x2) >> 8;
         o[7] = (x7 - x1) >> 8;
-        __builtin_amdgcn_sched_barrier(0);
+        ZPX_JPEGB_SCHED_BARRIER();
     }
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-        __builtin_amdgcn_sched_barrier(0);
+        ZPX_JPEGB_SCHED_BARRIER();
         int32_t t[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
