@@ -57,6 +57,11 @@ def parse():
     ap.add_argument("--no-adam7", action="store_true", help="configs[4]: progressive JPEG line only (A/B runs)")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
+    ap.add_argument("--no-strip", action="store_true",
+                    help="skip the strip-kernel fallback line (4094-wide 4:2:0 frames the block kernel refuses)")
+    ap.add_argument("--gather-chunks", type=int, default=8,
+                    help="N>1: the end-to-end gather moves each rank's shard in this many chunks, each as soon "
+                         "as it is decoded (1: one gather after the whole decode)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end streaming line (host entropy threads + H2D + kernels)")
     ap.add_argument("--e2e-images", type=int, default=64,
@@ -302,21 +307,58 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
     return out
 
 
+def bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg):
+    """The fused kernel's fallback: frames the block-per-lane kernel refuses
+    take the strip kernel (jpeg_kernels.hip) -- here 4094x4096 4:2:0 (width
+    % 4 != 0, so its RGBA rows are not 16-byte pieces); the reference runs
+    reconstructBlock on every frame shape (decoder.zig:1553-1634).  A batch
+    of `images` slots of one frame, slot 0 checked against the oracle."""
+    W, H = args.size - 2, args.size
+    d = S.jpeg_420(3000 + rank, W, H, args.quality)
+    co = jpeg.Coefficients(d)
+    jb = device.JpegBatch([co], slots=[0] * args.images, output="rgba", ctx=ctx)
+    if rank == 0:
+        import oracle_py as O
+
+        jb.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = O.jpeg_decode(d).rgba_pixels()
+        if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want)):
+            raise SystemExit("parity failure: strip-kernel JPEG != oracle")
+    steps = max(3, args.steps // 2)
+    wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, 1, ws)
+    ach = jb.bytes / (kern_ms * 1e-3) / 1e9
+    out = {"value": round(jb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
+           "kernel_ms_per_launch": round(kern_ms, 3),
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "jpeg_rgba_kernel",
+                        "algorithmic_bytes_per_launch": jb.bytes},
+           "coeff_bits": int(co.frame.coeff_bits),
+           "config": {"workload": f"{args.images}x {W}x{H} baseline 4:2:0 JPEG -> RGBA through the strip kernel "
+                                  "(block kernel refuses width % 4 != 0)"}}
+    del jb
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_e2e(args, torch, dist, ws, rank, ctx, S, threads):
     """configs[3], end to end from encoded bytes in host memory: this rank's
     shard of the mixed JPEG+PNG batch (image i -> rank i mod N) through
     zpx_batch_decode_rgba -- host entropy/inflate workers overlapped with
     pinned H2D copies and the kernels -- into this rank's RGBA8 arena in HBM,
-    then one RCCL gather of every arena to rank 0 (N > 1), timed apart.
-    The placement is zpix_amd.shard's (shared with the gloo test).  Never
-    `value`: it is bound by the host's serial Huffman/inflate work."""
+    and (N > 1) every arena gathered to rank 0 over RCCL in --gather-chunks
+    chunks, each as soon as this rank has decoded it (batch.start_rgba +
+    zpx_batch_wait_prefix), so the gather overlaps the decode of later
+    chunks.  The placement is zpix_amd.shard's (shared with the gloo test).
+    Never `value`: it is bound by the host's serial Huffman/inflate work."""
     from zpix_amd import batch, shard
 
     W = H = args.size
     total = args.e2e_images * ws
     uniq = {True: S.jpeg_420(0, W, H, args.quality), False: S.png_tc8_mixed(1, W, H)}
     bufs = [uniq[e2e_is_jpeg(i, ws)] for i in range(total)]
-    plan = shard.ShardPlan([(W, H)] * total, ws)
+    gather = ws > 1 and not args.no_gather
+    plan = shard.ShardPlan([(W, H)] * total, ws, chunks=max(1, args.gather_chunks) if gather else 1)
 
     def decode_fn(my_bufs, dsts):
         res, st = batch.decode_rgba(my_bufs, host_threads=threads, ctx=ctx, dst=dsts, with_stats=True)
@@ -326,9 +368,11 @@ def bench_e2e(args, torch, dist, ws, rank, ctx, S, threads):
     warm = torch.empty(2 * W * H * 4, dtype=torch.uint8, device="cuda")
     decode_fn([uniq[True], uniq[False]], [warm[:W * H * 4].view(H, W, 4), warm[W * H * 4:].view(H, W, 4)])
     del warm
-    gather = ws > 1 and not args.no_gather
+    def start_fn(my_bufs, dsts):
+        return batch.start_rgba(my_bufs, host_threads=threads, ctx=ctx, dst=dsts)
+
     r = shard.decode_and_gather(bufs, plan, rank, dist if ws > 1 else None, decode_fn, "cuda", gather=gather,
-                                sync=torch.cuda.synchronize)
+                                sync=torch.cuda.synchronize, start_fn=start_fn if plan.chunks > 1 else None)
     wall = max_over_ranks(dist, r.decode_s, "cuda")
     bad = sorted({s for s in r.statuses.values() if s != "Ok"})
     if bad:
@@ -347,8 +391,13 @@ def bench_e2e(args, torch, dist, ws, rank, ctx, S, threads):
                                   + (", RCCL gather to rank 0" if gather else ""), "configs": "configs[3]"}}
     if gather:
         gs = max_over_ranks(dist, r.gather_s, "cuda")
-        out["gather"] = {"bytes": plan.gather_bytes, "seconds": round(gs, 4),
-                         "GB_s": round(plan.gather_bytes / gs / 1e9, 1), "collective": "torch.distributed.gather (RCCL)"}
+        job = max_over_ranks(dist, r.wall_s, "cuda")
+        tail = max_over_ranks(dist, r.tail_s, "cuda")
+        out["with_gather"] = {"value": round(total * W * H / job / 1e6, 1), "unit": "MPixels/sec",
+                              "wall_s": round(job, 3), "note": "decode + the gather's tail: every image on rank 0"}
+        out["gather"] = {"bytes": plan.gather_bytes, "seconds": round(gs, 4), "tail_s": round(tail, 4),
+                         "chunks": plan.chunks, "GB_s": round(plan.gather_bytes / gs / 1e9, 1),
+                         "collective": f"torch.distributed.gather (RCCL), {plan.chunks} chunks overlapped with decode"}
         if rank == 0:  # spot-check the gathered placement: one image of every rank against its source
             import numpy as np
             import oracle_py as O
@@ -429,8 +478,7 @@ def main():
         launch_bytes = batch.bytes
         achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
-        # the kernel the plan ran (jpeg_kernels.hip: ZPX_JPEG_KERNEL=strip forces the strip kernel)
-        jkernel = "jpeg_rgba_kernel" if os.environ.get("ZPX_JPEG_KERNEL", "").startswith("s") else "jpeg_block_kernel"
+        jkernel = "jpeg_block_kernel"  # the kernel the plan runs on these frames (jpeg_kernels.hip)
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
@@ -517,7 +565,7 @@ def main():
         pv = pb.pixels * ws * steps / wall / 1e6
         ach = pb.bytes / (kern_ms * 1e-3) / 1e9
         ptraffic = None
-        pkernel = "png_unfilter_kernel<TC8>" if os.environ.get("ZPX_PNG_PAIR") == "0" else "png_pair_kernel<TC8>"
+        pkernel = "png_pair_kernel<TC8>"
         try:
             tp = json.load(open(args.traffic_json)).get("png", {})
             if tp.get("images") == args.images and tp.get("size") == args.size and tp.get("kernel") == pkernel:
@@ -540,6 +588,8 @@ def main():
     # ------------------------------------------------------------ configs[4] and end to end
     if not args.no_config5 and not args.png_only:
         result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)
+    if not args.no_strip and not args.png_only:
+        result["strip_fallback"] = bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg)
     if not args.no_e2e and not args.png_only:
         result["end_to_end"] = bench_e2e(args, torch, dist, ws, rank, ctx, S, threads)
     # ------------------------------------------------------------ CPU baseline (rank 0, N=1)

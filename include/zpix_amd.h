@@ -457,7 +457,8 @@ typedef struct zpx_batch_item {
 } zpx_batch_item;
 
 typedef struct zpx_batch_opts {
-    int32_t host_threads;    /* entropy/inflate workers; 0 = min(16, hardware threads) */
+    int32_t host_threads;    /* entropy/inflate workers; 0 = min(16, the process's CPU budget: affinity
+                                capped by the cgroup quota); sharded: that budget / ndev per device */
     int32_t depth;           /* images staged on the device at once; 0 = 2 * host_threads */
     int32_t dst_on_host;     /* 1: dst are host pointers (results copied back over PCIe) */
 } zpx_batch_opts;
@@ -489,6 +490,11 @@ typedef struct zpx_batch zpx_batch;
 int zpx_batch_start(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
                     zpx_batch **out);
 int zpx_batch_wait(zpx_batch *b, zpx_batch_stats *stats /* may be NULL */);
+/* Blocks until items 0..n-1 of a started batch are final (status set, RGBA
+ * complete in dst) or the batch has ended, and returns how many leading
+ * items are final.  Lets a caller move finished results on (the chunked
+ * gather of configs[3]) while later items still decode. */
+int zpx_batch_wait_prefix(zpx_batch *b, int n);
 
 /* configs[3] in one process: image i of `items` is
  * decoded on ctxs[i % ndev] -- one streaming pipeline (zpx_batch_decode_rgba,
@@ -498,16 +504,25 @@ int zpx_batch_wait(zpx_batch *b, zpx_batch_stats *stats /* may be NULL */);
  * when a context shares device 0's GPU.  items[i].dst are DEVICE pointers on
  * ctxs[0]'s device (dst_capacity bytes each); every other device decodes into
  * staging of that capacity first.  Statuses, widths and heights come back in
- * items as from zpx_batch_decode_rgba.  `stats` sums over the devices (wall_s
- * = the whole job, gather included); `gather` (may be NULL) splits the wall
- * time into decode and gather.  The reference has no counterpart (it is
+ * items as from zpx_batch_decode_rgba.  Each result moves as soon as its
+ * device finishes it (the gather overlaps the decode of later images); the
+ * communicators are created once per device set and cached.  A remote item
+ * is ZPX_OK only once it has arrived; one its shard's pipeline or the
+ * gather failed before moving carries that error.  opts->dst_on_host must be
+ * 0 (ZPX_E_INVALID_ARGUMENT).  `stats` sums over the devices (wall_s = the
+ * whole job, gather included); `gather` (may be NULL) splits the wall time
+ * into decode and the gather's tail.  The reference has no counterpart (it is
  * single-threaded, src/root.zig:24-40); per image the result is
  * zpix.fromBuffer + Image.rgbaPixels (image.zig:103-130). */
 typedef struct zpx_gather_stats {
     double decode_s;      /* until every device's pipeline finished */
-    double gather_s;      /* the gather to device 0 */
+    double gather_s;      /* from the first transfer posted to the last one complete (overlaps decode_s) */
     double gather_bytes;  /* bytes moved to device 0 */
     int32_t ndev, pad;
+    double tail_s;        /* the gather's part after decode_s (wall_s = decode_s + tail_s) */
+    double comm_setup_s;  /* communicator creation in this call, outside wall_s (0 once cached) */
+    int32_t comm_ranks;   /* communicator ranks used (1: no send/recv, device copies only) */
+    int32_t pad2;
 } zpx_gather_stats;
 int zpx_batch_decode_sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n_items,
                              const zpx_batch_opts *opts, zpx_batch_stats *stats /* may be NULL */,
@@ -529,6 +544,25 @@ int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds);
  * parallel in this process (tests: the parallel path ran, not its serial
  * fallback).  Host-only. */
 int64_t zpx_debug_jpeg_parallel_scans(void);
+/* Test hook for zpx_batch_decode_sharded: 1 installs an in-process fake
+ * communicator table in place of RCCL -- ncclSend/ncclRecv pairs matched at
+ * ncclGroupEnd and carried out as stream-ordered device copies (the receive
+ * stream waits for the send stream and the send stream for the copy) -- with
+ * one communicator rank per CONTEXT, so the send/recv branch runs even when
+ * every context shares one GPU; 0 restores RCCL.  Returns the previous
+ * setting. */
+int zpx_debug_shard_fake_comm(int on);
+/* Test switches (process-wide): sets option `name` to `value` and returns its
+ * previous value (-1: unknown name).  Each selects between two paths with
+ * the same results, so a test can cover both:
+ *   "jpeg_strip"  1: the fused JPEG plans use the strip kernel for every
+ *                 frame (default 0: the block-per-lane kernel where it applies);
+ *   "jpeg_sparse" 0: the batch pipeline uploads dense coefficient grids
+ *                 (default 1: sparse records);
+ *   "png_pair"    0: PNG frames use the one-row-per-lane kernel (default 1);
+ *   "qoi_segment" pixels per lane segment of the QOI encoder (16..4096;
+ *                 default 0 = 128). */
+int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the sparse
  * coefficient records the batch pipeline uploads and expands
  * them on the host into int32 grids (component after component, blocks x 64,

@@ -435,6 +435,20 @@ def test_qoi_decode_host_matches_oracle():
                     assert name == e.name, cut
 
 
+def test_qoi_decode_host_wrapping_diff():
+    """The product's host QOI decode wraps a qoi.h-style DIFF step mod 256, as
+    the oracle does (tests/test_oracle.py::test_qoi_decode_wrapping_diff)."""
+    import io
+
+    from PIL import Image as PI
+
+    px = np.array([[[255, 10, 10, 255], [0, 10, 10, 255], [1, 9, 255, 255], [255, 255, 0, 255]]], np.uint8)
+    b = io.BytesIO()
+    PI.fromarray(px, "RGBA").save(b, format="QOI")
+    name, img = _raw_qoi_decode(b.getvalue())
+    assert name == "Ok" and np.array_equal(img.pixels.reshape(1, 4, 4), px)
+
+
 def test_bmp_header_errors_match_oracle():
     """bmp readHeader's errors (src/bmp/decoder.zig:42-158) come from the host
     parse, before any device work, so they are checked without a GPU."""

@@ -74,19 +74,30 @@ def _oracle_decode_fn(bufs, dsts):
     return statuses, None
 
 
-def _worker(rank, ws, port, out_dir):
+def _oracle_one(b, d):
+    """decode_one for shard.ThreadedDecode: the oracle into one (H, W, 4) view."""
+    statuses, _ = _oracle_decode_fn([b], [d])
+    return statuses[0]
+
+
+def _worker(rank, ws, port, out_dir, chunks):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         bufs = [_image(i, ws) for i in range(N_IMAGES)]
-        plan = shard.ShardPlan([_dims(b) for b in bufs], ws)
-        r = shard.decode_and_gather(bufs, plan, rank, dist, _oracle_decode_fn, "cpu", gather=True)
+        plan = shard.ShardPlan([_dims(b) for b in bufs], ws, chunks=chunks)
+        if chunks == 1:  # the whole shard, then one gather
+            r = shard.decode_and_gather(bufs, plan, rank, dist, _oracle_decode_fn, "cpu", gather=True)
+        else:  # chunk c gathered while the later chunks still decode
+            r = shard.decode_and_gather(bufs, plan, rank, dist, device="cpu", gather=True,
+                                        start_fn=lambda b, d: shard.ThreadedDecode(_oracle_one, b, d))
         slowest = bench.max_over_ranks(dist, float(rank + 1), "cpu")
         if rank == 0:
             got = {i: (r.statuses[i], r.image(plan, i).reshape(-1).numpy().tobytes().hex()
                        if r.statuses[i] == "Ok" else None) for i in range(N_IMAGES)}
+            timing_ok = r.gather_s is not None and r.wall_s >= r.decode_s and abs(r.tail_s - (r.wall_s - r.decode_s)) < 1e-9
             with open(os.path.join(out_dir, "result.txt"), "w") as f:
-                f.write(repr((got, slowest, r.gather_s is not None, plan.slot_bytes)))
+                f.write(repr((got, slowest, timing_ok, plan.slot_bytes, plan.chunks)))
     finally:
         dist.destroy_process_group()
 
@@ -137,13 +148,38 @@ def test_max_over_ranks_single_process():
     assert bench.max_over_ranks(None, 1.5, "cpu") == 1.5
 
 
-def test_gloo_world2_sharded_decode_and_gather(tmp_path):
+def test_shard_plan_chunks():
+    """Chunked placement: each chunk is one fixed-size gather (chunk c of every
+    rank padded to the largest), images never overlap in an arena or in rank
+    0's gathered buffer, and a chunk's images are consecutive in their shard."""
+    dims = [(16, 8), None, (4, 4), (100, 3), (7, 9), (3, 3), (5, 5), (64, 64), (1, 1)]
+    for chunks in (1, 2, 3, 5, 50):
+        p = shard.ShardPlan(dims, 3, chunks=chunks)
+        assert p.chunks == min(chunks, 3)
+        assert sum(p.chunk_bytes) == p.slot_bytes or p.slot_bytes == 256
+        spans = []
+        for r in range(3):
+            for k, i in enumerate(p.owned[r]):
+                c = p.chunk_of(i)
+                lo, hi = p.chunk_images(c, r)
+                assert lo <= k < hi
+                assert p.chunk_base[c] <= p.offset[i] and p.offset[i] + p.nbytes(i) <= p.chunk_base[c] + p.chunk_bytes[c]
+                if p.nbytes(i):
+                    g = p.gathered_offset(i)
+                    spans.append((g, g + p.nbytes(i)))
+        spans.sort()
+        assert all(spans[k][1] <= spans[k + 1][0] for k in range(len(spans) - 1))
+        assert spans[-1][1] <= 3 * p.slot_bytes
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_gloo_world2_sharded_decode_and_gather(tmp_path, chunks):
     import oracle_py as O
 
     ws = 2
-    mp.spawn(_worker, args=(ws, _free_port(), str(tmp_path)), nprocs=ws, join=True)
-    got, slowest, gathered, slot = ast.literal_eval(open(tmp_path / "result.txt").read())
-    assert slowest == float(ws) and gathered and slot % 256 == 0
+    mp.spawn(_worker, args=(ws, _free_port(), str(tmp_path), chunks), nprocs=ws, join=True)
+    got, slowest, timing_ok, slot, nchunks = ast.literal_eval(open(tmp_path / "result.txt").read())
+    assert slowest == float(ws) and timing_ok and slot % 256 == 0 and nchunks == chunks
     assert sorted(got) == list(range(N_IMAGES))
     for i in range(N_IMAGES):
         data = _image(i, ws)

@@ -177,6 +177,67 @@ def test_batch_decode_sharded_matches_oracle(ndev):
     assert ok >= 6
 
 
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_batch_decode_sharded_fake_comm_send_recv(ndev):
+    """configs[3]'s communicator branch on the one-GPU box: with the in-process
+    fake communicator (zpx_debug_shard_fake_comm: RCCL's grouped send/recv
+    semantics, one rank per context) every context is its own rank, so every
+    remote result travels by ncclSend/ncclRecv on the gather streams, posted
+    as each image finishes.  Bit-exact against the oracle; the communicators
+    are created once (comm_setup_s is 0 on the second call)."""
+    from zpix_amd import shard
+
+    bufs = mixed_buffers()[-9:]
+    ctxs = [zpix_amd.context.default(0)] + [zpix_amd.Context(0) for _ in range(ndev - 1)]
+    dims = [batch._probe_dims(b) or (1, 1) for b in bufs]
+    prev = _lib.lib().zpx_debug_shard_fake_comm(1)
+    try:
+        for call in range(2):
+            dst = [torch.full((h, w, 4), 0x5a, dtype=torch.uint8, device="cuda:0") for w, h in dims]
+            torch.cuda.synchronize()
+            statuses, st, gs = shard.decode_sharded(bufs, ctxs, dst, host_threads=2)
+            assert gs.ndev == ndev and gs.comm_ranks == ndev
+            if call == 1:
+                assert gs.comm_setup_s == 0.0 or gs.comm_setup_s < 1e-3
+            assert abs(st.wall_s - (gs.decode_s + gs.tail_s)) < 1e-6
+            moved = 0
+            for i, data in enumerate(bufs):
+                want, status = oracle_rgba(data)
+                assert statuses[i] == status, (i, statuses[i], status)
+                if status == "Ok":
+                    assert np.array_equal(dst[i].cpu().numpy(), want), (call, i)
+                    if i % ndev:
+                        moved += dims[i][0] * dims[i][1] * 4
+            assert gs.gather_bytes == moved and moved > 0
+            assert gs.gather_s > 0
+    finally:
+        _lib.lib().zpx_debug_shard_fake_comm(prev)
+
+
+def test_batch_decode_sharded_rejects_host_dst():
+    """Results gather into device memory: dst_on_host is an invalid argument."""
+    ctxs = [zpix_amd.context.default(0)]
+    items = (_lib.zpx_batch_item * 1)()
+    handles = (C.c_void_p * 1)(ctxs[0].handle.value)
+    opts = _lib.zpx_batch_opts(1, 0, 1)
+    code = _lib.lib().zpx_batch_decode_sharded(handles, 1, items, 1, C.byref(opts), None, None)
+    assert _lib.error_name(code) == "InvalidArgument"
+
+
+def test_batch_start_wait_prefix():
+    """zpx_batch_wait_prefix: the leading images are final (status and RGBA)
+    before the batch ends; the chunked gather of configs[3] moves them then."""
+    bufs = mixed_buffers()[-8:]
+    run = batch.start_rgba(bufs, host_threads=2)
+    k = run.wait(3)
+    assert k >= 3
+    early = run.statuses(0, 3)
+    res, st = run.finish()
+    assert run.wait(len(bufs)) == len(bufs)
+    assert early == [r.status for r in res[:3]]
+    check_results(bufs, res)
+
+
 def test_batch_png_band_too_wide_rejected():
     """A pass whose 64-row band exceeds the kernel's 2 GiB band range is
     refused with Unsupported (never silently decoded with zero rows past
@@ -230,18 +291,11 @@ def test_batch_sparse_coefficient_upload():
     assert 0 < st.h2d_bytes < 0.8 * dense, (st.h2d_bytes, dense)
 
 
-def test_batch_dense_coefficient_upload_subprocess():
-    """ZPX_JPEG_SPARSE=0 keeps the dense-grid upload; same pixels."""
-    import os
-    import subprocess
-    import sys
-
-    code = (
-        "import sys; sys.path[:0]=['tests','.']\n"
-        "from test_gpu_batch import mixed_buffers, check_results\n"
-        "from zpix_amd import batch\n"
-        "bufs = mixed_buffers(); check_results(bufs, batch.decode_rgba(bufs, host_threads=3)); print('OK')\n"
-    )
-    env = dict(os.environ, ZPX_JPEG_SPARSE="0")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-    assert r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
+def test_batch_dense_coefficient_upload():
+    """The test switch "jpeg_sparse" = 0 keeps the dense-grid upload; same pixels."""
+    prev = _lib.lib().zpx_debug_option(b"jpeg_sparse", 0)
+    try:
+        bufs = mixed_buffers()
+        check_results(bufs, batch.decode_rgba(bufs, host_threads=3))
+    finally:
+        _lib.lib().zpx_debug_option(b"jpeg_sparse", prev)

@@ -126,26 +126,20 @@ def test_qoi_encode_gpu_matches_serial(shape, kind, ch):
     assert got == want
 
 
-@pytest.mark.parametrize("segment", ["16", "64", "256", "1024"])
-def test_qoi_encode_segment_sizes(segment, tmp_path):
-    """The segment size is a tuning knob; the bytes must not depend on it."""
-    import subprocess
-    import sys
+@pytest.mark.parametrize("segment", [16, 64, 256, 1024])
+def test_qoi_encode_segment_sizes(segment):
+    """The segment size is a tuning knob (test switch "qoi_segment"); the
+    bytes must not depend on it."""
+    from zpix_amd import _lib
 
-    code = (
-        "import numpy as np, sys; sys.path[:0]=['tests','.'];"
-        "import oracle_py as O; from zpix_amd import qoi as Q; from test_gpu_formats import _qoi_image;"
-        "ok=True\n"
-        "for k,(w,h) in enumerate([(1000,37),(77,64*16+3),(5,5)]):\n"
-        "  for kind in ('runs','mixed','init'):\n"
-        "    px=_qoi_image(k,w,h,4,kind); ok &= Q.encode(px,Q.Desc(w,h,4,0))==O.qoi_encode(px,w,h,4,0)\n"
-        "print('OK' if ok else 'MISMATCH')"
-    )
-    import os
-
-    env = dict(os.environ, ZPX_QOI_SEGMENT=segment)
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
-    assert r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+    prev = _lib.lib().zpx_debug_option(b"qoi_segment", segment)
+    try:
+        for k, (w, h) in enumerate([(1000, 37), (77, 64 * 16 + 3), (5, 5)]):
+            for kind in ("runs", "mixed", "init"):
+                px = _qoi_image(k, w, h, 4, kind)
+                assert Q.encode(px, Q.Desc(w, h, 4, 0)) == O.qoi_encode(px, w, h, 4, 0), (segment, w, h, kind)
+    finally:
+        _lib.lib().zpx_debug_option(b"qoi_segment", prev)
 
 
 def test_qoi_encode_4k_gpu():
@@ -171,6 +165,34 @@ def test_qoi_encode_device_form():
     torch.cuda.synchronize()
     n = int(d_len.item())
     assert bytes(d_out[:n].cpu().numpy()) == O.qoi_encode(px, w, h, 4, 0)
+
+
+def test_qoi_encode_device_two_streams_share_scratch():
+    """Encodes on two streams of one context share its scratch (tables,
+    prefixes, slots): each is ordered after the previous user's work
+    (zpx_ctx::scratch_ev), so back-to-back encodes of different images on
+    different streams, and the context's own stream, all stay exact."""
+    ctx = zpix_amd.context.default()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream(), None]
+    jobs = []
+    for k in range(6):
+        w, h = 640 + 64 * k, 480 - 32 * k
+        px = _qoi_image(40 + k, w, h, 4, "mixed")
+        desc = Q.Desc(w, h, 4, 0)
+        cap = Q.encode_bound(desc)
+        d_px = torch.from_numpy(px.reshape(-1)).cuda()
+        d_out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        d_len = torch.zeros(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        st = streams[k % 3]
+        Q.encode_device(d_px.data_ptr(), desc, d_out.data_ptr(), cap, d_len.data_ptr(),
+                        st.cuda_stream if st is not None else None, ctx)
+        jobs.append((px, w, h, d_px, d_out, d_len))
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    for px, w, h, _, d_out, d_len in jobs:
+        n = int(d_len.item())
+        assert bytes(d_out[:n].cpu().numpy()) == O.qoi_encode(px, w, h, 4, 0), (w, h)
 
 
 def test_qoi_decode_and_from_buffer():

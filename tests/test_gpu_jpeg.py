@@ -217,6 +217,33 @@ def test_jpeg_batch_4k_fused_matches_oracle():
     assert batch.bytes == 393216 * 128 + 4096 * 4096 * 4 + 3 * 256
 
 
+def test_jpeg_4k_strip_kernel_matches_oracle():
+    """Frames the block kernel refuses take the strip kernel: a 4094-wide
+    4:2:0 frame (width % 4 != 0; bench line "strip_fallback"), and the bench
+    frame itself with the test switch "jpeg_strip" forcing it."""
+    from zpix_amd import _lib
+
+    data = S.jpeg_420(5, 4094, 4096)
+    co = J.Coefficients(data)
+    batch = device.JpegBatch([co], slots=[0], output="rgba")
+    batch.launch(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = O.jpeg_decode(data).rgba_pixels().reshape(4096, 4094, 4)
+    assert torch.equal(batch.output_tensor(0).cpu(), torch.from_numpy(want))
+    del batch
+    data = S.jpeg_420(0, 4096, 4096)
+    co = J.Coefficients(data)
+    prev = _lib.lib().zpx_debug_option(b"jpeg_strip", 1)
+    try:
+        batch = device.JpegBatch([co], slots=[0], output="rgba")
+        batch.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().zpx_debug_option(b"jpeg_strip", prev)
+    want = O.jpeg_decode(data).rgba_pixels().reshape(4096, 4096, 4)
+    assert torch.equal(batch.output_tensor(0).cpu(), torch.from_numpy(want))
+
+
 def test_jpeg_batch_planes_matches_oracle():
     data = S.jpeg_420(3, 640, 480)
     co = J.Coefficients(data)

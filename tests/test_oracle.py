@@ -124,6 +124,25 @@ def test_qoi_encode_diffs_do_not_wrap():
     assert np.array_equal(O.qoi_decode(out).pixels.reshape(1, 2, 4), px)
 
 
+def test_qoi_decode_wrapping_diff():
+    """A qoi.h-style stream whose DIFF step wraps (255 -> 0 as dr = +1, the
+    1-byte QOI_OP_DIFF Pillow's encoder emits): the reference's @intCast
+    (decoder.zig:97-114) traps on it in a safety-checked build; the oracle
+    and the product wrap mod 256 as the QOI specification does (documented
+    deviation, formats_api.cpp) -- the same pixels as Pillow's decoder."""
+    from PIL import Image
+    import io
+
+    px = np.array([[[255, 10, 10, 255], [0, 10, 10, 255], [1, 9, 255, 255], [255, 255, 0, 255]]], np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(px, "RGBA").save(buf, format="QOI")
+    data = buf.getvalue()
+    assert any((b & 0xC0) == 0x40 for b in data[14:-8])  # a DIFF chunk is in there
+    img = O.qoi_decode(data)
+    assert np.array_equal(img.pixels.reshape(1, 4, 4), px)
+    assert np.array_equal(np.asarray(Image.open(io.BytesIO(data)).convert("RGBA")), px)
+
+
 def test_qoi_errors():
     with pytest.raises(O.OracleError) as e:
         O.qoi_encode(np.zeros(4, np.uint8), 0, 1, 4)

@@ -138,7 +138,8 @@ class zpx_qoi_desc(C.Structure):
 
 class zpx_gather_stats(C.Structure):
     _fields_ = [("decode_s", C.c_double), ("gather_s", C.c_double), ("gather_bytes", C.c_double),
-                ("ndev", C.c_int32), ("pad", C.c_int32)]
+                ("ndev", C.c_int32), ("pad", C.c_int32), ("tail_s", C.c_double), ("comm_setup_s", C.c_double),
+                ("comm_ranks", C.c_int32), ("pad2", C.c_int32)]
 
 
 # every symbol include/zpix_amd.h declares (checked by tests/test_abi.py)
@@ -155,7 +156,8 @@ EXPORTS = [
     "zpx_batch_decode_sharded", "zpx_debug_png_stall", "zpx_debug_jpeg_parallel_scans",
     "zpx_bmp_decode", "zpx_bmp_load", "zpx_bmp_probe_buffer", "zpx_qoi_decode", "zpx_qoi_load",
     "zpx_qoi_probe_buffer", "zpx_qoi_encode", "zpx_qoi_encode_bound", "zpx_qoi_encode_device",
-    "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel",
+    "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel", "zpx_batch_wait_prefix",
+    "zpx_debug_shard_fake_comm", "zpx_debug_option",
 ]
 
 _lib = None
@@ -209,6 +211,9 @@ def lib():
                                         C.POINTER(zpx_batch_stats)]),
         "zpx_batch_start": (i32, [vp, C.POINTER(zpx_batch_item), i32, C.POINTER(zpx_batch_opts), C.POINTER(vp)]),
         "zpx_batch_wait": (i32, [vp, C.POINTER(zpx_batch_stats)]),
+        "zpx_batch_wait_prefix": (i32, [vp, i32]),
+        "zpx_debug_shard_fake_comm": (i32, [i32]),
+        "zpx_debug_option": (i32, [C.c_char_p, i32]),
         "zpx_jpeg_decode_config": (i32, [C.c_char_p, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                          C.POINTER(C.c_int32)]),
         "zpx_png_decode_config": (i32, [C.c_char_p, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),

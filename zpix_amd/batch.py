@@ -58,16 +58,10 @@ def _probe_dims(data: bytes):
     return None
 
 
-def decode_rgba(buffers, on_host: bool = False, host_threads: int = 0, depth: int = 0, ctx=None,
-                dst=None, with_stats: bool = False):
-    """Decodes every buffer to RGBA8.
-
-    on_host=False: results are torch uint8 tensors (H, W, 4) on the context's
-    device (or the caller's `dst` tensors / device buffers); True: numpy arrays.
-    Images that fail carry their error name in `status` and no pixels."""
+def _bind(buffers, on_host: bool, c, dst):
+    """The zpx_batch_item array for `buffers` and the destinations it points at."""
     import numpy as np
 
-    c = ctx or context.default()
     n = len(buffers)
     items = (_lib.zpx_batch_item * max(1, n))()
     keep = [bytes(b) for b in buffers]
@@ -80,8 +74,12 @@ def decode_rgba(buffers, on_host: bool = False, host_threads: int = 0, depth: in
         if dst is not None:
             t = dst[i]
             outs.append(t)
-            it.dst = t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data
-            it.dst_capacity = t.numel() if hasattr(t, "numel") else t.nbytes
+            if t is None:
+                it.dst = None
+                it.dst_capacity = 0
+            else:
+                it.dst = t.data_ptr() if hasattr(t, "data_ptr") else t.ctypes.data
+                it.dst_capacity = t.numel() if hasattr(t, "numel") else t.nbytes
             it.dst_stride = 0
             continue
         if dims is None:
@@ -102,13 +100,14 @@ def decode_rgba(buffers, on_host: bool = False, host_threads: int = 0, depth: in
             it.dst = t.data_ptr()
         it.dst_capacity = w * h * 4
         it.dst_stride = 0
-    opts = _lib.zpx_batch_opts(host_threads, depth, 1 if on_host else 0)
-    st = _lib.zpx_batch_stats()
     if not on_host:
         import torch
 
         torch.cuda.synchronize(c.device)  # destinations allocated on torch's stream
-    _lib.check(_lib.lib().zpx_batch_decode_rgba(c.handle, items, n, C.byref(opts), C.byref(st)), c.handle)
+    return items, keep, outs
+
+
+def _results(items, outs, n):
     res = []
     fmt = {1: "jpeg", 2: "png"}
     for i in range(n):
@@ -116,7 +115,63 @@ def decode_rgba(buffers, on_host: bool = False, host_threads: int = 0, depth: in
         ok = it.status == 0
         res.append(BatchResult(_lib.error_name(it.status), it.width, it.height, fmt.get(it.format, "unknown"),
                                outs[i] if ok else None))
-    if with_stats:
-        return res, BatchStats(st.wall_s, st.host_s, st.h2d_bytes, st.d2h_bytes, st.pixels, st.host_threads,
-                               st.depth, st.failed, st.host_jpeg_s, st.host_png_s, st.jpeg_items, st.png_items)
     return res
+
+
+def _stats(st) -> BatchStats:
+    return BatchStats(st.wall_s, st.host_s, st.h2d_bytes, st.d2h_bytes, st.pixels, st.host_threads, st.depth,
+                      st.failed, st.host_jpeg_s, st.host_png_s, st.jpeg_items, st.png_items)
+
+
+def decode_rgba(buffers, on_host: bool = False, host_threads: int = 0, depth: int = 0, ctx=None,
+                dst=None, with_stats: bool = False):
+    """Decodes every buffer to RGBA8.
+
+    on_host=False: results are torch uint8 tensors (H, W, 4) on the context's
+    device (or the caller's `dst` tensors / device buffers); True: numpy arrays.
+    Images that fail carry their error name in `status` and no pixels."""
+    c = ctx or context.default()
+    n = len(buffers)
+    items, keep, outs = _bind(buffers, on_host, c, dst)
+    opts = _lib.zpx_batch_opts(host_threads, depth, 1 if on_host else 0)
+    st = _lib.zpx_batch_stats()
+    _lib.check(_lib.lib().zpx_batch_decode_rgba(c.handle, items, n, C.byref(opts), C.byref(st)), c.handle)
+    res = _results(items, outs, n)
+    return (res, _stats(st)) if with_stats else res
+
+
+class Running:
+    """A batch started with start_rgba: its pipeline runs on a native thread.
+    wait(n) blocks until images 0..n-1 are final (zpx_batch_wait_prefix: their
+    RGBA is complete in dst), so finished results can move on while later
+    images still decode; finish() joins and returns (results, stats)."""
+
+    def __init__(self, handle, items, keep, outs, n, ctx):
+        self._h, self._items, self._keep, self._outs, self._n, self._ctx = handle, items, keep, outs, n, ctx
+
+    def wait(self, n: int) -> int:
+        if self._h is None:
+            return self._n
+        return _lib.lib().zpx_batch_wait_prefix(self._h, n)
+
+    def statuses(self, lo: int, hi: int) -> list:
+        """Error names of images lo..hi-1 (final once wait(hi) returned >= hi)."""
+        return [_lib.error_name(self._items[i].status) for i in range(lo, hi)]
+
+    def finish(self):
+        st = _lib.zpx_batch_stats()
+        h, self._h = self._h, None
+        if h is not None:
+            _lib.check(_lib.lib().zpx_batch_wait(h, C.byref(st)), self._ctx.handle)
+        return _results(self._items, self._outs, self._n), _stats(st)
+
+
+def start_rgba(buffers, host_threads: int = 0, depth: int = 0, ctx=None, dst=None) -> Running:
+    """zpx_batch_start: decode_rgba into device memory, asynchronously."""
+    c = ctx or context.default()
+    n = len(buffers)
+    items, keep, outs = _bind(buffers, False, c, dst)
+    opts = _lib.zpx_batch_opts(host_threads, depth, 0)
+    h = C.c_void_p()
+    _lib.check(_lib.lib().zpx_batch_start(c.handle, items, n, C.byref(opts), C.byref(h)), c.handle)
+    return Running(h, items, keep, outs, n, c)

@@ -7,21 +7,28 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "zpix_amd.h"
 #include "device_types.h"
+#include "options.h"
 
 struct zpx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string last_error;
     // grow-only device scratch for stream-ordered work that needs no host
-    // round trip (the QOI encoder's tables and slots); used on `stream` or a
-    // caller stream, one call at a time per context
+    // round trip (the QOI encoder's tables and slots), on `stream` or a
+    // caller stream: every user takes scratch_mu while it enqueues, makes
+    // its stream wait for scratch_ev (the previous user's work), and
+    // records scratch_ev after its own, so uses on different streams run
+    // one after the other on the device
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
+    hipEvent_t scratch_ev = nullptr;
+    std::mutex scratch_mu;
 };
 
 namespace zpx {
@@ -138,6 +145,14 @@ struct DevJpegFrame;
 struct DevPngPass;
 struct DevImage;
 
+// zpx_batch_decode_rgba with a completion hook: on_done(user, i) runs on the
+// pipeline's dispatcher thread as soon as item i's status is final and its
+// result is complete in dst (the slot's last event has completed) -- what
+// the sharded gather and zpx_batch_wait_prefix post their transfers on.
+typedef void (*BatchDone)(void *user, int item);
+int batch_decode_rgba_hook(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                           zpx_batch_stats *stats, BatchDone on_done, void *user);
+
 // zpx_api.cpp helpers shared with the batch pipeline
 void jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes);
 DevJpegFrame dev_jpeg_frame(const zpx_jpeg_frame &f);
@@ -169,15 +184,11 @@ inline bool png_band_fits(uint32_t max_row_bytes, uint32_t band_rows = 128)
 // pixels a row, pass 7: 4096); in output-row order the last tickets are the
 // bottom bands of passes 6-7, and every wave but those idles for up to 2048
 // steps (simulated over 64 x 4K RGBA16: makespan 5,160 steps against 4,096 of
-// work a wave; longest-first: 4,372).  ZPX_PNG_SCHED=row restores the
-// output-row order (A/B: it lets the partial line writes of passes 1/2/4/6
-// meet in L2).  Without interlacing both are band-major order.
+// work a wave; longest-first: 4,372; measured 8.12 -> 7.79 ms).  Without
+// interlacing both are band-major order.
 inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passes, uint32_t band_rows)
 {
-    static const bool row_order = [] {
-        const char *e = getenv("ZPX_PNG_SCHED");
-        return e && e[0] == 'r';
-    }();
+    constexpr bool row_order = false; // (output-row order: measured slower, see above)
     std::vector<DevPngBand> sched;
     std::vector<uint64_t> key;
     for (size_t i = 0; i < passes.size(); i++)
@@ -206,15 +217,11 @@ struct PngBandPlan {
 int png_band_granules(int depth, uint32_t max_row_bytes);      // kernels.h
 bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride); // kernels.h
 // Which kernel takes a PNG image: the paired-row kernel wherever it
-// supports the depth (ZPX_PNG_PAIR=0 forces the one-row-per-lane kernel, for
-// A/B runs).
+// supports the depth (the test switch "png_pair" = 0 forces the
+// one-row-per-lane kernel).
 inline bool png_use_pair(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride)
 {
-    static const bool off = [] {
-        const char *e = getenv("ZPX_PNG_PAIR");
-        return e && e[0] == '0';
-    }();
-    return !off && png_pair_supported(depth, interlace, use_trns, width, out_stride);
+    return opt(Opt::PngPair) && png_pair_supported(depth, interlace, use_trns, width, out_stride);
 }
 inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> &passes,
                                   const std::vector<uint32_t> &rowbytes)
@@ -239,7 +246,7 @@ inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> 
 // interlaced image on the paired-row kernel are unfiltered into contiguous
 // staging rows (whole-line stores), and the merge kernel then writes the
 // image's even rows whole; pass 7 (the odd rows) goes to the image directly.
-// ZPX_PNG_ADAM7_STAGE=0 keeps the in-kernel scatter (A/B).
+// (The in-kernel scatter it replaced: 8.10 against 6.56 ms per 64 x 4K RGBA16.)
 struct Adam7Stage {
     std::vector<DevAdam7Merge> jobs; // stage[] relative to the staging base until png_adam7_rebase
     std::vector<size_t> staged;      // the redirected passes (their `out` relative likewise)
@@ -247,14 +254,7 @@ struct Adam7Stage {
     uint32_t max_erows = 0;          // the largest image's even rows
     int obpx = 0;                    // output bytes per pixel (one depth per group)
 };
-inline bool png_adam7_staging_on()
-{
-    static const bool on = [] {
-        const char *e = getenv("ZPX_PNG_ADAM7_STAGE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+inline bool png_adam7_staging_on() { return true; }
 // passes[first..] are frame f's, as png_frame_passes made them (Adam7 order,
 // empty passes skipped)
 inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPngPass> &passes, size_t first,

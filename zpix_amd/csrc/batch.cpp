@@ -33,6 +33,7 @@
 
 #include "api_internal.h"
 #include "device_types.h"
+#include "host_cpus.h"
 #include "jpeg_host.h"
 #include "kernels.h"
 #include "png_host.h"
@@ -85,22 +86,15 @@ struct Slot {
 
 bool host_reserve(HostBuf &b, size_t n) { return b.bytes >= n || b.alloc(n, false); }
 
-// ZPX_JPEG_SPARSE=0 uploads dense coefficient grids instead of records
-bool jpeg_sparse_upload()
-{
-    static const bool on = [] {
-        const char *e = getenv("ZPX_JPEG_SPARSE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// test switch "jpeg_sparse" = 0: dense coefficient grids instead of records
+bool jpeg_sparse_upload() { return opt(Opt::JpegSparse) != 0; }
 
 class Pipeline {
   public:
-    Pipeline(zpx_ctx *ctx, zpx_batch_item *items, int n, const zpx_batch_opts *o) : ctx_(ctx), items_(items), n_(n)
+    Pipeline(zpx_ctx *ctx, zpx_batch_item *items, int n, const zpx_batch_opts *o, BatchDone on_done, void *user)
+        : ctx_(ctx), items_(items), n_(n), on_done_(on_done), user_(user)
     {
-        const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-        threads_ = o && o->host_threads > 0 ? o->host_threads : std::min(16, hw);
+        threads_ = o && o->host_threads > 0 ? o->host_threads : std::min(16, host_cpu_budget());
         depth_ = o && o->depth > 0 ? o->depth : 2 * threads_;
         depth_ = std::max(depth_, 1);
         on_host_ = o && o->dst_on_host;
@@ -119,10 +113,16 @@ class Pipeline {
     int finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32_t W, uint32_t H, hipStream_t producer);
     void retire(Slot &s);
     void give_token();
+    void finished(int item) // item's status and result are final
+    {
+        if (on_done_) on_done_(user_, item);
+    }
 
     zpx_ctx *ctx_;
     zpx_batch_item *items_;
     int n_;
+    BatchDone on_done_ = nullptr;
+    void *user_ = nullptr;
     int threads_ = 1, depth_ = 1;
     bool on_host_ = false;
 
@@ -579,9 +579,11 @@ void Pipeline::retire(Slot &s)
         it.status = ZPX_OK;
         pixels_ += double(it.width) * it.height;
     }
+    const int item = s.dec->item;
     s.dec.reset(); // pinned host buffers go back to the pool
     s.busy = false;
     give_token();
+    finished(item);
 }
 
 int Pipeline::run(zpx_batch_stats *stats)
@@ -621,12 +623,14 @@ int Pipeline::run(zpx_batch_stats *stats)
             items_[i].status = ZPX_E_OUT_OF_MEMORY;
             done++;
             give_token();
+            finished(i);
         }
         if (d) {
             if (d->status != ZPX_OK) {
                 items_[d->item].status = d->status;
                 done++;
                 give_token();
+                finished(d->item);
             } else {
                 Slot *free_slot = nullptr;
                 for (auto &s : slots_)
@@ -644,12 +648,14 @@ int Pipeline::run(zpx_batch_stats *stats)
                 rc = issue(s, sync_done);
                 ZPX_TRACE("dispatch: item %d issued rc %d sync %d", s.dec->item, rc, sync_done ? 1 : 0);
                 if (rc == ZPX_OK && sync_done) {
-                    if (items_[s.dec->item].status == ZPX_OK)
-                        pixels_ += double(items_[s.dec->item].width) * items_[s.dec->item].height;
+                    const int item = s.dec->item;
+                    if (items_[item].status == ZPX_OK)
+                        pixels_ += double(items_[item].width) * items_[item].height;
                     s.dec.reset();
                     s.busy = false;
                     done++;
                     give_token();
+                    finished(item);
                 }
             }
         }
@@ -695,23 +701,46 @@ int Pipeline::run(zpx_batch_stats *stats)
 
 } // namespace
 
-extern "C" int zpx_batch_decode_rgba(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
-                                     zpx_batch_stats *stats)
+int zpx::batch_decode_rgba_hook(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                                zpx_batch_stats *stats, BatchDone on_done, void *user)
 {
     if (!ctx || n_items < 0 || (n_items > 0 && !items)) return ZPX_E_INVALID_ARGUMENT;
     CtxScope scope(ctx);
     try {
-        Pipeline p(ctx, items, n_items, opts);
+        Pipeline p(ctx, items, n_items, opts, on_done, user);
         return p.run(stats);
     } catch (...) {
         return ZPX_E_OUT_OF_MEMORY;
     }
 }
 
+extern "C" int zpx_batch_decode_rgba(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
+                                     zpx_batch_stats *stats)
+{
+    return batch_decode_rgba_hook(ctx, items, n_items, opts, stats, nullptr, nullptr);
+}
+
+// zpx_batch_start's handle: the pipeline's thread, and which items are final
+// (for zpx_batch_wait_prefix)
 struct zpx_batch {
     std::thread th;
     int rc = ZPX_OK;
     zpx_batch_stats stats{};
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint8_t> done; // done[i]: item i is final
+    int prefix = 0;            // items 0..prefix-1 are final
+    bool ended = false;        // the pipeline returned
+    static void on_done(void *user, int item)
+    {
+        zpx_batch *b = static_cast<zpx_batch *>(user);
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            b->done[static_cast<size_t>(item)] = 1;
+            while (b->prefix < static_cast<int>(b->done.size()) && b->done[static_cast<size_t>(b->prefix)]) b->prefix++;
+        }
+        b->cv.notify_all();
+    }
 };
 
 extern "C" int zpx_batch_start(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
@@ -724,12 +753,29 @@ extern "C" int zpx_batch_start(zpx_ctx *ctx, zpx_batch_item *items, int n_items,
     try {
         std::unique_ptr<zpx_batch> b(new zpx_batch);
         zpx_batch *bp = b.get();
-        b->th = std::thread([=] { bp->rc = zpx_batch_decode_rgba(ctx, items, n_items, &o, &bp->stats); });
+        b->done.assign(static_cast<size_t>(n_items), 0);
+        b->th = std::thread([=] {
+            const int rc = batch_decode_rgba_hook(ctx, items, n_items, &o, &bp->stats, &zpx_batch::on_done, bp);
+            {
+                std::lock_guard<std::mutex> lk(bp->mu);
+                bp->rc = rc;
+                bp->ended = true;
+            }
+            bp->cv.notify_all();
+        });
         *out = b.release();
     } catch (...) {
         return ZPX_E_OUT_OF_MEMORY;
     }
     return ZPX_OK;
+}
+
+extern "C" int zpx_batch_wait_prefix(zpx_batch *b, int n)
+{
+    if (!b) return ZPX_E_INVALID_ARGUMENT;
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->cv.wait(lk, [&] { return b->prefix >= n || b->ended; });
+    return b->prefix;
 }
 
 extern "C" int zpx_batch_wait(zpx_batch *b, zpx_batch_stats *stats)

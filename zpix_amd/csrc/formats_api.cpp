@@ -166,7 +166,15 @@ int qoi_decode_impl(const zpx_allocator *al, const uint8_t *data, size_t len, zp
         } else if (p < chunks_len) {
             const uint8_t b1 = data[p++];
             // payload bytes are read without the chunks_len check (:71-82); past
-            // the end of the buffer the reference's bounds check panics
+            // the end of the buffer the reference's bounds check panics, which
+            // maps to ZPX_E_PANIC.  Its other safety trap -- @intCast of a
+            // DIFF/LUMA step that leaves 0..255 (:97-114) -- is NOT mapped:
+            // those steps wrap mod 256, as the QOI specification (and qoi.h's
+            // encoder, which emits them for 255 -> 0) has them, and as a
+            // ReleaseFast reference build truncates; the reference's own
+            // encoder never emits one (encoder.zig:97-101).  The oracle does
+            // the same (zo_qoi_decode), pinned by tests/test_oracle.py
+            // test_qoi_decode_wrapping_diff.
             const size_t need = b1 == 0xfe ? 3 : b1 == 0xff ? 4 : (b1 & 0xc0) == 0x80 ? 1 : 0;
             if (p + need > len) {
                 zpx_image_free(al, &img);
@@ -185,7 +193,7 @@ int qoi_decode_impl(const zpx_allocator *al, const uint8_t *data, size_t len, zp
                 }
                 break;
             case 0: memcpy(px, index[b1 & 0x3f], 4); break;
-            case 1: // QOI_OP_DIFF (mod 256, as the QOI specification)
+            case 1: // QOI_OP_DIFF (mod 256, see above)
                 px[0] = static_cast<uint8_t>(px[0] + ((b1 >> 4) & 3) - 2);
                 px[1] = static_cast<uint8_t>(px[1] + ((b1 >> 2) & 3) - 2);
                 px[2] = static_cast<uint8_t>(px[2] + (b1 & 3) - 2);
@@ -214,12 +222,10 @@ bool qoi_desc_ok(const zpx_qoi_desc *d)
 
 uint32_t qoi_segment()
 {
-    static const uint32_t seg = [] {
-        const char *e = getenv("ZPX_QOI_SEGMENT");
-        const long v = e ? strtol(e, nullptr, 10) : 0;
-        return v >= 16 && v <= 4096 ? static_cast<uint32_t>(v) & ~15u : 128u; // whole load groups
-    }();
-    return seg;
+    // pixels per lane's segment: 128, or the test switch "qoi_segment"
+    // (16..4096, whole load groups) -- the bytes are the same at every size
+    const int v = opt(Opt::QoiSegment);
+    return v >= 16 && v <= 4096 ? static_cast<uint32_t>(v) & ~15u : 128u;
 }
 
 int qoi_encode_device_impl(zpx_ctx *ctx, const uint8_t *d_pixels, const zpx_qoi_desc *desc, uint8_t *d_out,
@@ -233,6 +239,12 @@ int qoi_encode_device_impl(zpx_ctx *ctx, const uint8_t *d_pixels, const zpx_qoi_
     const uint32_t S = qoi_segment();
     QoiEncodeArgs a;
     const size_t scratch = qoi_scratch_layout(n, S, nullptr, nullptr);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    // the context's scratch is shared: order this encode after the previous
+    // user's work, whatever stream that ran on (see zpx_ctx::scratch_ev)
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    if (!ctx->scratch_ev) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming));
+    else HIPCHK(ctx, hipStreamWaitEvent(st, ctx->scratch_ev, 0));
     HIPCHK(ctx, ctx_scratch(ctx, scratch));
     qoi_scratch_layout(n, S, &a, static_cast<uint8_t *>(ctx->scratch));
     a.pixels = d_pixels;
@@ -241,8 +253,8 @@ int qoi_encode_device_impl(zpx_ctx *ctx, const uint8_t *d_pixels, const zpx_qoi_
     a.colorspace = desc->colorspace;
     a.out = d_out;
     a.out_len = d_out_len;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     if (launch_qoi_encode(desc->channels, a, st)) return hip_fail(ctx, hipGetLastError(), "qoi encode kernels");
+    HIPCHK(ctx, hipEventRecord(ctx->scratch_ev, st));
     return ZPX_OK;
 }
 

@@ -500,6 +500,28 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
 //      output's last 32 KiB), then the rest of every chunk in parallel.
 // Anything irregular returns false and the caller runs the serial decoder,
 // so results are the serial path's by construction.
+// Runs job(i) for i in [first, n) on new threads, then job(i) for i < first
+// on this one, and joins them all.  False when a thread could not be started
+// (thread or pid limit): the threads already running are joined, nothing
+// unwinds past a joinable std::thread, and the caller falls back to the
+// serial decoder.
+template <typename F>
+bool run_pool(int first, int n, F &&job)
+{
+    std::vector<std::thread> pool;
+    bool started = true;
+    try {
+        pool.reserve(static_cast<size_t>(n > first ? n - first : 0));
+        for (int i = first; i < n; i++) pool.emplace_back(job, i);
+    } catch (...) {
+        started = false;
+    }
+    if (started)
+        for (int i = 0; i < first; i++) job(i);
+    for (auto &t : pool) t.join();
+    return started;
+}
+
 bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced, int threads)
 {
     *produced = 0;
@@ -509,7 +531,6 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
     std::vector<uint64_t> cand(T + 1, ~uint64_t(0));
     cand[0] = 16;
     const uint64_t total_bits = uint64_t(in_len) * 8;
-    std::vector<std::thread> pool;
     // 1. candidate starts
     auto search = [&](int i) {
         const uint64_t lo = total_bits * uint64_t(i) / uint64_t(T);
@@ -520,9 +541,7 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
                 return;
             }
     };
-    for (int i = 1; i < T; i++) pool.emplace_back(search, i);
-    for (auto &t : pool) t.join();
-    pool.clear();
+    if (!run_pool(1, T, [&](int i) { if (i) search(i); })) return false; // (cand[0] is the stream start)
     // 2. speculative decode, chunk i from cand[i] to the next candidate it lands on
     struct Chunk {
         std::vector<uint16_t> sym;
@@ -589,10 +608,7 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
         o.o -= kWin;
         c.n = o.o;
     };
-    for (int i = 1; i < T; i++) pool.emplace_back(run, i);
-    run(0);
-    for (auto &t : pool) t.join();
-    pool.clear();
+    if (!run_pool(1, T, run)) return false; // (chunk 0 on this thread)
     // the chain of chunks that landed on each other, from chunk 0 to the end
     std::vector<int> chain;
     size_t total = 0;
@@ -633,15 +649,14 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
         if (!resolve(k, n > kWin ? n - kWin : 0, n)) return false;
     }
     std::atomic<bool> bad{false};
-    for (size_t k = 1; k < chain.size(); k++) {
-        const size_t n = ch[chain[k]].n;
-        if (n > kWin && off[k] < want)
-            pool.emplace_back([&, k, n] {
-                if (!resolve(k, 0, n - kWin)) bad = true;
-            });
-    }
-    for (auto &t : pool) t.join();
-    if (bad) return false;
+    std::vector<size_t> bulk; // chunks with a bulk before their last 32 KiB
+    for (size_t k = 1; k < chain.size(); k++)
+        if (ch[chain[k]].n > kWin && off[k] < want) bulk.push_back(k);
+    const bool started = run_pool(0, static_cast<int>(bulk.size()), [&](int j) {
+        const size_t k = bulk[static_cast<size_t>(j)];
+        if (!resolve(k, 0, ch[chain[k]].n - kWin)) bad = true;
+    });
+    if (!started || bad) return false;
     *produced = want;
     return true;
 }

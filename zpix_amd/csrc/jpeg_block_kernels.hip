@@ -20,30 +20,15 @@
 namespace zpx {
 namespace {
 
-// Wave-local LDS ordering: a wave's LDS operations complete in order, so a
-// compiler fence plus lgkmcnt(0) orders its lanes' writes before its reads.
-__device__ __forceinline__ void wave_lds_sync()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
-
-#ifndef ZPX_JPEGB_LDS_INORDER
-#define ZPX_JPEGB_LDS_INORDER 1
-#endif
 // Ordering between LDS instructions of one wave (LDS -> LDS only; not for the
 // LDS-DMA, which is a vector-memory operation): the LDS unit executes a wave's
 // LDS instructions in issue order, all lanes of one before the next, so a
-// compiler fence is enough -- no wait for the writes to complete
-// (ZPX_JPEGB_LDS_INORDER=0: lgkmcnt(0) as wave_lds_sync).
+// compiler fence is enough -- no wait for the writes to complete (measured
+// against lgkmcnt(0) at every such point: int8 1.201 -> 1.193 ms).
 __device__ __forceinline__ void wave_lds_order()
 {
-#if ZPX_JPEGB_LDS_INORDER
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-#else
-    wave_lds_sync();
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -71,53 +56,21 @@ __device__ __forceinline__ void wave_lds_order()
 // static and the next pass's loads overlap the whole IDCT + colour work of
 // the current one.
 // ---------------------------------------------------------------------------
-#ifndef ZPX_JPEGB_WAVES_PER_EU
-#define ZPX_JPEGB_WAVES_PER_EU 3 // int8 instances (168 VGPRs, no scratch)
-#endif
-#ifndef ZPX_JPEGB_WAVES_PER_EU16
-#define ZPX_JPEGB_WAVES_PER_EU16 2 // int16 instances (at 3 they spill)
-#endif
-#ifndef ZPX_JPEGB_INLANE
-#define ZPX_JPEGB_INLANE 1 // aligned (4:4:4) chroma blocks stay in registers: 32 VGPRs, no LDS tile (0: through the tile)
-#endif
-#ifndef ZPX_JPEGB_DEPTH2
-#define ZPX_JPEGB_DEPTH2 0 // 1: int8 coefficient DMA two passes ahead (measured slower)
-#endif
-#ifndef ZPX_JPEGB_STORE_LDS
-#define ZPX_JPEGB_STORE_LDS 1 // RGBA rows through an LDS row tile: whole-line stores (0: two half-line stores,
-                              // 2: a 1 KiB tile in two rounds per row everywhere, 3: two rows per round)
-#endif
-#ifndef ZPX_JPEGB_QSGPR
-#define ZPX_JPEGB_QSGPR 1 // (dot2) quant-pair rows by scalar loads from the frame descriptor, no LDS table
-#endif
-#ifndef ZPX_JPEGB_SCHED
-#define ZPX_JPEGB_SCHED 0 // 1: scheduling barriers between the 1-D transforms of the pair IDCT (at 116 VGPRs
-                          // they no longer pay: without, 107 VGPRs and 0.6 % faster int8, A/B x3)
-#endif
-#if ZPX_JPEGB_SCHED
-#define ZPX_JPEGB_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define ZPX_JPEGB_SCHED_BARRIER() ((void)0)
-#endif
-#ifndef ZPX_JPEGB_ROUNDS16
-#define ZPX_JPEGB_ROUNDS16 1 // int16 instances: 4 = the row in 4 rounds through a 512-byte tile (their 8 KiB
-                             // coefficient image leaves room for 12 waves per CU only so): 2.07 ms against 1.47 at 8 waves
-#endif
-#ifndef ZPX_JPEGB_DMA_NT
-#define ZPX_JPEGB_DMA_NT 2 // non-temporal coefficient DMA: 0 never, 1 always, 2 for the in-lane (4:4:4)
-                           // and int16 instances (alternating A/B: 4:4:4 1.90 -> 1.85 ms, int16
-                           // 1.398 -> 1.378; int8 4:2:0 1% slower with it)
-#endif
-#ifndef ZPX_JPEGB_XCD_REMAP
-#define ZPX_JPEGB_XCD_REMAP 1 // consecutive tasks on one XCD (0: round-robin)
-#endif
-#ifndef ZPX_JPEGB_STORE_AUX
-#define ZPX_JPEGB_STORE_AUX 2 // cache policy of the RGBA stores (2 = nt; whole lines per instruction)
-#endif
-
-#ifndef ZPX_JPEGB_DOT2
-#define ZPX_JPEGB_DOT2 1 // row IDCT stages 1-2 as v_dot2 over packed (coef * q) pairs (0: 32-bit dequant + idct_row)
-#endif
+// Fixed design choices, each measured against its alternative (DESIGN.md
+// 4.1a "Measured and rejected"):
+//   - waves per EU: 3 for the int8 instances (<= 168 VGPRs, no scratch), 2
+//     for int16 (at 3 they spill);
+//   - 4:4:4 chroma blocks stay in their lanes (32 VGPRs) instead of an LDS
+//     tile: 16 waves per CU instead of 8;
+//   - the coefficient DMA runs one pass ahead (two: slower at either
+//     occupancy), non-temporal for the in-lane and int16 instances (4:4:4
+//     1.90 -> 1.85 ms, int16 1.398 -> 1.378; int8 4:2:0 1 % slower with it);
+//   - RGBA rows leave through a 2 KiB LDS row tile, as non-temporal
+//     whole-line stores (two half-line stores per lane: 1.35 / 1.72 ms
+//     against 1.26);
+//   - workgroups renumbered so that one XCD holds consecutive tasks (1.7 %).
+constexpr int kWavesPerEu8 = 3, kWavesPerEu16 = 2;
+constexpr int kStoreAux = 2; // nt
 
 // Samples stay in the signed domain (sample - 128, the IDCT's clamp range
 // before its level shift): the +128 costs nothing folded into the colour
@@ -163,62 +116,7 @@ __device__ __forceinline__ void glds16(const void *src, const void *lds_base)
                      : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
 }
 
-// s[k] = coef[k] * q[k] (natural order), lane j's block from the LDS image
-template <typename CoefT>
-__device__ __forceinline__ void dequant_block(const uint8_t *img, int j, const int32_t *q, int32_t s[64])
-{
-    using I = CoefImage<CoefT>;
-    constexpr int PER = 16 / static_cast<int>(sizeof(CoefT)); // coefficients per piece
-    // one piece at a time: its 16 bytes and its PER table values are read
-    // together (one LDS wait per piece), then multiplied
-#pragma unroll
-    for (int pc = 0; pc < I::P; pc++) {
-        const u32x4 w = *reinterpret_cast<const u32x4 *>(img + 16 * I::slot(j, pc));
-        i32x4 qv[PER / 4];
-#pragma unroll
-        for (int i = 0; i < PER / 4; i++) qv[i] = *reinterpret_cast<const i32x4 *>(q + pc * PER + 4 * i);
-#pragma unroll
-        for (int kk = 0; kk < PER; kk++) {
-            const int k = pc * PER + kk; // coefficient index
-            if constexpr (sizeof(CoefT) == 1) {
-                // |coef| < 2^7, q < 2^17: the 24-bit multiply is exact
-                s[k] = __mul24(static_cast<int32_t>(w[kk >> 2] << (24 - 8 * (kk & 3))) >> 24, qv[kk >> 2][kk & 3]);
-            } else {
-                s[k] = __mul24(static_cast<int32_t>(w[kk >> 1] << (16 - 16 * (kk & 1))) >> 16, qv[kk >> 2][kk & 3]);
-            }
-            // materialize the product here: otherwise hipcc sinks the
-            // multiplies into the IDCT and keeps all 64 table values live
-            asm volatile("" : "+v"(s[k]));
-        }
-    }
-}
-
-// 2-D IDCT of one block in registers: rows (idct.zig:79-145), then columns
-// with level shift and clamp (idct.zig:148-200, decoder.zig:1622-1628).
-template <bool NARROW>
-__device__ __forceinline__ void idct_block(int32_t s[64])
-{
-    // (scheduling barriers between the 1-D transforms: interleaving them
-    // buys ILP the other resident waves already provide, and costs the
-    // registers that push the kernel into scratch)
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        idct_row<NARROW>(s + 8 * r);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-        __builtin_amdgcn_sched_barrier(0);
-        int32_t t[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
-        idct_col_clamp<NARROW, true>(t);
-#pragma unroll
-        for (int i = 0; i < 8; i++) s[8 * i + c] = t[i];
-    }
-}
-
-// ---- row IDCT over packed pairs (ZPX_JPEGB_DOT2) -------------------------
+// ---- row IDCT over packed pairs -------------------------------------------
 // Stages 1 and 2 of idct.zig's row pass (:99-120) are rotations of pairs of
 // dequantized coefficients: x4' = x8 + (W1-W7)x4 with x8 = W7(x4+x5) is
 // W1*x4 + W7*x5 exactly (no rounding between), and likewise for the other
@@ -254,16 +152,10 @@ __device__ __forceinline__ uint32_t pk_mul16(uint32_t a, uint32_t b)
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, a) * __builtin_bit_cast(v2u16, b));
 }
 
-// Quant-pair table of one component: per row r, four dwords holding
-// (q[r][1], q[r][7]), (q[r][5], q[r][3]), (q[r][2], q[r][6]), (q[r][0], q[r][4])
-// as u16 pairs (natural order; tables are at most 16-bit, decoder.zig:629-666).
-__device__ __forceinline__ uint32_t qpair(const int32_t *q, int i)
-{
-    constexpr int lo[4] = {1, 5, 2, 0}, hi[4] = {7, 3, 6, 4};
-    const int r = i >> 2, k = i & 3;
-    return (static_cast<uint32_t>(q[8 * r + lo[k]]) & 0xffffu) | static_cast<uint32_t>(q[8 * r + hi[k]]) << 16;
-}
-
+// Quant-pair rows (DevJpegFrame::qp, built by the host): per row r, four
+// dwords holding (q[r][1], q[r][7]), (q[r][5], q[r][3]), (q[r][2], q[r][6]),
+// (q[r][0], q[r][4]) as u16 pairs (natural order; tables are at most 16-bit,
+// decoder.zig:629-666).
 // The coefficient pairs of row r, in the qpair order, sign-extended to i16.
 // int8: a piece holds rows 2k and 2k+1 (natural order, 8 bytes a row); the
 // v_perm sign selectors reach the odd bytes of a dword, so the even
@@ -327,11 +219,11 @@ __device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT
         o[5] = (x0 - x4) >> 8;
         o[6] = (x3 - x2) >> 8;
         o[7] = (x7 - x1) >> 8;
-        ZPX_JPEGB_SCHED_BARRIER();
     }
+    // (no scheduling barriers between the 1-D transforms: at 107 VGPRs
+    // hipcc's interleaving is 0.6 % faster than keeping them apart)
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-        ZPX_JPEGB_SCHED_BARRIER();
         int32_t t[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
@@ -402,18 +294,13 @@ __device__ __forceinline__ void static_for(F &&f)
 }
 
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 2 ? ZPX_JPEGB_WAVES_PER_EU16 : ZPX_JPEGB_WAVES_PER_EU)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 2 ? kWavesPerEu16 : kWavesPerEu8)))
 void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int tasks_per_frame, int total_tasks)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
     constexpr int T = 64 / H0;                                  // MCUs per task
-    constexpr bool kInLane = ZPX_JPEGB_INLANE && !kGray && HC == H0 && VC == V0; // chroma block (x, y) <-> luma block (x, y)
-    // rounds of the RGBA row tile (ZPX_JPEGB_STORE_LDS 1 / 2): 1 = the 2 KiB
-    // tile; int16 with an LDS chroma tile takes ZPX_JPEGB_ROUNDS16
-    constexpr int kRounds = ZPX_JPEGB_STORE_LDS == 2 ? 2
-                            : (ZPX_JPEGB_STORE_LDS == 1 && sizeof(CoefT) == 2 && !kGray && !kInLane) ? ZPX_JPEGB_ROUNDS16
-                                                                                                    : 1;
-    static_assert(kRounds == 1 || kRounds == 2 || kRounds == 4, "row tile rounds");
+    constexpr bool kInLane = !kGray && HC == H0 && VC == V0; // chroma block (x, y) <-> luma block (x, y)
+    constexpr bool kDmaNt = kInLane || sizeof(CoefT) == 2;    // non-temporal coefficient DMA
     constexpr int CBW = kGray ? 1 : T * HC;                     // chroma blocks across a task, per component
     constexpr int CBH = kGray ? 1 : VC;
     constexpr int NCB = kGray ? 0 : 2 * CBW * CBH;              // chroma blocks of a task
@@ -431,24 +318,22 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     };
     constexpr auto yrow = [](int p) { return kGray ? p : kInLane ? p / 3 : p - CP; };
 
-#if ZPX_JPEGB_DOT2 && ZPX_JPEGB_QSGPR
-    // (quant-pair tables come from the frame descriptor: DevJpegFrame::qp)
-#elif ZPX_JPEGB_DOT2
-    __shared__ __attribute__((aligned(16))) uint32_t qs[3][32]; // Y, Cb, Cr quant-pair tables (qpair)
-#else
-    __shared__ __attribute__((aligned(16))) int32_t qs[3][64]; // Y, Cb, Cr (natural order)
-#endif
-    // coefficient images: DEPTH passes in flight (int8: the DMA runs two
-    // passes ahead, int16 one -- LDS per wave stays within the occupancy
-    // the registers allow)
-    constexpr int IMG = 64 * 64 * static_cast<int>(sizeof(CoefT));
-    constexpr int DEPTH = (ZPX_JPEGB_DEPTH2 && sizeof(CoefT) == 1 && NP >= 2) ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) uint8_t cimg[DEPTH * IMG];
+    // (quant-pair rows come from the frame descriptor, DevJpegFrame::qp, by
+    // scalar loads: no LDS table, 16 waves per CU for int8 4:2:0)
+    constexpr int IMG = 64 * 64 * static_cast<int>(sizeof(CoefT)); // the pass's coefficient image
+    __shared__ __attribute__((aligned(16))) uint8_t cimg[IMG];
     __shared__ __attribute__((aligned(16))) uint8_t ctile[2][CTILE];
-#if ZPX_JPEGB_STORE_LDS
-    __shared__ __attribute__((aligned(16))) uint8_t otile[kRounds > 1 ? 2048 / kRounds : ZPX_JPEGB_STORE_LDS == 3 ? 4096 : 2048]; // output row(s) of the task (512 RGBA px each)
-#endif
+    // one output row of the task (512 RGBA pixels), as 128 16-byte slots;
+    // slot s lives at slot s ^ ((s >> 3) & 1), so that both the lanes'
+    // 32-byte-strided writes (ds_write_b128: groups of 8 lanes, banks mod 32)
+    // and the 16-byte reads of the whole-line stores (ds_read_b128: the 4
+    // 16-lane groups, banks mod 64) are conflict-free
+    __shared__ __attribute__((aligned(16))) uint8_t otile[2048];
     const int lane = threadIdx.x;
+    // row tile: lane's two 16-byte pixel groups are slots 2 lane, 2 lane + 1;
+    // it reads back slots lane and 64 + lane (see otile)
+    const uint32_t wa0 = 16u * ((2u * lane) ^ ((lane >> 2) & 1u)), wa1 = 16u * ((2u * lane + 1u) ^ ((lane >> 2) & 1u));
+    const uint32_t ra = 16u * (static_cast<uint32_t>(lane) ^ ((lane >> 3) & 1u));
 
     // per-frame uniform values, read once per frame change (frame fields
     // read inside the loop compile to vector loads whose vmcnt waits would
@@ -522,22 +407,6 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         }
         return b;
     };
-    auto load_q = [&](int f) __attribute__((always_inline)) {
-        const DevJpegFrame &fr = frames[f];
-#if ZPX_JPEGB_DOT2 && ZPX_JPEGB_QSGPR
-        (void)fr;
-        return;
-#elif ZPX_JPEGB_DOT2
-#pragma unroll
-        for (int i = lane; i < 3 * 32; i += 64) qs[i >> 5][i & 31] = qpair(fr.qt[i >> 5], i & 31);
-#else
-#pragma unroll
-        for (int i = lane; i < 3 * 64; i += 64) qs[i >> 6][i & 63] = fr.qt[i >> 6][i & 63];
-#endif
-        wave_lds_order();
-    };
-
-#if ZPX_JPEGB_XCD_REMAP
     // workgroups are dealt to the 8 XCDs round-robin: renumber them so that
     // the waves of one XCD hold consecutive task indices (neighbouring tasks
     // share an XCD's L2)
@@ -547,14 +416,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         const int q = nw / 8, r = nw % 8, x = w % 8;
         task = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
     }
-#else
-    int task = blockIdx.x;
-#endif
     if (task >= total_tasks) return;
     const int tstride = static_cast<int>(gridDim.x);
     int f, my, mx0;
     coords(task, f, my, mx0);
-    load_q(f);
     TaskSrc ts = task_src(f);
     // one pass's 64 blocks -> cimg (LDS-DMA, see CoefImage).  DMA
     // instruction k carries blocks B*k .. B*k+B-1, which lie in one grid row
@@ -578,37 +443,26 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             const int last = row_ok ? gw - 1 : 0;
             const int bx = min(mx0_ * hh + b0.cx + lane % I::B, last);
             const int q = (lane / I::B + I::P - (I::P == 8 ? k : 0)) % I::P;
-            glds16<ZPX_JPEGB_DMA_NT == 1 || (ZPX_JPEGB_DMA_NT == 2 && (kInLane || sizeof(CoefT) == 2))>(row + static_cast<uint32_t>(bx * BYTES + 16 * q),
-                                                                           img + 1024 * k);
+            glds16<kDmaNt>(row + static_cast<uint32_t>(bx * BYTES + 16 * q), img + 1024 * k);
         }
     };
     // vmcnt bookkeeping (the DMA is inline asm, so the kernel counts it):
-    // S(p) stores per pass, L DMA instructions per pass; the image of pass p
-    // was issued DEPTH passes earlier, and at pass p's start the operations
-    // issued after it are the intervening passes' stores and DMAs.
-    constexpr int L = CoefImage<CoefT>::P;
-    constexpr int kRowStores = kRounds == 4 ? 4 : 2; // store instructions per pixel row
-    constexpr auto S = [=](int p) { return kind(((p % NP) + NP) % NP) == 0 ? 8 * kRowStores : 0; };
-    constexpr auto vm_wait = [=](int p) { return DEPTH == 2 ? S(p - 2) + L + S(p - 1) : S(p - 1); };
-    // the loop head expects the steady state: the first DEPTH images in
-    // flight, each followed by the previous task's stores it would have seen
-    // (dropped stores: empty range, distinct offsets)
+    // S(p) stores per pass; the image of pass p was issued one pass earlier,
+    // and at pass p's start the operations issued after it are that pass's
+    // stores.
+    constexpr auto S = [=](int p) { return kind(((p % NP) + NP) % NP) == 0 ? 16 : 0; }; // 8 rows x 2 stores
+    constexpr auto vm_wait = [=](int p) { return S(p - 1); };
+    // the loop head expects the steady state: the first image in flight,
+    // followed by the previous task's stores it would have seen (dropped
+    // stores: empty range, distinct offsets)
     const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
     auto pad_stores = [&](int n) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 32; i++)
-            if (i < n) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, ZPX_JPEGB_STORE_AUX);
+            if (i < n) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, kStoreAux);
     };
-    if constexpr (DEPTH == 2) {
-        issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
-        pad_stores(S(NP - 2));
-        issue_pass(ts, my, mx0, std::integral_constant<int, 1>{}, cimg + IMG);
-        pad_stores(S(NP - 1));
-    } else {
-        issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
-        pad_stores(S(NP - 1));
-    }
-    int cur = 0; // image of the current pass
+    issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
+    pad_stores(S(NP - 1));
     uint32_t cbr[kInLane ? 16 : 1], crr[kInLane ? 16 : 1]; // in-lane chroma samples (bytes)
     (void)cbr;
     (void)crr;
@@ -635,7 +489,6 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<void *>(static_cast<uintptr_t>(oa_hi << 32 | oa_lo)), 0,
             __builtin_amdgcn_readfirstlane(rows_here * static_cast<int>(ostride)), 0x00020000);
-        const int xpix = (mx0 * H0 + lane) * 8; // first pixel column of the lane's luma block
         const bool y_present = ts.g[0] != nullptr;
 
         static_for<NP>([&](auto P) __attribute__((always_inline)) {
@@ -644,26 +497,17 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             // this pass's image has landed: the DMA was followed by the
             // previous pass's stores only (16 after a luma pass)
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(vm_wait(p)) : "memory");
-            uint8_t *const img = cimg + (DEPTH == 2 ? cur * IMG : 0);
-#if ZPX_JPEGB_DOT2
             u32x4 raw[CoefImage<CoefT>::P];
-            load_raw<CoefT>(img, lane, raw);
-#else
-            dequant_block<CoefT>(img, lane, &qs[pass_block(P, lane).comp][0], s);
-#endif
+            load_raw<CoefT>(cimg, lane, raw);
             // every lane's reads of the image are done before the DMA refills it
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // pass p + DEPTH's coefficients load while this pass (and the next) computes
-            constexpr int pn = p + DEPTH;
+            // pass p + 1's coefficients load while this pass computes
+            constexpr int pn = p + 1;
             if constexpr (pn < NP)
-                issue_pass(ts, my, mx0, std::integral_constant<int, pn>{}, img);
+                issue_pass(ts, my, mx0, std::integral_constant<int, pn>{}, cimg);
             else
-                issue_pass(tsn, myn, mxn, std::integral_constant<int, pn - NP>{}, img);
-            if constexpr (DEPTH == 2) cur ^= 1;
-#ifndef ZPX_JPEGB_TIMING_NO_IDCT // timing-only builds (wrong pixels): cost breakdown
-#if ZPX_JPEGB_DOT2
+                issue_pass(tsn, myn, mxn, std::integral_constant<int, pn - NP>{}, cimg);
             static_assert(NARROW, "the pair IDCT needs |coef * q| <= 16384");
-#if ZPX_JPEGB_QSGPR
             {
                 // the pass's component(s): one for luma / in-lane passes, and
                 // for a chroma pass Cb in lanes < kCb, Cr above (4:2:0, 4:2:2)
@@ -683,18 +527,6 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     }
                 }, s);
             }
-#else
-            idct_block_pairs<CoefT>(raw, [&](int r) __attribute__((always_inline)) {
-                return *reinterpret_cast<const u32x4 *>(&qs[pass_block(P, lane).comp][4 * r]);
-            }, s);
-#endif
-#else
-            idct_block<NARROW>(s);
-#endif
-#else
-#pragma unroll
-            for (int i = 0; i < 64; i++) s[i] &= 0xff;
-#endif
 
             if constexpr (kind(p) == 1) {
                 // chroma block -> tile (never-scanned component: samples 0)
@@ -772,84 +604,29 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                             cr = sbyte(cs[u >> 2][1], u & 3);
                             if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) t = ct[u];
                         }
-#ifndef ZPX_JPEGB_TIMING_NO_COLOR
                         px[x] = rgba_pixel<COLOR>(s[8 * y + x], cb, cr, t);
-#else
-                        px[x] = static_cast<uint32_t>(s[8 * y + x]) ^ cb ^ (cr << 8) ^ static_cast<uint32_t>(t.r);
-#endif
                     }
                     const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
                     // (the host sends only frames with 16-byte aligned rows and
                     // W % 4 == 0: a 4-pixel piece is wholly inside or outside)
-#if ZPX_JPEGB_STORE_LDS == 3
-                    // two rows through a 4 KiB tile: four 1 KiB stores a round
-                    *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
-                    *reinterpret_cast<u32x4 *>(otile + 2048 * (y & 1) + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
-                    if (y & 1) {
-                        wave_lds_order();
-                        u32x4 v[4];
-#pragma unroll
-                        for (int i = 0; i < 4; i++) v[i] = *reinterpret_cast<const u32x4 *>(otile + 1024 * i + 16 * lane);
-                        wave_lds_order();
-                        const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int xx = (i & 1) ? xb : xa;
-                            const uint32_t ro = rowoff - ((i >> 1) ? 0u : ostride);
-                            __builtin_amdgcn_raw_buffer_store_b128(v[i], orsrc, xx < W ? ro + static_cast<uint32_t>(xx) * 4 : kDrop,
-                                                                   0, ZPX_JPEGB_STORE_AUX);
-                        }
-                    }
-#elif ZPX_JPEGB_STORE_LDS
-                    if constexpr (kRounds > 1) {
-                    // the row's 512 pixels in kRounds rounds through a 2048 / kRounds byte
-                    // tile: 64 / kRounds lanes write theirs, 128 / kRounds lanes store 16 B each
-                    constexpr int TB = 2048 / kRounds, LPR = 64 / kRounds;
-#pragma unroll
-                    for (int h = 0; h < kRounds; h++) {
-                        if (lane / LPR == h) {
-                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane % LPR)) = u32x4{px[0], px[1], px[2], px[3]};
-                            *reinterpret_cast<u32x4 *>(otile + 32 * (lane % LPR) + 16) = u32x4{px[4], px[5], px[6], px[7]};
-                        }
-                        wave_lds_order();
-                        const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + (16 * lane) % TB);
-                        wave_lds_order();
-                        const int xa = mx0 * H0 * 8 + (512 / kRounds) * h + 4 * lane;
-                        const bool mine = 16 * lane < TB;
-                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, mine && xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
-                                                               0, ZPX_JPEGB_STORE_AUX);
-                    }
-                    } else {
-                    // the row's 512 pixels through a 2 KiB LDS row tile: each
-                    // store instruction then writes 1 KiB contiguous (whole lines)
-                    *reinterpret_cast<u32x4 *>(otile + 32 * lane) = u32x4{px[0], px[1], px[2], px[3]};
-                    *reinterpret_cast<u32x4 *>(otile + 32 * lane + 16) = u32x4{px[4], px[5], px[6], px[7]};
+                    // the row's 512 pixels through the LDS row tile (swizzled,
+                    // see otile): each store instruction then writes 1 KiB
+                    // contiguous (whole lines)
+                    *reinterpret_cast<u32x4 *>(otile + wa0) = u32x4{px[0], px[1], px[2], px[3]};
+                    *reinterpret_cast<u32x4 *>(otile + wa1) = u32x4{px[4], px[5], px[6], px[7]};
                     wave_lds_order(); // (cross-lane: keep hipcc from reordering around it)
-                    const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + 16 * lane);
-                    const u32x4 vb = *reinterpret_cast<const u32x4 *>(otile + 1024 + 16 * lane);
+                    const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + ra);
+                    const u32x4 vb = *reinterpret_cast<const u32x4 *>(otile + 1024 + ra);
                     wave_lds_order();
                     const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
                     __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
-                                                           0, ZPX_JPEGB_STORE_AUX);
+                                                           0, kStoreAux);
                     __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, xb < W ? rowoff + static_cast<uint32_t>(xb) * 4 : kDrop,
-                                                           0, ZPX_JPEGB_STORE_AUX);
-                    }
-#else
-                    const uint32_t o0 = xpix < W ? rowoff + static_cast<uint32_t>(xpix) * 4 : kDrop;
-                    const uint32_t o1 = xpix + 4 < W ? rowoff + static_cast<uint32_t>(xpix) * 4 + 16 : kDrop;
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{px[0], px[1], px[2], px[3]}, orsrc, o0, 0,
-                                                           ZPX_JPEGB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{px[4], px[5], px[6], px[7]}, orsrc, o1, 0,
-                                                           ZPX_JPEGB_STORE_AUX);
-#endif
+                                                           0, kStoreAux);
                 }
             }
         });
         if (!more) break;
-        if (fn != f) {
-            wave_lds_order(); // every dequant of this task has read qs
-            load_q(fn);
-        }
         if constexpr (CP > 0) wave_lds_order(); // the tile's reads precede the next task's writes
         task = tn;
         f = fn;
@@ -862,20 +639,8 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 } // namespace
 
 namespace {
-int block_cu_count()
-{
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess)
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        n = cus;
-    }
-    return n;
-}
-
 // resident one-wave workgroups on the device for one kernel instance
-// (occupancy API: registers + LDS), capped by ZPX_JPEGB_WAVES_PER_CU (A/B runs)
+// (occupancy API: registers + LDS)
 template <typename K>
 int resident_waves(K kernel)
 {
@@ -885,8 +650,7 @@ int resident_waves(K kernel)
     // tasks, so a SIMD holding one wave more than the others would set the
     // launch's end (9 waves per CU ran 4:4:4 int16 22 % slower than 8)
     if (per_cu > 4) per_cu &= ~3;
-    if (const char *e = getenv("ZPX_JPEGB_WAVES_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
-    return block_cu_count() * per_cu;
+    return device_cu_count() * per_cu;
 }
 
 template <typename CoefT, int H0, int V0, int HC, int VC, int COLOR>

@@ -3,6 +3,7 @@
 // split: scans always accumulate into coefficient grids and no pixel is
 // produced here.  References are to src/jpeg/decoder.zig unless noted.
 #include "jpeg_host.h"
+#include "host_cpus.h"
 
 #include <hip/hip_runtime.h>
 
@@ -792,17 +793,20 @@ int Decoder::sos(int32_t n)
     o_.mxx = mxx;
     o_.myy = myy;
     if (o_.sparse.valid) return kSparseAbort; // a second scan after a record scan: redo with grids
-    const bool records = sparse_ok_ && !seen_sos_ && !o_.progressive && ns == 3 && o_.n_comp == 3 &&
-                         !(threads_ > 1 && restart_interval_ > 0);
+    bool records = sparse_ok_ && !seen_sos_ && !o_.progressive && ns == 3 && o_.n_comp == 3 &&
+                   !(threads_ > 1 && restart_interval_ > 0);
     seen_sos_ = true;
+    int32_t bpm = 0;
+    for (int k = 0; k < ns; k++) bpm += o_.comp[scan[k].id].h * o_.comp[scan[k].id].v;
+    const size_t nrec = size_t(mxx) * size_t(myy) * size_t(bpm);
+    // every coefficient costs at least two bits of entropy-coded data, plus
+    // one DC entry per block; never more than dense int16
+    const size_t bound = std::min(3 * (4 * len_ + nrec), nrec * (64 * 3));
+    // the device reads every 64th record's byte offset as a uint32: a frame
+    // whose records could pass 4 GiB takes grids
+    if (bound > size_t(UINT32_MAX)) records = false;
     if (records) {
         JpegSparse &sp = o_.sparse;
-        int32_t bpm = 0;
-        for (int k = 0; k < ns; k++) bpm += o_.comp[scan[k].id].h * o_.comp[scan[k].id].v;
-        const size_t nrec = size_t(mxx) * size_t(myy) * size_t(bpm);
-        // every coefficient costs at least two bits of entropy-coded data, plus
-        // one DC entry per block; never more than dense int16
-        const size_t bound = std::min(3 * (4 * len_ + nrec), nrec * (64 * 3));
         if (!sp.counts.alloc(nrec, false) || !sp.data.alloc(bound, false)) return ZPX_E_OUT_OF_MEMORY;
         sp.cap = bound;
         sp.nrec = sp.bytes = 0;
@@ -1213,8 +1217,7 @@ int jpeg_huff_threads()
 {
     static const int n = [] {
         if (const char *e = getenv("ZPX_HUFF_THREADS")) return std::max(1, atoi(e));
-        const unsigned hw = std::thread::hardware_concurrency();
-        return static_cast<int>(std::min(8u, hw ? hw : 1u));
+        return std::min(8, host_cpu_budget());
     }();
     return n;
 }

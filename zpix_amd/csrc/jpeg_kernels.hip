@@ -18,6 +18,7 @@
 #include "device_types.h"
 #include "jpeg_idct.h"
 #include "kernels.h"
+#include "options.h"
 
 namespace zpx {
 namespace {
@@ -535,29 +536,27 @@ int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, i
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-namespace {
-int cu_count()
+int device_cu_count()
 {
-    static int n = 0;
-    if (n == 0) {
+    static const int n = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess)
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        n = cus;
-    }
+        return cus > 0 ? cus : 256;
+    }();
     return n;
 }
 
-// Resident workgroups per CU for one kernel instance: the occupancy API
-// (registers + LDS), capped by ZPX_JPEG_WG_PER_CU when set (A/B runs).
+namespace {
+// Resident workgroups on the device for one kernel instance: the occupancy
+// API (registers + LDS).
 template <typename K>
 int persistent_workgroups(K kernel)
 {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu < 1)
         per_cu = 4;
-    if (const char *e = getenv("ZPX_JPEG_WG_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
-    return cu_count() * per_cu;
+    return device_cu_count() * per_cu;
 }
 
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
@@ -626,11 +625,8 @@ int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int 
                      int vc, int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, hipStream_t stream)
 {
     // the block-per-lane kernel (jpeg_block_kernels.hip) takes the common
-    // frames; ZPX_JPEG_KERNEL=strip forces the strip kernel (A/B runs)
-    static const bool strip_only = [] {
-        const char *e = getenv("ZPX_JPEG_KERNEL");
-        return e && e[0] == 's';
-    }();
+    // frames; the test switch "jpeg_strip" forces the strip kernel
+    const bool strip_only = opt(Opt::JpegStrip) != 0;
     if (vec_out && !strip_only) {
         const int rc = launch_jpeg_block(d_frames, n_frames, color, h0, v0, hc, vc, max_mxx, max_myy, coeff_bits,
                                          narrow, stream);

@@ -25,6 +25,10 @@ int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int
                       int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream);
 
 // png_kernels.hip
+// CUs of the current device (read once: the node's GPUs are alike; a
+// function-local static, so concurrent first calls from the per-device
+// pipeline threads are safe)
+int device_cu_count();
 int png_chunk_bytes(int depth);
 // uint64 granules of boundary buffer per band for rows of up to max_row_bytes
 int png_band_granules(int depth, uint32_t max_row_bytes);

@@ -109,10 +109,7 @@ int launch_png_adam7_merge(int obpx, const DevAdam7Merge *d_jobs, int njobs, uin
     // about 32,768 blocks in all, a block per even row of an image at a time
     // (64 x 4K RGBA16: 1.59 ms; 8,192 blocks 1.60, 2,048 1.62; RGBA8 0.82 /
     // 0.91 / 0.85)
-    static const uint32_t total = [] {
-        const char *e = getenv("ZPX_A7_BLOCKS"); // (A/B runs)
-        return e && atoi(e) > 0 ? static_cast<uint32_t>(atoi(e)) : 32768u;
-    }();
+    constexpr uint32_t total = 32768u;
     uint32_t per = (total + static_cast<uint32_t>(njobs) - 1) / static_cast<uint32_t>(njobs);
     per = per < max_erows ? per : max_erows;
     const dim3 grid(per, static_cast<uint32_t>(njobs));

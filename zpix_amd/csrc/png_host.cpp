@@ -5,6 +5,7 @@
 // (the reference uses Zig std.compress.flate; inflate is lossless, so the
 // bytes are identical).
 #include "png_host.h"
+#include "host_cpus.h"
 
 #include "crc32_fast.h"
 #include "inflate_fast.h"
@@ -421,8 +422,7 @@ int png_inflate_threads()
 {
     static const int n = [] {
         if (const char *e = getenv("ZPX_INFLATE_THREADS")) return std::max(1, atoi(e));
-        const unsigned hw = std::thread::hardware_concurrency();
-        return static_cast<int>(std::min(8u, hw ? hw : 1u));
+        return std::min(8, host_cpu_budget());
     }();
     return n;
 }

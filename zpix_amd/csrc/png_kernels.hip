@@ -917,40 +917,13 @@ __global__ void png_ctl_kernel(uint32_t *ctl)
     ctl[2] = 0;
 }
 
-int png_waves_per_cu()
-{
-    static int n = 0;
-    if (n == 0) {
-        const char *e = getenv("ZPX_PNG_WAVES_PER_CU");
-        n = e ? atoi(e) : 8;
-        if (n < 1) n = 1;
-        if (n > 32) n = 32;
-    }
-    return n;
-}
-
-int cus()
-{
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, c = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        n = c;
-    }
-    return n;
-}
+// persistent grid: 8 waves per CU (3, 4, 6, 12, 16, 24 measured slower or
+// equal)
+constexpr int kPngWavesPerCu = 8;
 
 } // namespace
 
-uint32_t png_default_spin_limit()
-{
-    static const uint32_t n = [] {
-        const char *e = getenv("ZPX_PNG_SPIN_LIMIT");
-        const long v = e ? atol(e) : 0;
-        return v > 0 ? static_cast<uint32_t>(v) : static_cast<uint32_t>(ZPX_PNG_SPIN_LIMIT);
-    }();
-    return n;
-}
+uint32_t png_default_spin_limit() { return static_cast<uint32_t>(ZPX_PNG_SPIN_LIMIT); }
 
 namespace {
 
@@ -958,16 +931,11 @@ template <int DEPTH>
 void launch_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl, uint64_t *boundary,
               uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
 {
-    static const bool trace = getenv("ZPX_BATCH_TRACE") != nullptr;
-    if (trace) fprintf(stderr, "[zpx png] launch depth %d nsched %u\n", DEPTH, nsched);
-    const uint32_t want = static_cast<uint32_t>(cus() * png_waves_per_cu());
+    const uint32_t want = static_cast<uint32_t>(device_cu_count() * kPngWavesPerCu);
     const uint32_t grid = nsched < want ? nsched : want;
-    if (trace) fprintf(stderr, "[zpx png] grid %u; ctl kernel\n", grid);
     hipLaunchKernelGGL(png_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
-    if (trace) fprintf(stderr, "[zpx png] unfilter kernel\n");
     hipLaunchKernelGGL((png_unfilter_kernel<DEPTH>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl, boundary,
                        band_granules, spin_limit ? spin_limit : png_default_spin_limit());
-    if (trace) fprintf(stderr, "[zpx png] launched\n");
 }
 
 } // namespace

@@ -632,19 +632,16 @@ template <int DEPTH, bool TRNS>
 void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
                    uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
 {
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        const char *e = getenv("ZPX_PNG_WAVES_PER_CU");
+    // resident waves per CU from the occupancy API (one per instance: a
+    // function-local static, initialised once even from concurrent threads)
+    static const int per_cu = [] {
         int occ = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH, TRNS>, 64, 0) != hipSuccess ||
             occ < 1)
             occ = 4;
-        per_cu = e ? atoi(e) : occ;
-        if (per_cu < 1) per_cu = 1;
-    }
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t want = static_cast<uint32_t>(cus * per_cu);
+        return occ;
+    }();
+    const uint32_t want = static_cast<uint32_t>(device_cu_count() * per_cu);
     const uint32_t grid = nsched < want ? nsched : want;
     hipLaunchKernelGGL(png_pair_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
     hipLaunchKernelGGL((png_pair_kernel<DEPTH, TRNS>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl,

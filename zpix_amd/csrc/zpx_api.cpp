@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -67,6 +68,10 @@ extern "C" void zpx_ctx_destroy(zpx_ctx *ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->scratch_ev) {
+        (void)hipEventSynchronize(ctx->scratch_ev);
+        (void)hipEventDestroy(ctx->scratch_ev);
+    }
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     delete ctx;
 }
@@ -1183,6 +1188,21 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
         return ZPX_E_HIP;
     }
     return ZPX_OK;
+}
+
+namespace zpx {
+namespace {
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}}; // JpegStrip, JpegSparse, PngPair, QoiSegment
+const char *const kOptNames[static_cast<int>(Opt::Count)] = {"jpeg_strip", "jpeg_sparse", "png_pair", "qoi_segment"};
+} // namespace
+int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
+} // namespace zpx
+
+extern "C" int zpx_debug_option(const char *name, int value)
+{
+    for (int i = 0; name && i < static_cast<int>(Opt::Count); i++)
+        if (strcmp(name, kOptNames[i]) == 0) return g_opt[i].exchange(value);
+    return -1;
 }
 
 extern "C" int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds)
