@@ -495,16 +495,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
                 __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, ZPX_RGBA_STORE_AUX);
             }
         } else {
+            // rows only dword aligned (e.g. 4094-wide frames at stride 4W) or
+            // a width % 4 != 0: whole chunks still leave as one 16-byte store
+            // (dword-aligned; the memory system splits it), and only a row's
+            // last, partial chunk as dwords.  Cached, not non-temporal: a
+            // non-temporal store that covers part of a 16-byte piece goes to
+            // HBM on its own (4-byte nt stores: 5.95 ms for 64 4094x4096
+            // frames)
 #pragma unroll
             for (int it = 0; it < OUT_IT; it++) {
                 const int q = min(it * G + tid, CHUNKS - 1);
                 const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
                 const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
+                const int x = X0 + cx;
+                const uint32_t o = row * ostride + static_cast<uint32_t>(x) * 4;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, x + 3 < W ? o : kDrop, 0, 0);
+                const bool part = x < W && x + 3 >= W; // 1..3 pixels of the chunk inside the row
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const uint32_t off = X0 + cx + e < W ? row * ostride + (X0 + cx + e) * 4 : kDrop;
-                    __builtin_amdgcn_raw_buffer_store_b32(v[e], rsrc, off, 0, ZPX_RGBA_STORE_AUX);
-                }
+                for (int e = 0; e < 3; e++)
+                    __builtin_amdgcn_raw_buffer_store_b32(v[e], rsrc, part && x + e < W ? o + 4 * e : kDrop, 0, 0);
             }
         }
         group_sync<G>(); // tile / row buffer reused by the next strip
