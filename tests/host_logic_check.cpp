@@ -3,9 +3,11 @@
 //   - png_schedule (api_internal.h): every band's predecessor in its pass holds
 //     a lower ticket (the kernels' no-deadlock rule), and tickets go longest
 //     row first;
-//   - png_adam7_stage / png_adam7_rebase: passes 1-6 redirected into
-//     disjoint, aligned staging rows with xf = yf = 1, pass 7 untouched, and
-//     merge jobs whose stage pointers and strides match the redirected passes;
+//   - png_adam7_stage / png_adam7_rebase: passes 1-5 redirected into
+//     disjoint, aligned staging rows with xf = yf = 1, passes 6-7 untouched,
+//     pass 6 pointing at a merge job whose stage pointers and strides match
+//     the redirected passes, and png_plan_bands putting pass 6's bands (and
+//     only those) in the second launch's schedule;
 //   - dev_jpeg_frame: the quant-pair tables of the block kernel's row pass.
 // Prints "ok" and exits 0, or names the first failed check and exits 1.
 #include <cstdio>
@@ -75,13 +77,28 @@ int main()
     }
     check_schedule(passes, 128);
     check_schedule(passes, 64);
+    {
+        std::vector<DevPngPass> p = passes;
+        const PngBandPlan bp = png_plan_bands(ZPX_PNG_TCA16, true, p, rowbytes);
+        CHECK(bp.sched.size() + bp.sched2.size() == bp.nbands);
+        // passes 6 and 7: 2048 rows each of the 4K image, 23 and 22 of the 77x45 one
+        CHECK(bp.sched2.size() == 2 * 16 + 2);
+        for (const DevPngBand &b : bp.sched) CHECK(p[b.pass].merge == nullptr && !p[b.pass].launch2);
+        std::map<uint32_t, uint32_t> next_band;
+        for (size_t t = 0; t < bp.sched2.size(); t++) {
+            const DevPngPass &d = p[bp.sched2[t].pass];
+            CHECK(d.launch2 && d.yf == 2 && ((d.xf == 2 && d.merge != nullptr) || (d.xf == 1 && d.merge == nullptr)));
+            CHECK(bp.sched2[t].band == next_band[bp.sched2[t].pass]++); // band order within a pass
+            if (t > 0) CHECK(p[bp.sched2[t - 1].pass].row_bytes >= d.row_bytes); // pass 7 (longest) first
+        }
+    }
 
-    CHECK(st.jobs.size() == 2);
-    CHECK(st.staged.size() == 12);
-    CHECK(st.max_erows == 2048);
+    CHECK(st.jobs.size() == 2 && st.merge_pass.size() == 2);
+    CHECK(st.staged.size() == 10);
     std::vector<uint8_t> staging(st.bytes + 256);
     uint8_t *base = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(staging.data()) + 255) & ~uintptr_t(255));
-    png_adam7_rebase(passes, st, base);
+    std::vector<DevAdam7Merge> jobs_dev(2);
+    png_adam7_rebase(passes, st, base, jobs_dev.data());
     // staged passes: contiguous, aligned, disjoint rows inside the staging area
     std::vector<std::pair<uint8_t *, uint8_t *>> spans;
     for (size_t i : st.staged) {
@@ -95,16 +112,20 @@ int main()
     for (size_t a = 0; a < spans.size(); a++)
         for (size_t b = a + 1; b < spans.size(); b++)
             CHECK(spans[a].second <= spans[b].first || spans[b].second <= spans[a].first);
-    // pass 7 of each Adam7 image still writes the odd rows of the image
+    // passes 6 and 7 of each Adam7 image still write the image: pass 7 the
+    // odd rows, pass 6 (merging) the even ones
     for (int k = 0; k < 2; k++) {
         const DevPngPass &p7 = passes[first_of[k] + 6];
-        CHECK(p7.xo == 0 && p7.yo == 1 && p7.xf == 1 && p7.yf == 2 && p7.out == fake_out.data());
+        CHECK(p7.xo == 0 && p7.yo == 1 && p7.xf == 1 && p7.yf == 2 && p7.out == fake_out.data() && !p7.merge);
+        const DevPngPass &p6 = passes[first_of[k] + 5];
+        CHECK(p6.xo == 1 && p6.yo == 0 && p6.xf == 2 && p6.yf == 2 && p6.out == fake_out.data());
+        CHECK(p6.merge == jobs_dev.data() + k);
     }
     // merge jobs name the same staging rows as the redirected passes, by Adam7 pass
     for (int k = 0; k < 2; k++) {
         const DevAdam7Merge &m = st.jobs[k];
-        CHECK(m.width == imgs[k].w && m.height == imgs[k].h && m.out == fake_out.data());
-        for (int p = 0; p < 6; p++) {
+        CHECK(m.width == imgs[k].w);
+        for (int p = 0; p < 5; p++) {
             const DevPngPass &d = passes[first_of[k] + p];
             CHECK(m.stage[p] == d.out && m.sstride[p] == d.out_stride);
         }

@@ -19,9 +19,11 @@ for p in sorted(os.listdir(base)):
                  else "png_adam7_merge" if "png_adam7_merge" in name else None)
         import re
         if short == "png_pair":  # one entry per depth template (tc8 vs the Adam7 RGBA16 line)
-            m = re.search(r"png_pair_kernel<(\d+)", name)
+            m = re.search(r"png_pair_kernel<(\d+)(?:, *\w+, *(\w+))?", name)
             if m and m.group(1) != "6":
                 short = "png_pair_d" + m.group(1)
+            if m and m.group(2) == "true":  # the Adam7 pass-6 merge launch
+                short += "_merge" if short != "png_pair" else "_d6_merge"
         if short == "jpeg_block":  # the headline instance keeps the plain key
             m = re.search(r"jpeg_block_kernel<([^>]*)>", name)
             if m and m.group(1).replace(" ", "") not in ("signedchar,true,2,2,1,1,0", "char,true,2,2,1,1,0"):

@@ -212,7 +212,8 @@ inline std::vector<DevPngBand> png_schedule(const std::vector<DevPngPass> &passe
 struct PngBandPlan {
     bool pair = false;
     uint32_t band_rows = 64, nbands = 0, granules = 0, max_rb = 0;
-    std::vector<DevPngBand> sched;
+    std::vector<DevPngBand> sched;  // first launch: every band but the Adam7 merge passes'
+    std::vector<DevPngBand> sched2; // second launch: passes 6 (merging the staged 1-5) and 7 of Adam7 images
 };
 int png_band_granules(int depth, uint32_t max_row_bytes);      // kernels.h
 bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride); // kernels.h
@@ -238,23 +239,35 @@ inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> 
     }
     b.sched = png_schedule(passes, b.band_rows);
     b.granules = static_cast<uint32_t>(png_band_granules(depth, b.max_rb));
+    // Adam7 pass 6 reads the staged passes 1-5: it runs in a second launch,
+    // with pass 7 (the longest bands, first) to fill the waves while pass 6's
+    // bands chain down the image (band order within a pass is kept by the
+    // stable partition)
+    const auto merge_band = [&](const DevPngBand &d) { return passes[d.pass].launch2 != 0; };
+    std::stable_partition(b.sched.begin(), b.sched.end(), [&](const DevPngBand &d) { return !merge_band(d); });
+    const auto cut = std::find_if(b.sched.begin(), b.sched.end(), merge_band);
+    b.sched2.assign(cut, b.sched.end());
+    b.sched.erase(cut, b.sched.end());
     return b;
 }
 
 
-// Adam7 through a staging area (png_adam7_kernels.hip): passes 1-6 of an
-// interlaced image on the paired-row kernel are unfiltered into contiguous
-// staging rows (whole-line stores), and the merge kernel then writes the
-// image's even rows whole; pass 7 (the odd rows) goes to the image directly.
-// (The in-kernel scatter it replaced: 8.10 against 6.56 ms per 64 x 4K RGBA16.)
+// Adam7 through a staging area (paired-row kernel): passes 1-5 of an
+// interlaced image are unfiltered into contiguous staging rows (whole-line
+// stores); pass 6 then writes every even row of the image whole, its odd
+// columns from its own pixels and its even columns read from the staged
+// passes (DevAdam7Merge), and pass 7 (the odd rows) goes to the image
+// directly.  Passes 6 and 7 run in a second launch of the kernel over their
+// own band schedule (PngBandPlan::sched2), so the staged rows are complete
+// and visible when pass 6 reads them.  Every row is then written once, whole: the
+// scatter of the passes xf apart into the image took 8.1 ms per 64 x 4K
+// RGBA16, staging passes 1-6 plus a merge kernel 6.5.
 struct Adam7Stage {
     std::vector<DevAdam7Merge> jobs; // stage[] relative to the staging base until png_adam7_rebase
+    std::vector<size_t> merge_pass;  // jobs[j]'s pass 6 (index into passes)
     std::vector<size_t> staged;      // the redirected passes (their `out` relative likewise)
     size_t bytes = 0;                // staging bytes
-    uint32_t max_erows = 0;          // the largest image's even rows
-    int obpx = 0;                    // output bytes per pixel (one depth per group)
 };
-inline bool png_adam7_staging_on() { return true; }
 // passes[first..] are frame f's, as png_frame_passes made them (Adam7 order,
 // empty passes skipped)
 inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPngPass> &passes, size_t first,
@@ -262,16 +275,22 @@ inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPng
 {
     static const uint32_t kA7[6][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4}, {0, 2, 2, 4}, {1, 0, 2, 2}};
     DevAdam7Merge m{};
-    m.out = f.out;
-    m.out_stride = f.out_stride;
     m.width = f.width;
-    m.height = f.height;
+    size_t p6 = ~size_t(0);
     for (size_t i = first; i < passes.size(); i++) {
         DevPngPass &d = passes[i];
         int pno = -1;
         for (int p = 0; p < 6; p++)
             if (d.xo == kA7[p][0] && d.yo == kA7[p][1] && d.xf == kA7[p][2] && d.yf == kA7[p][3]) pno = p;
-        if (pno < 0) continue; // pass 7
+        if (pno < 0) { // pass 7: the image's odd rows, second launch (beside pass 6)
+            d.launch2 = 1;
+            continue;
+        }
+        if (pno == 5) {
+            p6 = i;
+            d.launch2 = 1;
+            continue;
+        }
         const uint64_t sstride = (uint64_t(d.width) * obpx + 127) & ~uint64_t(127);
         st.bytes = (st.bytes + 255) & ~size_t(255);
         m.stage[pno] = reinterpret_cast<const uint8_t *>(static_cast<uintptr_t>(st.bytes));
@@ -283,16 +302,24 @@ inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPng
         st.staged.push_back(i);
         st.bytes += sstride * d.rows;
     }
+    if (p6 == ~size_t(0)) return; // (no pass 6: a 1-pixel-wide image, which png_pair_supported never takes)
+    // (a placeholder until png_adam7_rebase points it at the device job:
+    // png_plan_bands only needs to know which passes merge)
+    passes[p6].merge = reinterpret_cast<const DevAdam7Merge *>(static_cast<uintptr_t>(st.jobs.size() + 1));
     st.jobs.push_back(m);
-    st.max_erows = std::max(st.max_erows, (f.height + 1) / 2);
-    st.obpx = obpx;
+    st.merge_pass.push_back(p6);
 }
-inline void png_adam7_rebase(std::vector<DevPngPass> &passes, Adam7Stage &st, uint8_t *base)
+// staging at `base`, the jobs (one DevAdam7Merge each) at `jobs` on the device
+inline void png_adam7_rebase(std::vector<DevPngPass> &passes, Adam7Stage &st, uint8_t *base,
+                             const DevAdam7Merge *jobs)
 {
     for (size_t i : st.staged) passes[i].out = base + reinterpret_cast<uintptr_t>(passes[i].out);
-    for (auto &m : st.jobs)
-        for (int p = 0; p < 6; p++)
+    for (size_t j = 0; j < st.jobs.size(); j++) {
+        DevAdam7Merge &m = st.jobs[j];
+        for (int p = 0; p < 5; p++)
             m.stage[p] = m.sstride[p] ? base + reinterpret_cast<uintptr_t>(m.stage[p]) : nullptr;
+        passes[st.merge_pass[j]].merge = jobs + j;
+    }
 }
 
 } // namespace zpx

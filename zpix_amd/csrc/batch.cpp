@@ -74,7 +74,7 @@ struct Decoded {
 };
 
 struct Slot {
-    DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid, dstage; // dstage: Adam7 passes 1-6 (Adam7Stage)
+    DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid, dstage; // dstage: Adam7 passes 1-5 (Adam7Stage)
     HostBuf hdesc, hstatus; // pinned descriptor staging, PNG status word
     hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
     std::unique_ptr<Decoded> dec;
@@ -460,50 +460,52 @@ int Pipeline::issue_png(Slot &s)
     png_frame_passes(f, passes, rowbytes, bytes);
     const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W, img_stride);
     Adam7Stage a7;
-    if (pair && ps.interlace && png_adam7_staging_on()) {
+    if (pair && ps.interlace) {
         png_adam7_stage(f, static_cast<int>(ps.out_bpp), passes, 0, a7);
         HIPCHK(ctx_, s.dstage.reserve(a7.bytes));
-        png_adam7_rebase(passes, a7, s.dstage.as<uint8_t>());
     }
     const PngBandPlan bp = png_plan_bands(ps.depth, pair, passes, rowbytes);
-    const std::vector<DevPngBand> &sched = bp.sched; // output-row order (api_internal.h)
     const uint32_t granules = bp.granules;
     const uint32_t base = bp.nbands;
-    // descriptor staging: passes | sched | palette (256 zpx_color) | Adam7 merge job
+    const uint32_t ns = static_cast<uint32_t>(bp.sched.size()), ns2 = static_cast<uint32_t>(bp.sched2.size());
+    // descriptor staging: passes | sched, sched2 | palette (256 zpx_color) | Adam7 merge job
     const size_t pass_b = align_up(passes.size() * sizeof(DevPngPass));
-    const size_t sched_b = align_up(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand));
+    const size_t sched_b = align_up(std::max<size_t>(1, ns + ns2) * sizeof(DevPngBand));
     const size_t pal_b = align_up(256 * sizeof(zpx_color));
     const size_t merge_b = a7.jobs.size() * sizeof(DevAdam7Merge);
     const size_t desc_b = pass_b + sched_b + pal_b + merge_b;
+    HIPCHK(ctx_, s.ddesc.reserve(desc_b));
+    uint8_t *dd = s.ddesc.as<uint8_t>();
+    if (!a7.jobs.empty())
+        png_adam7_rebase(passes, a7, s.dstage.as<uint8_t>(),
+                         reinterpret_cast<const DevAdam7Merge *>(dd + pass_b + sched_b + pal_b));
     if (!host_reserve(s.hdesc, desc_b)) return ZPX_E_OUT_OF_MEMORY;
     uint8_t *h = static_cast<uint8_t *>(s.hdesc.ptr);
     memcpy(h, passes.data(), passes.size() * sizeof(DevPngPass));
-    if (!sched.empty()) memcpy(h + pass_b, sched.data(), sched.size() * sizeof(DevPngBand));
+    if (ns) memcpy(h + pass_b, bp.sched.data(), ns * sizeof(DevPngBand));
+    if (ns2) memcpy(h + pass_b + ns * sizeof(DevPngBand), bp.sched2.data(), ns2 * sizeof(DevPngBand));
     memcpy(h + pass_b + sched_b, ps.palette, 256 * sizeof(zpx_color));
     if (merge_b) memcpy(h + pass_b + sched_b + pal_b, a7.jobs.data(), merge_b);
-    HIPCHK(ctx_, s.ddesc.reserve(desc_b));
-    HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.ptr, h, desc_b, hipMemcpyHostToDevice, ctx_->stream));
+    HIPCHK(ctx_, hipMemcpyAsync(dd, h, desc_b, hipMemcpyHostToDevice, ctx_->stream));
     const size_t bound_b = std::max<size_t>(1, base) * granules * sizeof(uint64_t);
     if (s.dbound.bytes < bound_b) { // fresh granules carry tag 0, older than any epoch
         HIPCHK(ctx_, s.dbound.alloc(bound_b));
         HIPCHK(ctx_, hipMemsetAsync(s.dbound.ptr, 0, bound_b, ctx_->stream));
     }
-    uint8_t *dd = s.ddesc.as<uint8_t>();
-    ZPX_TRACE("png: item %d %ux%u depth %d interlace %d passes %zu bands %zu granules %u", d.item, W, H, ps.depth,
-              ps.interlace, passes.size(), sched.size(), granules);
+    ZPX_TRACE("png: item %d %ux%u depth %d interlace %d passes %zu bands %u+%u granules %u", d.item, W, H, ps.depth,
+              ps.interlace, passes.size(), ns, ns2, granules);
     const DevPngPass *dp = reinterpret_cast<const DevPngPass *>(dd);
     const DevPngBand *dsch = reinterpret_cast<const DevPngBand *>(dd + pass_b);
-    const uint32_t ns = static_cast<uint32_t>(sched.size());
     const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, dp, dsch, ns, s.dctl.as<uint32_t>(),
                                            s.dbound.as<uint64_t>(), granules, ctx_->stream)
                          : launch_png_unfilter(ps.depth, dp, dsch, ns, s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(),
                                                granules, ctx_->stream);
     if (lrc)
         return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
-    if (merge_b &&
-        launch_png_adam7_merge(a7.obpx, reinterpret_cast<const DevAdam7Merge *>(dd + pass_b + sched_b + pal_b), 1,
-                               a7.max_erows, ctx_->stream))
-        return hip_fail(ctx_, hipGetLastError(), "batch: png adam7 merge");
+    // Adam7: pass 6 merges the staged passes once the first launch is done
+    if (ns2 && launch_png_pair_merge(ps.depth, ps.use_transparent, dp, dsch + ns, ns2, s.dctl.as<uint32_t>(),
+                                     s.dbound.as<uint64_t>(), granules, ctx_->stream))
+        return hip_fail(ctx_, hipGetLastError(), "batch: png adam7 merge pass");
     HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, ctx_->stream));
     s.check_png = true;
     if (rgba_native) {

@@ -23,9 +23,12 @@ struct DevJpegFrame {
 
 // One PNG unfilter job: a (pass of a) PNG image.  Rows are processed by the
 // skewed wavefront kernel in bands of 64 rows (one row per lane).
+struct DevAdam7Merge;
 struct DevPngPass {
     const uint8_t *filtered; // first filter byte of this pass
     uint8_t *out;            // output image base
+    const DevAdam7Merge *merge; // Adam7 pass 6 on the paired-row kernel: the staged passes 1-5 it merges
+                                // into whole even rows (png_pair_kernels.hip), else null
     int32_t *max_index;      // paletted: max index seen (atomicMax), else null
     uint64_t out_stride;     // bytes between output rows of the full image
     uint32_t width;          // pixels in a pass row
@@ -36,18 +39,18 @@ struct DevPngPass {
     uint32_t band_base;      // index of this pass's first band in the progress table
     uint8_t trns[6];         // tRNS colour key (raw bytes)
     uint8_t use_trns;
-    uint8_t pad;
+    uint8_t launch2; // paired-row kernel: the band runs in the group's second launch (Adam7 passes 6-7)
 };
 
-// Adam7 merge job of one interlaced image (png_adam7_kernels.hip): passes
-// 1-6 unfiltered into staging rows (stage[p], sstride[p] bytes apart) are
-// gathered into the even rows of the image.
+// Adam7 on the paired-row kernel, per interlaced image: passes 1-5 are
+// unfiltered into staging rows (stage[p], sstride[p] bytes apart; together
+// the even-row, even-column quarter of the image), and pass 6 -- the odd
+// columns of the even rows -- writes every even row whole, taking its even
+// columns from them (png_pair_kernels.hip, flush_merge).
 struct DevAdam7Merge {
-    uint8_t *out;             // image base
-    uint64_t out_stride;      // bytes between image rows
-    uint32_t width, height;   // image size in pixels
-    const uint8_t *stage[6];  // passes 1-6 (null when empty)
-    uint32_t sstride[6];      // staging row stride of each pass
+    const uint8_t *stage[5];  // passes 1-5 (null when empty)
+    uint32_t sstride[5];      // staging row stride of each pass
+    uint32_t width;           // image width in pixels
 };
 
 // A scheduled band: which pass and which band in it.  Bands are ordered so

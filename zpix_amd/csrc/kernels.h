@@ -47,11 +47,11 @@ bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width,
 // trns: the images carry a tRNS colour key (RGB8 / RGB16; one value per launch)
 int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
                     uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit = 0);
+// the second launch of an Adam7 group: its pass-6 bands (sched), merged with
+// the staged passes 1-5 into whole even rows (the 4- and 8-byte-pixel depths)
+int launch_png_pair_merge(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
+                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s);
 
-// color_kernels.hip
-// Adam7 even rows from the staged passes 1-6 (obpx 4 or 8); max_erows =
-// the largest image's even rows
-int launch_png_adam7_merge(int obpx, const DevAdam7Merge *d_jobs, int njobs, uint32_t max_erows, hipStream_t s);
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);
 int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s);
 int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,

@@ -5,6 +5,12 @@
 // output bytes: RGB8 (RGBA / NRGBA with a colour key), RGBA8, Gray8, Gray16,
 // RGB16 (RGBA64 / NRGBA64 with a colour key), RGBA16.
 //
+// Adam7 (api_internal.h, Adam7Stage): passes 1-5 are unfiltered into
+// staging rows, pass 7 into the image's odd rows -- both contiguous -- and
+// pass 6, in a second launch, writes every even row whole: its own pixels
+// at the odd columns, the even columns read from the staged passes
+// (flush_merge).  No pass scatters pixels xf apart into the image.
+//
 // Work layout.  A wave owns a band of 128 rows of one pass: lane j holds rows
 // 2j (low 16-bit half of every register) and 2j+1 (high half), so one VALU
 // instruction reconstructs a byte of each.  Rows are cut into chunks of CB
@@ -177,30 +183,20 @@ __device__ __forceinline__ v4u expand_chunk(const DevPngPass &ps, const uint32_t
     }
 }
 
-// chunk k's 16 output bytes into output row `orow` of the pass (pixels xf apart)
+// chunk k's 16 output bytes into a contiguous output row
 template <int DEPTH>
-__device__ __forceinline__ void put_chunk(const DevPngPass &ps, gu8 *orow, int k, v4u v)
+__device__ __forceinline__ void put_chunk(gu8 *orow, int k, v4u v)
 {
-    using T = PairTraits<DEPTH>;
-    if (ps.xf == 1) {
-        *gptr<v4u>(orow + static_cast<size_t>(k) * 16) = v;
-    } else {
-#pragma unroll
-        for (int u = 0; u < T::C; u++) {
-            gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u) * ps.xf + ps.xo) * T::OBPX;
-            if constexpr (T::OBPX == 8) *gptr<v2u>(d) = v2u{v[2 * u], v[2 * u + 1]};
-            else *gptr<uint32_t>(d) = v[u];
-        }
-    }
+    *gptr<v4u>(orow + static_cast<size_t>(k) * 16) = v;
 }
 
-// the pixels [x0, x0 + n) of a partial last chunk (n < C), byte stores
+// the pixels [k C, k C + n) of a partial last chunk (n < C), byte stores
 template <int DEPTH>
-__device__ __forceinline__ void put_partial(const DevPngPass &ps, gu8 *orow, int k, v4u v, int n)
+__device__ __forceinline__ void put_partial(gu8 *orow, int k, v4u v, int n)
 {
     using T = PairTraits<DEPTH>;
     for (int u = 0; u < n; u++) {
-        gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u) * ps.xf + ps.xo) * T::OBPX;
+        gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u)) * T::OBPX;
         for (int i = 0; i < T::OBPX; i++) {
             const int byte = u * T::OBPX + i;
             d[i] = static_cast<uint8_t>(v[byte >> 2] >> ((byte & 3) * 8));
@@ -208,6 +204,41 @@ __device__ __forceinline__ void put_partial(const DevPngPass &ps, gu8 *orow, int
     }
 }
 
+// ---- Adam7 pass 6 (xo 1, xf 2, yo 0, yf 2) merged with the staged passes
+// 1-5 (`interlacing`, png/decoder.zig:59-67; mergePassInto :1289-1373): the
+// staged pixel at even column x = 2p of even image row y, by pass
+//   y % 4 == 2: pass 5 (xo 0, xf 2, yo 2, yf 4), column p;
+//   p odd:      pass 4 (xo 2, xf 4, yo 0, yf 4), column p / 2;
+//   y % 8 == 4: pass 3 (xo 0, xf 4, yo 4, yf 8), column p / 2;
+//   else:       pass 1 (xo 0, xf 8) or 2 (xo 4, xf 8), column p / 4.
+struct A7Src {
+    const uint8_t *stage[5];
+    uint32_t sstride[5];
+    uint32_t width; // image pixels
+};
+template <int OBPX>
+__device__ __forceinline__ const ZPX_GLOBAL uint8_t *a7_even(const A7Src &a, uint32_t p, uint32_t y)
+{
+    const bool p5 = (y & 2) != 0, p4 = !p5 && (p & 1), p3 = !p5 && !p4 && (y & 4), p2 = !p5 && !p4 && !p3 && (p & 2);
+    const uint8_t *b = p5 ? a.stage[4] : p4 ? a.stage[3] : p3 ? a.stage[2] : p2 ? a.stage[1] : a.stage[0];
+    const uint32_t st = p5 ? a.sstride[4] : p4 ? a.sstride[3] : p3 ? a.sstride[2] : p2 ? a.sstride[1] : a.sstride[0];
+    const uint32_t row = (p5 || p4) ? y >> 2 : y >> 3;
+    const uint32_t col = p5 ? p : (p4 || p3) ? p >> 1 : p >> 2;
+    return (const ZPX_GLOBAL uint8_t *)(b + static_cast<uint64_t>(row) * st + static_cast<uint64_t>(col) * OBPX);
+}
+// one pixel's OBPX bytes (4 or 8) as dwords
+template <int OBPX>
+__device__ __forceinline__ v2u a7_load(const ZPX_GLOBAL uint8_t *src)
+{
+    if constexpr (OBPX == 8) return *reinterpret_cast<const ZPX_GLOBAL v2u *>(src);
+    else return v2u{*reinterpret_cast<const ZPX_GLOBAL uint32_t *>(src), 0u};
+}
+template <int OBPX>
+__device__ __forceinline__ void a7_store(gu8 *dst, v2u v)
+{
+    if constexpr (OBPX == 8) *gptr<v2u>(dst) = v;
+    else *gptr<uint32_t>(dst) = v[0];
+}
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 __device__ __forceinline__ Rsrc make_rsrc(const void *base, uint32_t bytes)
 {
@@ -296,7 +327,7 @@ constexpr int kSc1 = 16;
 // an offset every buffer access drops (stores) or reads as zero (loads)
 constexpr int kOOR = 0x7ffffff0;
 
-template <int DEPTH, bool TRNS>
+template <int DEPTH, bool TRNS, bool MERGE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__restrict__ sched, uint32_t nsched,
                      uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit)
@@ -327,6 +358,20 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
 #endif
         const DevPngPass ps = passes[bd.pass];
         const uint32_t rb = ps.row_bytes;
+        // Adam7 pass 6 (the only strided pass this kernel takes), in the
+        // instance of the group's second launch (MERGE): its registers stay
+        // out of the other instances; pass 7 shares that launch
+        const bool merge = MERGE && ps.merge != nullptr;
+        A7Src a7{};
+        if (merge) {
+            const DevAdam7Merge &m = *ps.merge;
+#pragma unroll
+            for (int p = 0; p < 5; p++) {
+                a7.stage[p] = m.stage[p];
+                a7.sstride[p] = m.sstride[p];
+            }
+            a7.width = m.width;
+        }
         const int nchunks = static_cast<int>(((rb + BPP - 1) / BPP + C - 1) / C);
         const int nfull = static_cast<int>(ps.width / C); // chunks whose pixels are all inside the row
         const uint32_t base = bd.band * 128;
@@ -449,30 +494,39 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + (k & (kSlots - 1)) * 4]);
                 store(post, r * static_cast<int>(orow_bytes), k, v);
             };
-#ifndef ZPX_PNG_TIMING_NO_SCATTER // timing-only builds (wrong pixels): Adam7 passes stored as if contiguous
-            if (ps.xf == 1) { // contiguous rows: one 16-byte store per chunk
-#else
-            if (true) {
-#endif
+            if (!merge) { // contiguous rows: one 16-byte store per chunk
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     round(i, [&](bool post, int ro, int k, v4u v) {
                         __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc, post ? ro + k * 16 : kOOR, 0, 0);
                     });
-            } else { // Adam7 pass: pixels xf apart
+            } else if constexpr (MERGE) { // Adam7 pass 6: 32 contiguous bytes per lane, whole lines per lane group
+                // every round's staged pixels first (their loads in flight together), then the stores
+                v2u e[16][C];
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int r = 8 * i + (lane >> 3);
+                    const bool post = blk[i] != 0xffffu;
+                    const uint32_t k = (post ? blk[i] : 0u) * 8 + (lane & 7);
+                    const uint32_t y = post ? 2 * (base + r) : 0u; // (row 0, pixel 0: a valid address)
+#pragma unroll
+                    for (int u = 0; u < C; u++)
+                        e[i][u] = a7_load<T::OBPX>(a7_even<T::OBPX>(a7, post ? k * C + u : 0u, y));
+                }
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     round(i, [&](bool post, int ro, int k, v4u v) {
-#pragma unroll
-                        for (int u = 0; u < C; u++) {
-                            const int xo =
-                                static_cast<int>((static_cast<uint32_t>(k * C + u) * ps.xf + ps.xo) * T::OBPX);
-                            if constexpr (T::OBPX == 8)
-                                __builtin_amdgcn_raw_buffer_store_b64(v2u{v[2 * u], v[2 * u + 1]}, out_rsrc,
-                                                                      post ? ro + xo : kOOR, 0, 0);
-                            else
-                                __builtin_amdgcn_raw_buffer_store_b32(v[u], out_rsrc, post ? ro + xo : kOOR, 0, 0);
+                        v4u lo, hi;
+                        if constexpr (T::OBPX == 8) {
+                            lo = v4u{e[i][0][0], e[i][0][1], v[0], v[1]};
+                            hi = v4u{e[i][1][0], e[i][1][1], v[2], v[3]};
+                        } else {
+                            lo = v4u{e[i][0][0], v[0], e[i][1][0], v[1]};
+                            hi = v4u{e[i][2][0], v[2], e[i][3][0], v[3]};
                         }
+                        const int o = ro + k * 32;
+                        __builtin_amdgcn_raw_buffer_store_b128(lo, out_rsrc, post ? o : kOOR, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(hi, out_rsrc, post ? o + 16 : kOOR, 0, 0);
                     });
             }
         };
@@ -599,10 +653,47 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             const int fl = h ? fl1 : fl0;
             gu8 *orow = h ? out1 : out0;
             const int rbase = h ? ring1 : ring0;
-            for (int k = fl * 8; k < nchunks; k++) {
-                const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
-                if (k < nfull) put_chunk<DEPTH>(ps, orow, k, v);
-                else put_partial<DEPTH>(ps, orow, k, v, static_cast<int>(ps.width) - k * C);
+            if (merge) {
+                // the row's last (< 16) chunks with their staged pixels, 4
+                // chunks at a time (their loads in flight together), then an
+                // odd width's last column, which is a staged pixel
+                const uint32_t y = 2 * (base + 2 * lane + h);
+                for (int k0 = fl * 8; k0 < nchunks; k0 += 4) {
+                    v2u te[4][C];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int k = k0 + j;
+                        const int n = k < nfull ? C : static_cast<int>(ps.width) - k * C; // (<= 0 past the row)
+#pragma unroll
+                        for (int u = 0; u < C; u++)
+                            te[j][u] = a7_load<T::OBPX>(a7_even<T::OBPX>(a7, u < n ? static_cast<uint32_t>(k * C + u) : 0u,
+                                                                         u < n ? y : 0u));
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int k = k0 + j;
+                        if (k >= nchunks) break;
+                        const int n = k < nfull ? C : static_cast<int>(ps.width) - k * C;
+                        const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
+                        for (int u = 0; u < n; u++) {
+                            gu8 *d = orow + static_cast<size_t>(2 * (k * C + u)) * T::OBPX;
+                            a7_store<T::OBPX>(d, te[j][u]);
+                            if constexpr (T::OBPX == 8) a7_store<8>(d + 8, v2u{v[2 * u], v[2 * u + 1]});
+                            else a7_store<4>(d + 4, v2u{v[u], 0u});
+                        }
+                    }
+                }
+                if (a7.width & 1) {
+                    const uint32_t p = ps.width;
+                    a7_store<T::OBPX>(orow + static_cast<size_t>(2 * p) * T::OBPX,
+                                      a7_load<T::OBPX>(a7_even<T::OBPX>(a7, p, y)));
+                }
+            } else {
+                for (int k = fl * 8; k < nchunks; k++) {
+                    const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
+                    if (k < nfull) put_chunk<DEPTH>(orow, k, v);
+                    else put_partial<DEPTH>(orow, k, v, static_cast<int>(ps.width) - k * C);
+                }
             }
         }
         wave_lds_sync();
@@ -628,7 +719,7 @@ __global__ void png_pair_ctl_kernel(uint32_t *ctl)
     ctl[2] = 0;
 }
 
-template <int DEPTH, bool TRNS>
+template <int DEPTH, bool TRNS, bool MERGE = false>
 void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
                    uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
 {
@@ -636,7 +727,7 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
     // function-local static, initialised once even from concurrent threads)
     static const int per_cu = [] {
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH, TRNS>, 64, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH, TRNS, MERGE>, 64, 0) != hipSuccess ||
             occ < 1)
             occ = 4;
         return occ;
@@ -644,7 +735,7 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
     const uint32_t want = static_cast<uint32_t>(device_cu_count() * per_cu);
     const uint32_t grid = nsched < want ? nsched : want;
     hipLaunchKernelGGL(png_pair_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
-    hipLaunchKernelGGL((png_pair_kernel<DEPTH, TRNS>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl,
+    hipLaunchKernelGGL((png_pair_kernel<DEPTH, TRNS, MERGE>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl,
                        boundary, band_granules, spin_limit);
 }
 
@@ -671,6 +762,7 @@ bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width,
     default: return false;
     }
     if ((depth == ZPX_PNG_G8 || depth == ZPX_PNG_G16) && (interlace || use_trns)) return false;
+    if (interlace && width < 2) return false; // Adam7 here needs a pass 6 to merge the staged passes
     // every (non-empty) pass row holds at least one chunk's bytes (no lane's
     // group starts before the band), and a band's 128 pass rows of output
     // span less than the 2 GiB buffer range
@@ -704,6 +796,26 @@ int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPng
         else launch_pair_t<ZPX_PNG_TC16, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
         break;
     default: return -2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_png_pair_merge(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
+                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s)
+{
+    const uint32_t sl = png_default_spin_limit();
+    switch (depth) {
+    case ZPX_PNG_TCA8: launch_pair_t<ZPX_PNG_TCA8, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
+    case ZPX_PNG_TCA16: launch_pair_t<ZPX_PNG_TCA16, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
+    case ZPX_PNG_TC8:
+        if (trns) launch_pair_t<ZPX_PNG_TC8, true, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        else launch_pair_t<ZPX_PNG_TC8, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        break;
+    case ZPX_PNG_TC16:
+        if (trns) launch_pair_t<ZPX_PNG_TC16, true, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        else launch_pair_t<ZPX_PNG_TC16, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+        break;
+    default: return -2; // (Gray8 / Gray16 are never interlaced on this kernel: png_pair_supported)
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

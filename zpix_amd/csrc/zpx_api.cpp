@@ -319,9 +319,8 @@ struct PngGroup {
     bool trns = false; // (pair kernel) the images carry a tRNS colour key
     DevBuf passes, sched, scratch, boundary;
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
-    DevBuf staging, merge_jobs; // Adam7 passes 1-6 and their merge jobs (Adam7Stage)
-    int merge_n = 0, merge_obpx = 0;
-    uint32_t merge_erows = 0;
+    DevBuf staging, merge_jobs; // Adam7 passes 1-5 and pass 6's merge jobs (Adam7Stage)
+    uint32_t nsched2 = 0;       // bands of the second launch (Adam7 pass 6), after the first nsched
     size_t scratch_zero_bytes = 0;
 };
 
@@ -423,9 +422,11 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
         ctx->last_error = "png: a band of this image exceeds the kernel's 2 GiB band range";
         return ZPX_E_UNSUPPORTED;
     }
-    const std::vector<DevPngBand> &sched = bp.sched; // output-row order (api_internal.h)
+    std::vector<DevPngBand> sched = bp.sched; // longest first (api_internal.h), then the second launch's
+    sched.insert(sched.end(), bp.sched2.begin(), bp.sched2.end());
     const uint32_t base = bp.nbands;
-    g.nsched = static_cast<uint32_t>(sched.size());
+    g.nsched = static_cast<uint32_t>(bp.sched.size());
+    g.nsched2 = static_cast<uint32_t>(bp.sched2.size());
     g.nbands = base;
     g.band_bytes = bp.granules; // granules per band
     HIPCHK(ctx, g.passes.alloc(passes.size() * sizeof(DevPngPass)));
@@ -539,18 +540,14 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
             png_frame_passes(frames[idx], passes, rowbytes, bytes);
             const int obpx = png_out_bpp(frames[idx].depth, frames[idx].use_transparent != 0);
             bytes += uint64_t(frames[idx].width) * frames[idx].height * obpx;
-            if (g->pair && frames[idx].interlace && png_adam7_staging_on())
-                png_adam7_stage(frames[idx], obpx, passes, first, a7);
+            if (g->pair && frames[idx].interlace) png_adam7_stage(frames[idx], obpx, passes, first, a7);
         }
         if (!a7.jobs.empty()) {
             HIPCHK(ctx, g->staging.alloc(a7.bytes));
-            png_adam7_rebase(passes, a7, g->staging.as<uint8_t>());
             HIPCHK(ctx, g->merge_jobs.alloc(a7.jobs.size() * sizeof(DevAdam7Merge)));
+            png_adam7_rebase(passes, a7, g->staging.as<uint8_t>(), g->merge_jobs.as<DevAdam7Merge>());
             HIPCHK(ctx, hipMemcpy(g->merge_jobs.ptr, a7.jobs.data(), a7.jobs.size() * sizeof(DevAdam7Merge),
                                   hipMemcpyHostToDevice));
-            g->merge_n = static_cast<int>(a7.jobs.size());
-            g->merge_obpx = a7.obpx;
-            g->merge_erows = a7.max_erows;
         }
         if (int e = png_build_group(ctx, *g, passes, rowbytes)) return e;
         plan->png.push_back(std::move(g));
@@ -589,9 +586,12 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
                                                      g->nsched, g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(),
                                                      g->band_bytes, st);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
-        if (g->merge_n > 0 &&
-            launch_png_adam7_merge(g->merge_obpx, g->merge_jobs.as<DevAdam7Merge>(), g->merge_n, g->merge_erows, st))
-            return hip_fail(ctx, hipGetLastError(), "png adam7 merge launch");
+        // Adam7: pass 6 merges the staged passes once the first launch is done
+        if (g->nsched2 && launch_png_pair_merge(g->depth, g->trns, g->passes.as<DevPngPass>(),
+                                                g->sched.as<DevPngBand>() + g->nsched, g->nsched2,
+                                                g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes,
+                                                st))
+            return hip_fail(ctx, hipGetLastError(), "png adam7 merge pass launch");
     }
     return ZPX_OK;
 }
