@@ -3,11 +3,11 @@
 //   - png_schedule (api_internal.h): every band's predecessor in its pass holds
 //     a lower ticket (the kernels' no-deadlock rule), and tickets go longest
 //     row first;
-//   - png_adam7_stage / png_adam7_rebase: passes 1-5 redirected into
-//     disjoint, aligned staging rows with xf = yf = 1, passes 6-7 untouched,
-//     pass 6 pointing at a merge job whose stage pointers and strides match
-//     the redirected passes, and png_plan_bands putting pass 6's bands (and
-//     only those) in the second launch's schedule;
+//   - png_adam7_stage / png_adam7_rebase: passes 1-5 redirected into the
+//     quarter image Q (every Q pixel written exactly once), passes 6-7
+//     writing the image, pass 6 pointing at a merge job naming Q, and
+//     png_plan_bands putting passes 6-7 (and only those) in the second
+//     launch's schedule;
 //   - dev_jpeg_frame: the quant-pair tables of the block kernel's row pass.
 // Prints "ok" and exits 0, or names the first failed check and exits 1.
 #include <cstdio>
@@ -99,36 +99,39 @@ int main()
     uint8_t *base = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(staging.data()) + 255) & ~uintptr_t(255));
     std::vector<DevAdam7Merge> jobs_dev(2);
     png_adam7_rebase(passes, st, base, jobs_dev.data());
-    // staged passes: contiguous, aligned, disjoint rows inside the staging area
-    std::vector<std::pair<uint8_t *, uint8_t *>> spans;
-    for (size_t i : st.staged) {
-        const DevPngPass &d = passes[i];
-        CHECK(d.xf == 1 && d.yf == 1 && d.xo == 0 && d.yo == 0);
-        CHECK(d.out_stride % 128 == 0 && d.out_stride >= uint64_t(d.width) * 8);
-        CHECK((reinterpret_cast<uintptr_t>(d.out) & 255) == 0);
-        CHECK(d.out >= base && d.out + d.out_stride * d.rows <= base + st.bytes);
-        spans.push_back({d.out, d.out + d.out_stride * d.rows});
+    // passes 1-5 write the quarter image Q (pixel (2X, 2Y) at Q[Y][X]): in
+    // Q's coordinates, inside the image's own Q, and together they cover every
+    // Q pixel exactly once
+    static const uint32_t kA7[5][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4}, {0, 2, 2, 4}};
+    for (int k = 0; k < 2; k++) {
+        const DevAdam7Merge &m = st.jobs[k];
+        const uint32_t qw = (imgs[k].w + 1) / 2, qh = (imgs[k].h + 1) / 2;
+        CHECK(m.width == imgs[k].w && m.qstride % 128 == 0 && m.qstride >= uint64_t(qw) * 8);
+        CHECK((reinterpret_cast<uintptr_t>(m.q) & 255) == 0 && m.q >= base && m.q + m.qstride * qh <= base + st.bytes);
+        std::vector<int> cover(size_t(qw) * qh, 0);
+        for (int p = 0; p < 5; p++) {
+            const DevPngPass &d = passes[first_of[k] + p];
+            CHECK(d.out == m.q && d.out_stride == m.qstride && !d.launch2 && d.merge == nullptr);
+            CHECK(d.xo * 2 == kA7[p][0] && d.yo * 2 == kA7[p][1] && d.xf * 2 == kA7[p][2] && d.yf * 2 == kA7[p][3]);
+            for (uint32_t r = 0; r < d.rows; r++)
+                for (uint32_t c = 0; c < d.width; c++) {
+                    const uint32_t X = c * d.xf + d.xo, Y = r * d.yf + d.yo;
+                    CHECK(X < qw && Y < qh);
+                    if (X < qw && Y < qh) cover[size_t(Y) * qw + X]++;
+                }
+        }
+        bool once = true;
+        for (int c : cover) once &= c == 1;
+        CHECK(once);
     }
-    for (size_t a = 0; a < spans.size(); a++)
-        for (size_t b = a + 1; b < spans.size(); b++)
-            CHECK(spans[a].second <= spans[b].first || spans[b].second <= spans[a].first);
     // passes 6 and 7 of each Adam7 image still write the image: pass 7 the
-    // odd rows, pass 6 (merging) the even ones
+    // odd rows, pass 6 (merging Q) the even ones
     for (int k = 0; k < 2; k++) {
         const DevPngPass &p7 = passes[first_of[k] + 6];
         CHECK(p7.xo == 0 && p7.yo == 1 && p7.xf == 1 && p7.yf == 2 && p7.out == fake_out.data() && !p7.merge);
         const DevPngPass &p6 = passes[first_of[k] + 5];
         CHECK(p6.xo == 1 && p6.yo == 0 && p6.xf == 2 && p6.yf == 2 && p6.out == fake_out.data());
-        CHECK(p6.merge == jobs_dev.data() + k);
-    }
-    // merge jobs name the same staging rows as the redirected passes, by Adam7 pass
-    for (int k = 0; k < 2; k++) {
-        const DevAdam7Merge &m = st.jobs[k];
-        CHECK(m.width == imgs[k].w);
-        for (int p = 0; p < 5; p++) {
-            const DevPngPass &d = passes[first_of[k] + p];
-            CHECK(m.stage[p] == d.out && m.sstride[p] == d.out_stride);
-        }
+        CHECK(p6.merge == jobs_dev.data() + k && p6.launch2 && p7.launch2);
     }
 
     // ---- quant-pair tables of dev_jpeg_frame

@@ -252,20 +252,22 @@ inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> 
 }
 
 
-// Adam7 through a staging area (paired-row kernel): passes 1-5 of an
-// interlaced image are unfiltered into contiguous staging rows (whole-line
-// stores); pass 6 then writes every even row of the image whole, its odd
-// columns from its own pixels and its even columns read from the staged
-// passes (DevAdam7Merge), and pass 7 (the odd rows) goes to the image
-// directly.  Passes 6 and 7 run in a second launch of the kernel over their
-// own band schedule (PngBandPlan::sched2), so the staged rows are complete
-// and visible when pass 6 reads them.  Every row is then written once, whole: the
-// scatter of the passes xf apart into the image took 8.1 ms per 64 x 4K
-// RGBA16, staging passes 1-6 plus a merge kernel 6.5.
+// Adam7 through a staging area (paired-row kernel).  The pixels of passes
+// 1-5 are exactly those with an even row and an even column: they are
+// unfiltered into the quarter image Q[Y][X] = pixel (2X, 2Y) -- pass 5 its
+// odd rows whole, passes 1-4 its even rows, 2 or 4 pixels apart -- and pass
+// 6 then writes every even row y of the image whole: its own pixels at the
+// odd columns, row y / 2 of Q at the even ones (16-byte loads, whole lines).
+// Pass 7 writes the odd rows directly.  Passes 6 and 7 run in a second
+// launch of the kernel over their own band schedule (PngBandPlan::sched2),
+// so Q is complete and visible when pass 6 reads it.  Every row of the
+// image is then written once, whole: the scatter of all passes xf apart
+// into the image took 8.1 ms per 64 x 4K RGBA16, staging passes 1-6 plus a
+// merge kernel 6.5.
 struct Adam7Stage {
-    std::vector<DevAdam7Merge> jobs; // stage[] relative to the staging base until png_adam7_rebase
+    std::vector<DevAdam7Merge> jobs; // q relative to the staging base until png_adam7_rebase
     std::vector<size_t> merge_pass;  // jobs[j]'s pass 6 (index into passes)
-    std::vector<size_t> staged;      // the redirected passes (their `out` relative likewise)
+    std::vector<size_t> staged;      // passes writing Q (their `out` relative likewise)
     size_t bytes = 0;                // staging bytes
 };
 // passes[first..] are frame f's, as png_frame_passes made them (Adam7 order,
@@ -274,35 +276,37 @@ inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPng
                             Adam7Stage &st)
 {
     static const uint32_t kA7[6][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4}, {0, 2, 2, 4}, {1, 0, 2, 2}};
-    DevAdam7Merge m{};
-    m.width = f.width;
     size_t p6 = ~size_t(0);
+    for (size_t i = first; i < passes.size(); i++)
+        if (passes[i].xo == 1 && passes[i].xf == 2) p6 = i;
+    if (p6 == ~size_t(0)) return; // (no pass 6: a 1-pixel-wide image, which png_pair_supported never takes)
+    const uint64_t qw = (uint64_t(f.width) + 1) / 2, qh = (uint64_t(f.height) + 1) / 2;
+    const uint64_t qstride = (qw * obpx + 127) & ~uint64_t(127);
+    st.bytes = (st.bytes + 255) & ~size_t(255);
+    const size_t q = st.bytes;
+    st.bytes += qstride * qh;
+    DevAdam7Merge m{};
+    m.q = reinterpret_cast<const uint8_t *>(static_cast<uintptr_t>(q));
+    m.qstride = qstride;
+    m.width = f.width;
     for (size_t i = first; i < passes.size(); i++) {
         DevPngPass &d = passes[i];
         int pno = -1;
         for (int p = 0; p < 6; p++)
             if (d.xo == kA7[p][0] && d.yo == kA7[p][1] && d.xf == kA7[p][2] && d.yf == kA7[p][3]) pno = p;
-        if (pno < 0) { // pass 7: the image's odd rows, second launch (beside pass 6)
+        if (pno < 0 || pno == 5) { // pass 7 (the odd rows) and pass 6: the image, second launch
             d.launch2 = 1;
             continue;
         }
-        if (pno == 5) {
-            p6 = i;
-            d.launch2 = 1;
-            continue;
-        }
-        const uint64_t sstride = (uint64_t(d.width) * obpx + 127) & ~uint64_t(127);
-        st.bytes = (st.bytes + 255) & ~size_t(255);
-        m.stage[pno] = reinterpret_cast<const uint8_t *>(static_cast<uintptr_t>(st.bytes));
-        m.sstride[pno] = static_cast<uint32_t>(sstride);
-        d.out = reinterpret_cast<uint8_t *>(static_cast<uintptr_t>(st.bytes));
-        d.out_stride = sstride;
-        d.xo = d.yo = 0;
-        d.xf = d.yf = 1;
+        // passes 1-5 in Q's coordinates: (x, y) -> (x / 2, y / 2)
+        d.out = reinterpret_cast<uint8_t *>(static_cast<uintptr_t>(q));
+        d.out_stride = qstride;
+        d.xo /= 2;
+        d.yo /= 2;
+        d.xf /= 2;
+        d.yf /= 2;
         st.staged.push_back(i);
-        st.bytes += sstride * d.rows;
     }
-    if (p6 == ~size_t(0)) return; // (no pass 6: a 1-pixel-wide image, which png_pair_supported never takes)
     // (a placeholder until png_adam7_rebase points it at the device job:
     // png_plan_bands only needs to know which passes merge)
     passes[p6].merge = reinterpret_cast<const DevAdam7Merge *>(static_cast<uintptr_t>(st.jobs.size() + 1));
@@ -315,9 +319,7 @@ inline void png_adam7_rebase(std::vector<DevPngPass> &passes, Adam7Stage &st, ui
 {
     for (size_t i : st.staged) passes[i].out = base + reinterpret_cast<uintptr_t>(passes[i].out);
     for (size_t j = 0; j < st.jobs.size(); j++) {
-        DevAdam7Merge &m = st.jobs[j];
-        for (int p = 0; p < 5; p++)
-            m.stage[p] = m.sstride[p] ? base + reinterpret_cast<uintptr_t>(m.stage[p]) : nullptr;
+        st.jobs[j].q = base + reinterpret_cast<uintptr_t>(st.jobs[j].q);
         passes[st.merge_pass[j]].merge = jobs + j;
     }
 }

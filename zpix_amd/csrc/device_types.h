@@ -43,14 +43,15 @@ struct DevPngPass {
 };
 
 // Adam7 on the paired-row kernel, per interlaced image: passes 1-5 are
-// unfiltered into staging rows (stage[p], sstride[p] bytes apart; together
-// the even-row, even-column quarter of the image), and pass 6 -- the odd
-// columns of the even rows -- writes every even row whole, taking its even
-// columns from them (png_pair_kernels.hip, flush_merge).
+// unfiltered into the quarter image Q[Y][X] = pixel (2X, 2Y) -- the
+// even-row, even-column pixels, which are exactly theirs -- and pass 6 (the
+// odd columns of the even rows) writes every even row y whole, taking its
+// even columns from row y / 2 of Q (png_pair_kernels.hip).
 struct DevAdam7Merge {
-    const uint8_t *stage[5];  // passes 1-5 (null when empty)
-    uint32_t sstride[5];      // staging row stride of each pass
+    const uint8_t *q;         // Q, ceil(W / 2) x ceil(H / 2) pixels
+    uint64_t qstride;         // bytes between rows of Q
     uint32_t width;           // image width in pixels
+    uint32_t pad;
 };
 
 // A scheduled band: which pass and which band in it.  Bands are ordered so

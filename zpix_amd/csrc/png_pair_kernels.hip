@@ -41,7 +41,7 @@
 // loop is unconditional -- out-of-range offsets read zero / drop the store --
 // so s_waitcnt counts stay exact); each reconstructed chunk is expanded to
 // its 16 output bytes (colour key, 16-bit order) into a per-row LDS ring of
-// kSlots = 16 slots; every group, a fixed 16 rounds of cooperative flush
+// 2 FL slots (PairShape); every FL steps, a fixed 2 FL rounds of cooperative flush
 // store each row's newly completed aligned 8-chunk block (one 128-byte line
 // of RGBA8) with 8 lanes per row, from a transposed per-row flush state.
 // The boundary window of the band above is prefetched one group ahead and
@@ -67,8 +67,7 @@ typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gptr(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
-constexpr int kG = 8;       // steps per group (input burst, flush period)
-constexpr int kSlots = 16;  // ring slots per row: a pending block's 7 + one group's 8 chunks fit
+constexpr int kG = 8; // steps per group (input burst)
 #ifndef ZPX_PNG_SLEEP
 #define ZPX_PNG_SLEEP 2
 #endif
@@ -89,6 +88,24 @@ ZPX_PAIR_TRAITS(ZPX_PNG_TCA8, 4, 4)
 ZPX_PAIR_TRAITS(ZPX_PNG_TC16, 6, 8)
 ZPX_PAIR_TRAITS(ZPX_PNG_TCA16, 8, 8)
 #undef ZPX_PAIR_TRAITS
+
+// Flush shape of an instance: FL = chunks per flushed block = steps between
+// flushes; the ring holds 2 FL chunks a row (a pending block's FL - 1 plus
+// FL new ones), and W waves per SIMD fit its LDS (128 rows x (2 FL + 1) x
+// 16 B) and registers.  FL 8 (35 KiB of ring) leaves one wave per SIMD,
+// which issues a VOP3 only every ~5 cycles.  FL 4 (18 KiB) fits two, whose
+// instructions interleave (tools/ubench/valu_rate: 6.98 cycles each at 2
+// waves per SIMD, 1.45x the SIMD's issue rate) -- but 64 x 4K tc8 ran 2.84
+// ms that way against 2.32: with 2,048 resident waves every band of an
+// image starts at once and waits for the band above it, and the input
+// loads, 64 rows per instruction, are the limit rather than issue
+// (tools/ubench/png_load_pattern: this load shape alone reads the stream at
+// 2.2 TB/s).  So FL stays 8.
+template <int DEPTH, bool MERGE>
+struct PairShape {
+    static constexpr int FL = 8;
+    static constexpr int W = FL == 4 ? 2 : 1;
+};
 
 // ---- packed 16-bit helpers (v_pk_*_u16)
 __device__ __forceinline__ u16x2 as16(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
@@ -190,13 +207,13 @@ __device__ __forceinline__ void put_chunk(gu8 *orow, int k, v4u v)
     *gptr<v4u>(orow + static_cast<size_t>(k) * 16) = v;
 }
 
-// the pixels [k C, k C + n) of a partial last chunk (n < C), byte stores
+// the pixels [k C, k C + n) of chunk k (n <= C), xf apart, byte stores
 template <int DEPTH>
-__device__ __forceinline__ void put_partial(gu8 *orow, int k, v4u v, int n)
+__device__ __forceinline__ void put_partial(const DevPngPass &ps, gu8 *orow, int k, v4u v, int n)
 {
     using T = PairTraits<DEPTH>;
     for (int u = 0; u < n; u++) {
-        gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u)) * T::OBPX;
+        gu8 *d = orow + static_cast<size_t>(static_cast<uint32_t>(k * T::C + u) * ps.xf + ps.xo) * T::OBPX;
         for (int i = 0; i < T::OBPX; i++) {
             const int byte = u * T::OBPX + i;
             d[i] = static_cast<uint8_t>(v[byte >> 2] >> ((byte & 3) * 8));
@@ -204,27 +221,19 @@ __device__ __forceinline__ void put_partial(gu8 *orow, int k, v4u v, int n)
     }
 }
 
-// ---- Adam7 pass 6 (xo 1, xf 2, yo 0, yf 2) merged with the staged passes
-// 1-5 (`interlacing`, png/decoder.zig:59-67; mergePassInto :1289-1373): the
-// staged pixel at even column x = 2p of even image row y, by pass
-//   y % 4 == 2: pass 5 (xo 0, xf 2, yo 2, yf 4), column p;
-//   p odd:      pass 4 (xo 2, xf 4, yo 0, yf 4), column p / 2;
-//   y % 8 == 4: pass 3 (xo 0, xf 4, yo 4, yf 8), column p / 2;
-//   else:       pass 1 (xo 0, xf 8) or 2 (xo 4, xf 8), column p / 4.
+// ---- Adam7 pass 6 (xo 1, xf 2, yo 0, yf 2) merged with the quarter image Q
+// of passes 1-5 (`interlacing`, png/decoder.zig:59-67; mergePassInto
+// :1289-1373): the pixel at even column x = 2p of even image row y is
+// Q[y / 2][p].
 struct A7Src {
-    const uint8_t *stage[5];
-    uint32_t sstride[5];
+    const uint8_t *q;
+    uint64_t qstride;
     uint32_t width; // image pixels
 };
 template <int OBPX>
 __device__ __forceinline__ const ZPX_GLOBAL uint8_t *a7_even(const A7Src &a, uint32_t p, uint32_t y)
 {
-    const bool p5 = (y & 2) != 0, p4 = !p5 && (p & 1), p3 = !p5 && !p4 && (y & 4), p2 = !p5 && !p4 && !p3 && (p & 2);
-    const uint8_t *b = p5 ? a.stage[4] : p4 ? a.stage[3] : p3 ? a.stage[2] : p2 ? a.stage[1] : a.stage[0];
-    const uint32_t st = p5 ? a.sstride[4] : p4 ? a.sstride[3] : p3 ? a.sstride[2] : p2 ? a.sstride[1] : a.sstride[0];
-    const uint32_t row = (p5 || p4) ? y >> 2 : y >> 3;
-    const uint32_t col = p5 ? p : (p4 || p3) ? p >> 1 : p >> 2;
-    return (const ZPX_GLOBAL uint8_t *)(b + static_cast<uint64_t>(row) * st + static_cast<uint64_t>(col) * OBPX);
+    return (const ZPX_GLOBAL uint8_t *)(a.q + static_cast<uint64_t>(y >> 1) * a.qstride + static_cast<uint64_t>(p) * OBPX);
 }
 // one pixel's OBPX bytes (4 or 8) as dwords
 template <int OBPX>
@@ -328,18 +337,23 @@ constexpr int kSc1 = 16;
 constexpr int kOOR = 0x7ffffff0;
 
 template <int DEPTH, bool TRNS, bool MERGE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+__global__ __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(PairShape<DEPTH, MERGE>::W, PairShape<DEPTH, MERGE>::W)))
 void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__restrict__ sched, uint32_t nsched,
                      uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit)
 {
     using T = PairTraits<DEPTH>;
     constexpr int BPP = T::BPP, CB = T::CB, CW = T::CW, C = T::C;
     constexpr int GD = kG * CW + 1;         // input dwords per row per group (+1: alignbyte carry)
-    constexpr int RS = kSlots * 4 + 4;      // ring dwords per row: 16 output chunks of 16 bytes + 16 bytes of bank skew
+    constexpr int FL = PairShape<DEPTH, MERGE>::FL; // chunks per flushed block, steps between flushes
+    constexpr int kSlots = 2 * FL;          // ring slots per row
+    constexpr int RPR = 64 / FL;            // rows per flush round (FL lanes each)
+    constexpr int NR = 128 / RPR;           // flush rounds
+    constexpr int RS = kSlots * 4 + 4;      // ring dwords per row: 2 FL output chunks of 16 bytes + 16 bytes of bank skew
     constexpr int WG = kG * CW;             // boundary granules of one window (kG chunks)
     static_assert(WG % 2 == 0 && WG / 2 <= 64, "window loads are granule pairs, one per lane");
     __shared__ __attribute__((aligned(16))) uint32_t ring[128 * RS + 4]; // + a trash slot
-    __shared__ __attribute__((aligned(16))) uint32_t fst[128];           // flush state, [row % 8][row / 8]
+    __shared__ __attribute__((aligned(16))) uint32_t fst[128];           // flush state, [row % RPR][row / RPR]
     constexpr int kTrash = 128 * RS;
 
     const int lane = threadIdx.x;
@@ -365,11 +379,8 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         A7Src a7{};
         if (merge) {
             const DevAdam7Merge &m = *ps.merge;
-#pragma unroll
-            for (int p = 0; p < 5; p++) {
-                a7.stage[p] = m.stage[p];
-                a7.sstride[p] = m.sstride[p];
-            }
+            a7.q = m.q;
+            a7.qstride = m.qstride;
             a7.width = m.width;
         }
         const int nchunks = static_cast<int>(((rb + BPP - 1) / BPP + C - 1) / C);
@@ -465,64 +476,78 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             w = __builtin_amdgcn_raw_buffer_load_b128(prev_rsrc, o, 0, kSc1);
         };
 
-        // every kG steps: each row that completed an aligned block of 8 full
-        // chunks (one 128-byte line of RGBA8) posts it; in round i, lanes
-        // 8g..8g+7 store row 8i+g's posted block from the ring, one chunk each
+        // every FL steps: each row that completed an aligned block of FL full
+        // chunks (FL = 8: one 128-byte line of RGBA8) posts it; in round i,
+        // lanes FL g .. FL g + FL - 1 store row RPR i + g's posted block from
+        // the ring, one chunk each
         auto flush = [&](int t_end) {
             const int d0 = ok0 ? min(max(t_end - skew0, 0), nchunks) : 0;
             const int d1 = ok1 ? min(max(t_end - skew1, 0), nchunks) : 0;
-            const bool p0 = (min(d0, nfull) >> 3) > fl0, p1 = (min(d1, nfull) >> 3) > fl1;
-            const int r0 = 2 * lane, r1 = r0 + 1; // row r's state at fst[(r % 8) * 16 + r / 8]
-            fst[(r0 & 7) * 16 + (r0 >> 3)] = p0 ? static_cast<uint32_t>(fl0) : 0xffffu;
-            fst[(r1 & 7) * 16 + (r1 >> 3)] = p1 ? static_cast<uint32_t>(fl1) : 0xffffu;
+            const bool p0 = min(d0, nfull) / FL > fl0, p1 = min(d1, nfull) / FL > fl1;
+            const int r0 = 2 * lane, r1 = r0 + 1; // row r's state at fst[(r % RPR) * NR + r / RPR]
+            fst[(r0 % RPR) * NR + r0 / RPR] = p0 ? static_cast<uint32_t>(fl0) : 0xffffu;
+            fst[(r1 % RPR) * NR + r1 / RPR] = p1 ? static_cast<uint32_t>(fl1) : 0xffffu;
             fl0 += p0 ? 1 : 0;
             fl1 += p1 ? 1 : 0;
             wave_lds_sync();
-            uint32_t blk[16]; // this lane group's rows 8i + g, i = 0..15
+            uint32_t blk[NR]; // this lane group's rows RPR i + g, i = 0..NR-1
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const v4u v = *reinterpret_cast<const v4u *>(&fst[(lane >> 3) * 16 + 4 * q]);
+            for (int q = 0; q < NR / 4; q++) {
+                const v4u v = *reinterpret_cast<const v4u *>(&fst[(lane / FL) * NR + 4 * q]);
                 blk[4 * q] = v[0];
                 blk[4 * q + 1] = v[1];
                 blk[4 * q + 2] = v[2];
                 blk[4 * q + 3] = v[3];
             }
             auto round = [&](int i, auto &&store) __attribute__((always_inline)) {
-                const int r = 8 * i + (lane >> 3);
+                const int r = RPR * i + lane / FL;
                 const bool post = blk[i] != 0xffffu;
-                const int k = static_cast<int>(post ? blk[i] : 0u) * 8 + (lane & 7);
+                const int k = static_cast<int>(post ? blk[i] : 0u) * FL + lane % FL;
                 const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + (k & (kSlots - 1)) * 4]);
                 store(post, r * static_cast<int>(orow_bytes), k, v);
             };
-            if (!merge) { // contiguous rows: one 16-byte store per chunk
+            if (ps.xf == 1) { // contiguous rows: one 16-byte store per chunk
 #pragma unroll
-                for (int i = 0; i < 16; i++)
+                for (int i = 0; i < NR; i++)
                     round(i, [&](bool post, int ro, int k, v4u v) {
                         __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc, post ? ro + k * 16 : kOOR, 0, 0);
                     });
+            } else if (!merge) { // Adam7 passes 1-4 into Q: pixels xf (2 or 4) apart
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                    round(i, [&](bool post, int ro, int k, v4u v) {
+#pragma unroll
+                        for (int u = 0; u < C; u++) {
+                            const int xo =
+                                static_cast<int>((static_cast<uint32_t>(k * C + u) * ps.xf + ps.xo) * T::OBPX);
+                            if constexpr (T::OBPX == 8)
+                                __builtin_amdgcn_raw_buffer_store_b64(v2u{v[2 * u], v[2 * u + 1]}, out_rsrc,
+                                                                      post ? ro + xo : kOOR, 0, 0);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b32(v[u], out_rsrc, post ? ro + xo : kOOR, 0, 0);
+                        }
+                    });
             } else if constexpr (MERGE) { // Adam7 pass 6: 32 contiguous bytes per lane, whole lines per lane group
-                // every round's staged pixels first (their loads in flight together), then the stores
-                v2u e[16][C];
+                // every round's Q pixels first (one 16-byte load each, in flight together), then the stores
+                v4u e[NR];
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const int r = 8 * i + (lane >> 3);
+                for (int i = 0; i < NR; i++) {
+                    const int r = RPR * i + lane / FL;
                     const bool post = blk[i] != 0xffffu;
-                    const uint32_t k = (post ? blk[i] : 0u) * 8 + (lane & 7);
+                    const uint32_t k = (post ? blk[i] : 0u) * FL + lane % FL;
                     const uint32_t y = post ? 2 * (base + r) : 0u; // (row 0, pixel 0: a valid address)
-#pragma unroll
-                    for (int u = 0; u < C; u++)
-                        e[i][u] = a7_load<T::OBPX>(a7_even<T::OBPX>(a7, post ? k * C + u : 0u, y));
+                    e[i] = *reinterpret_cast<const ZPX_GLOBAL v4u *>(a7_even<T::OBPX>(a7, post ? k * C : 0u, y));
                 }
 #pragma unroll
-                for (int i = 0; i < 16; i++)
+                for (int i = 0; i < NR; i++)
                     round(i, [&](bool post, int ro, int k, v4u v) {
                         v4u lo, hi;
                         if constexpr (T::OBPX == 8) {
-                            lo = v4u{e[i][0][0], e[i][0][1], v[0], v[1]};
-                            hi = v4u{e[i][1][0], e[i][1][1], v[2], v[3]};
+                            lo = v4u{e[i][0], e[i][1], v[0], v[1]};
+                            hi = v4u{e[i][2], e[i][3], v[2], v[3]};
                         } else {
-                            lo = v4u{e[i][0][0], v[0], e[i][1][0], v[1]};
-                            hi = v4u{e[i][2][0], v[2], e[i][3][0], v[3]};
+                            lo = v4u{e[i][0], v[0], e[i][1], v[1]};
+                            hi = v4u{e[i][2], v[2], e[i][3], v[3]};
                         }
                         const int o = ro + k * 32;
                         __builtin_amdgcn_raw_buffer_store_b128(lo, out_rsrc, post ? o : kOOR, 0, 0);
@@ -542,7 +567,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         {
             const Rsrc none = make_rsrc(base4, 0u); // extent 0: every store is dropped
 #pragma unroll
-            for (int i = 0; i < 2 * kG + 16; i++)  // distinct, unmergeable offsets
+            for (int i = 0; i < 2 * kG + (kG / FL) * NR; i++) // distinct, unmergeable offsets
                 __builtin_amdgcn_raw_buffer_store_b32(0u, none, 4096 * i + lane * 4, 0, 0);
         }
         for (int g0 = 0; g0 < nsteps; g0 += kG) {
@@ -639,12 +664,14 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 }
                 k0++;
                 k1++;
+                if ((st + 1) % FL == 0) { // (every FL steps; st is a constant of the unrolled loop)
+                    wave_lds_sync();
+                    flush(g0 + st + 1);
+                    wave_lds_sync(); // fst is rewritten at the next flush
+                }
             }
-            wave_lds_sync();
-            flush(g0 + kG);
-            wave_lds_sync(); // fst is rewritten at the next flush
         }
-        // ---- row tails: the last (< 16) unflushed chunks, the last partial
+        // ---- row tails: the last (< 2 FL) unflushed chunks, the last partial
         gu8 *out0 = obase + static_cast<size_t>(2 * lane) * orow_bytes;
         gu8 *out1 = out0 + orow_bytes;
         for (int h = 0; h < 2; h++) {
@@ -658,7 +685,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 // chunks at a time (their loads in flight together), then an
                 // odd width's last column, which is a staged pixel
                 const uint32_t y = 2 * (base + 2 * lane + h);
-                for (int k0 = fl * 8; k0 < nchunks; k0 += 4) {
+                for (int k0 = fl * FL; k0 < nchunks; k0 += 4) {
                     v2u te[4][C];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
@@ -689,10 +716,10 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                                       a7_load<T::OBPX>(a7_even<T::OBPX>(a7, p, y)));
                 }
             } else {
-                for (int k = fl * 8; k < nchunks; k++) {
+                for (int k = fl * FL; k < nchunks; k++) {
                     const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
-                    if (k < nfull) put_chunk<DEPTH>(orow, k, v);
-                    else put_partial<DEPTH>(orow, k, v, static_cast<int>(ps.width) - k * C);
+                    if (k < nfull && ps.xf == 1) put_chunk<DEPTH>(orow, k, v);
+                    else put_partial<DEPTH>(ps, orow, k, v, k < nfull ? C : static_cast<int>(ps.width) - k * C);
                 }
             }
         }
