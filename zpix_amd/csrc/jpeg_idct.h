@@ -7,9 +7,6 @@
 
 #include <cstdint>
 
-#ifndef ZPX_COEF_NT
-#define ZPX_COEF_NT 1 // 1: non-temporal coefficient loads (read once)
-#endif
 #define ZPX_GLOBAL __attribute__((address_space(1)))
 
 namespace zpx {

@@ -24,9 +24,7 @@ namespace zpx {
 namespace {
 
 constexpr int kThreads = 256;
-#ifndef ZPX_RGBA_STORE_AUX
-#define ZPX_RGBA_STORE_AUX 2 // cache policy bits of the fused kernel's output stores (2 = nt)
-#endif
+constexpr int kStoreAux = 2; // the aligned-row RGBA stores: non-temporal (cached: 1.643 against 1.622 ms)
 constexpr int kBlkStride = 72; // dwords per 8x8 block in LDS (64 + 8 pad: conflict-free column reads)
 
 // Load one 8-coefficient row of a block (natural order) and dequantize it.
@@ -134,16 +132,10 @@ __global__ __launch_bounds__(kThreads) void jpeg_planar_kernel(const DevJpegFram
 //   P3c: 16-byte stores, a wave writes 1 KiB of one output row per instruction.
 // ---------------------------------------------------------------------------
 
-#ifndef ZPX_JPEG_GROUP
-#define ZPX_JPEG_GROUP 256 // threads that cooperate on one strip: 256 (workgroup) or 64 (one wave)
-#endif
-constexpr int kGroup = ZPX_JPEG_GROUP;
-static_assert(kGroup == 64 || kGroup == kThreads, "a strip group is one wave or the workgroup");
-// about 96 blocks per 256 threads (3 coefficient rows per lane)
-#ifndef ZPX_JPEG_STRIP_BLOCKS
-#define ZPX_JPEG_STRIP_BLOCKS 96
-#endif
-constexpr int kStripBlocks = ZPX_JPEG_STRIP_BLOCKS * kGroup / kThreads;
+// the workgroup's 256 threads share a strip of about 96 blocks (3
+// coefficient rows per lane; 48 / 64 / 128-block strips ran 17-60 % slower)
+constexpr int kGroup = kThreads;
+constexpr int kStripBlocks = 96;
 constexpr int strip_mcus(int blocks_per_mcu)
 {
     return blocks_per_mcu >= kStripBlocks ? 1 : kStripBlocks / blocks_per_mcu;
@@ -178,13 +170,9 @@ __device__ __forceinline__ void load_row_raw(const CoefT *p, RowRegs<CoefT> &r)
 {
     using A = typename RowRegs<CoefT>::A;
     const ZPX_GLOBAL A *g = (const ZPX_GLOBAL A *)p;
-#if ZPX_COEF_NT
+    // non-temporal: every coefficient is read once (cached loads: 1.646 against 1.622 ms)
     r.a = __builtin_nontemporal_load(g);
     if constexpr (sizeof(CoefT) == 4) r.b = __builtin_nontemporal_load((const ZPX_GLOBAL u32x4 *)p + 1);
-#else
-    r.a = g[0];
-    if constexpr (sizeof(CoefT) == 4) r.b = ((const ZPX_GLOBAL u32x4 *)p)[1];
-#endif
 }
 
 template <typename CoefT>
@@ -217,11 +205,9 @@ __device__ __forceinline__ void unpack_dequant(const RowRegs<CoefT> &r, const in
     }
 }
 
+// 5 waves per EU (87 VGPRs): 5 workgroups, 20 waves, per CU (4: +5 %)
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
-#ifndef ZPX_JPEG_WAVES_PER_EU
-#define ZPX_JPEG_WAVES_PER_EU 5
-#endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JPEG_WAVES_PER_EU))) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames, int strips_x,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5))) void jpeg_rgba_kernel(const DevJpegFrame *__restrict__ frames, int strips_x,
                                                              int strips_per_frame, int total_strips)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
@@ -367,7 +353,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
         }
         group_sync<G>();
 
-#ifndef ZPX_JPEG_COPY_ONLY
         // ---- P2: chroma columns -> LDS tile
         if constexpr (!kGray) {
             const bool cb_present = fr.coeffs[1] != nullptr, cr_present = fr.coeffs[2] != nullptr;
@@ -436,11 +421,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
                     const int i = i0 + j;
                     const int32_t Yv = yv[it][i];
                     uint32_t pix;
-#ifdef ZPX_JPEG_NO_COLOR // timing-only build: luma as gray, no colour math
-                    if constexpr (true) {
-#else
                     if constexpr (kGray) {
-#endif
                         pix = static_cast<uint32_t>(Yv) * 0x010101u | 0xff000000u;
                     } else if constexpr (COLOR == ZPX_JPEG_COLOR_RGB) {
                         pix = static_cast<uint32_t>(Yv) | static_cast<uint32_t>(cb) << 8 |
@@ -466,11 +447,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
             }
         }
         group_sync<G>();
-#else
-        // timing-only build: the row buffer (raw dequantized rows) is stored as
-        // the tile, so the launch moves the same bytes with no IDCT/colour work
-        uint32_t *otile = reinterpret_cast<uint32_t *>(buf);
-#endif
 
         // ---- P3c: stores of the tile through a per-strip buffer descriptor.
         // Lanes outside the image get an offset past num_records and the
@@ -492,7 +468,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ZPX_JP
                 const int row = q / (PXW / 4), cx = (q % (PXW / 4)) * 4;
                 const u32x4 v = *reinterpret_cast<const u32x4 *>(otile + row * PXW + cx);
                 const uint32_t off = X0 + cx < W ? row * ostride + (X0 + cx) * 4 : kDrop;
-                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, ZPX_RGBA_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, kStoreAux);
             }
         } else {
             // rows only dword aligned (e.g. 4094-wide frames at stride 4W) or

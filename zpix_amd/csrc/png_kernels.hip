@@ -33,41 +33,23 @@
 namespace zpx {
 namespace {
 
-#ifndef ZPX_PNG_WIN
-#define ZPX_PNG_WIN 16
-#endif
-constexpr int kRegionChunks = ZPX_PNG_WIN;
-#ifndef ZPX_PNG_GROUP
-#define ZPX_PNG_GROUP 8
-#endif
-constexpr int kGroup = ZPX_PNG_GROUP; // steps per input/output burst
-#ifndef ZPX_PNG_LDS_OUT
-#define ZPX_PNG_LDS_OUT 1
-#endif
-constexpr bool kLdsOut = ZPX_PNG_LDS_OUT != 0; // output chunks staged in an LDS ring, flushed as aligned lines
-constexpr int kOutSlots = 17;                  // 16 ring slots + 1 of padding per lane
-#ifndef ZPX_PNG_PAIR_LOADS
-#define ZPX_PNG_PAIR_LOADS 0
-#endif
-constexpr bool kPairLoads = ZPX_PNG_PAIR_LOADS != 0; // input bursts issued two groups at a time
-#ifndef ZPX_PNG_COOP_STORE
-#define ZPX_PNG_COOP_STORE 1
-#endif
-constexpr bool kCoopStore = ZPX_PNG_COOP_STORE != 0; // ring flush: 8 lanes per row, whole lines per store
-#ifndef ZPX_PNG_COOP_LOAD
-#define ZPX_PNG_COOP_LOAD 0
-#endif
-constexpr bool kCoopLoad = ZPX_PNG_COOP_LOAD != 0; // group input: 8 lanes per row load its 128-byte window
-// LDS dwords per row of the input stage: the row's window of NP 16-byte
-// pieces plus one piece of padding (4-way bank spread for the per-lane reads)
-constexpr int stage_pieces(int gd) { return (12 + 4 * gd + 15) / 16; } // window start is 16-aligned, <= 12 B early
-constexpr int stage_dw(int gd) { return stage_pieces(gd) <= 8 ? 36 : 44; }
+// Fixed choices (each measured against its alternatives):
+//   - boundary windows of 16 chunks (4 / 8 / 32: within 3 %);
+//   - groups of 8 steps: one input burst and one output flush per group
+//     (16-step groups do not unroll, and spill);
+//   - output chunks through a per-lane LDS ring (16 slots + 1 of padding),
+//     flushed as whole aligned lines by 8 lanes per row (one lane per row:
+//     4.07 ms, register bursts: 4.37, against 3.6 per 64 x 4K tc8); the
+//     cooperative line loads through LDS, paired bursts and a 12-byte raw
+//     ring were slower or equal;
+//   - 2 x 64 cycles of s_sleep between boundary polls (0 / 1: equal).
+constexpr int kRegionChunks = 16;
+constexpr int kGroup = 8;     // steps per input/output burst
+constexpr int kOutSlots = 17; // 16 ring slots + 1 of padding per lane
 #ifndef ZPX_PNG_SPIN_LIMIT
-#define ZPX_PNG_SPIN_LIMIT (1u << 20) // default polls per wait (ZPX_PNG_SPIN_LIMIT env overrides at launch)
+#define ZPX_PNG_SPIN_LIMIT (1u << 20) // default polls per wait
 #endif
-#ifndef ZPX_PNG_SLEEP
-#define ZPX_PNG_SLEEP 2 // s_sleep between boundary polls (units of 64 cycles)
-#endif
+constexpr int kSleep = 2;
 
 template <int DEPTH>
 struct Traits;
@@ -110,18 +92,9 @@ typedef uint32_t gv4 __attribute__((ext_vector_type(4)));
 typedef uint32_t gv2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gcast(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
-// Store n bytes held in dwords w[] to dst, using 16-byte stores when aligned.
-// Output stores: the image is written once and never re-read by this kernel,
-// so ZPX_PNG_NT_STORE marks them non-temporal (the L2 keeps the input lines
-// a row's next group re-reads).
-#ifndef ZPX_PNG_NT_STORE
-#define ZPX_PNG_NT_STORE 0
-#endif
-__device__ __forceinline__ void store16(ZPX_GLOBAL gv4 *p, gv4 v)
-{
-    if constexpr (ZPX_PNG_NT_STORE) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+// A 16-byte output store (cached: non-temporal ones skip the L2's write
+// combining, and each piece became its own HBM write: 11.6 against 3.6 ms)
+__device__ __forceinline__ void store16(ZPX_GLOBAL gv4 *p, gv4 v) { *p = v; }
 
 template <int NB>
 __device__ __forceinline__ void store_bytes(gu8 *dst, const uint32_t (&w)[(NB + 3) / 4])
@@ -476,23 +449,11 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     constexpr bool kGroupStore = group_store_depth<DEPTH>();
     static_assert(!kGroupStore || CW == 4 || DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TC16, "16-byte output chunks");
     static_assert(WG <= 128, "a window is two 8-byte granules per lane");
-    static_assert(!kLdsOut || G % 8 == 0, "the output ring flushes every 8 steps, 16 slots");
+    static_assert(G % 8 == 0, "the output ring flushes every 8 steps, 16 slots");
     __shared__ __attribute__((aligned(16))) uint64_t win_lds[WG];
-    // output ring (kLdsOut): 16 chunks of 16 bytes per lane, +1 slot of padding
-    // ZPX_PNG_RAW_RING=1: TC8/TC16 (12-byte chunks) keep the chunk's reconstructed bytes (3
-    // dwords) and pack them to 16 output bytes at the flush: 12.3 KB per wave
-    // instead of 17.4 KB, 12 resident waves per CU. Measured: 3.61 ms at 12
-    // waves/CU, the same as the default ring, so it stays off.
-#ifndef ZPX_PNG_RAW_RING
-#define ZPX_PNG_RAW_RING 0
-#endif
-    constexpr bool kRawRing = ZPX_PNG_RAW_RING && kLdsOut && kGroupStore && CW == 3;
-    constexpr int kRingDw = kRawRing ? 16 * CW + 1 : 4 * kOutSlots; // dwords per lane (odd stride when raw)
-    __shared__ __attribute__((aligned(16))) uint32_t out_lds[kLdsOut && kGroupStore ? 64 * kRingDw : 1];
-    // input stage (kCoopLoad): each row's 128-byte window of the next group
-    constexpr int NP = stage_pieces(GD), kStageDw = stage_dw(GD);
-    static_assert(!kCoopLoad || (NP <= 9 && (NP <= 8 || kStageDw >= 40)), "input window: 8 pieces by 8-lane groups, +1 by one round");
-    __shared__ __attribute__((aligned(16))) uint32_t in_lds[kCoopLoad ? 64 * kStageDw : 1];
+    // output ring: 16 chunks of 16 bytes per lane, +1 slot of padding
+    constexpr int kRingDw = 4 * kOutSlots; // dwords per lane
+    __shared__ __attribute__((aligned(16))) uint32_t out_lds[kGroupStore ? 64 * kRingDw : 1];
 
     const int lane = threadIdx.x;
     const uint32_t epoch = __builtin_amdgcn_readfirstlane(ctl[0]);
@@ -536,9 +497,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         // them), so a 16-byte load holding a row's last bytes is never cut by
         // the range check; loads wholly past it read zeros
         const uint8_t *band0 = ps.filtered + static_cast<size_t>(bd.band) * 64 * (rb + 1);
-        // (line-aligned for the cooperative loads, so a row's window is its lines)
-        const uintptr_t base_mask = kCoopLoad ? ~uintptr_t(127) : ~uintptr_t(3);
-        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & base_mask);
+        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
         const uint32_t delta = static_cast<uint32_t>(band0 - base4);
         const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
         const uint32_t nrec = extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent);
@@ -569,8 +528,8 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         constexpr bool kKeyWidens = DEPTH == ZPX_PNG_G8 || DEPTH == ZPX_PNG_G16;
         // Adam7 passes (xf > 1) of the 4- and 8-byte-pixel depths also go
         // through the ring: a chunk's pixels are scattered xf apart at flush
-        constexpr bool kStrided = kLdsOut && (DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TCA8 ||
-                                              DEPTH == ZPX_PNG_TC16 || DEPTH == ZPX_PNG_TCA16);
+        constexpr bool kStrided = DEPTH == ZPX_PNG_TC8 || DEPTH == ZPX_PNG_TCA8 || DEPTH == ZPX_PNG_TC16 ||
+                                  DEPTH == ZPX_PNG_TCA16;
         const bool gstore = kGroupStore && (ps.xf == 1 || kStrided) && !(kKeyWidens && ps.use_trns) &&
                             ((reinterpret_cast<uintptr_t>(ps.out) | ps.out_stride) & 15) == 0;
         // chunk k's 16 output bytes (pack_chunk16) into output row orow
@@ -590,25 +549,12 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         gu8 *out_row = (gu8 *)(ps.out + static_cast<size_t>(y * ps.yf + ps.yo) * ps.out_stride);
         // output ring slot (k & 15) of row r: write my chunk, read any row's
         auto ring_put = [&](int k, const uint32_t (&ob)[CW]) __attribute__((always_inline)) {
-            if constexpr (kRawRing) {
-#pragma unroll
-                for (int i = 0; i < CW; i++) out_lds[lane * kRingDw + (k & 15) * CW + i] = ob[i];
-            } else {
-                uint32_t w[4];
-                pack_chunk16<DEPTH, CW>(ps, ob, w);
-                *reinterpret_cast<gv4 *>(&out_lds[lane * kRingDw + (k & 15) * 4]) = gv4{w[0], w[1], w[2], w[3]};
-            }
+            uint32_t w[4];
+            pack_chunk16<DEPTH, CW>(ps, ob, w);
+            *reinterpret_cast<gv4 *>(&out_lds[lane * kRingDw + (k & 15) * 4]) = gv4{w[0], w[1], w[2], w[3]};
         };
         auto ring_get = [&](int r, int k) __attribute__((always_inline)) -> gv4 {
-            if constexpr (kRawRing) {
-                uint32_t ob[CW], w[4];
-#pragma unroll
-                for (int i = 0; i < CW; i++) ob[i] = out_lds[r * kRingDw + (k & 15) * CW + i];
-                pack_chunk16<DEPTH, CW>(ps, ob, w);
-                return gv4{w[0], w[1], w[2], w[3]};
-            } else {
-                return *reinterpret_cast<const gv4 *>(&out_lds[r * kRingDw + (k & 15) * 4]);
-            }
+            return *reinterpret_cast<const gv4 *>(&out_lds[r * kRingDw + (k & 15) * 4]);
         };
 
         uint32_t left[BPP], ul[BPP];
@@ -627,14 +573,14 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         // burst, never in two halves a group apart. Called every 8 steps, so
         // at most 15 chunks are pending and 16 slots never collide.
         auto flush_out = [&](int steps) __attribute__((always_inline)) {
-            if constexpr (kGroupStore && kLdsOut) {
+            if constexpr (kGroupStore) {
                 if (!gstore) return; // wave-uniform
                 const int done = min(steps - skew, nchunks); // chunks [0, done) reconstructed
                 const int upto = done == nchunks ? done : (done & ~7);
                 const int lo = row_ok ? flushed : 0;
                 const int hi = row_ok ? max(lo, min(upto, nfull)) : 0;
                 if (row_ok) flushed = max(flushed, upto);
-                if constexpr (kCoopStore) {
+                {
                     // Eight lanes write one row's aligned 8-chunk block: each
                     // store instruction covers 8 whole lines instead of 16 bytes
                     // of 64 lines. The block is read from the row's ring slots.
@@ -652,13 +598,6 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     }
                     for (int kf = lo + 8; kf < hi; kf++) // a row's tail past its last whole block (end of row only)
                         put_chunk(out_row, kf, ring_get(lane, kf));
-                } else {
-                    int kf = lo;
-#pragma unroll
-                    for (int i = 0; i < 8; i++, kf++)
-                        if (kf < hi) put_chunk(out_row, kf, ring_get(lane, kf));
-                    for (; kf < hi; kf++)
-                        put_chunk(out_row, kf, ring_get(lane, kf));
                 }
             }
         };
@@ -666,7 +605,6 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
         // One group: G steps from step0 over this lane's chunks k0 .. k0+G-1
         // (k0 = step0 - skew), input dwords in `in`.
         auto run_group = [&](const uint32_t (&in)[GD], int step0) {
-            uint32_t gw[kGroupStore && !kLdsOut ? G : 1][4];
 #pragma unroll
             for (int r = 0; r < G; r++) {
                 const int step = step0 + r;
@@ -714,7 +652,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                             if (lane == 0) atomicOr(status, 1u);
                             break;
                         }
-                        __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
+                        __builtin_amdgcn_s_sleep(kSleep);
                         fill_window(step - wi);
                     }
                     uint32_t gv[CW];
@@ -757,12 +695,8 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 for (int i = 0; i < CW; i++) outp[i] = ob[i];
 
                 const bool full = k < nfull;
-                if constexpr (kGroupStore && kLdsOut) {
-                    if (gstore && act && full) {
-                        ring_put(k, ob);
-                    }
-                } else if constexpr (kGroupStore) {
-                    pack_chunk16<DEPTH, CW>(ps, ob, gw[r]);
+                if constexpr (kGroupStore) {
+                    if (gstore && act && full) ring_put(k, ob);
                 }
                 if (act) {
                     if (!(gstore && full)) {
@@ -778,17 +712,6 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                     }
                 }
                 if ((r & 7) == 7) flush_out(step + 1);
-            }
-            if constexpr (kGroupStore && !kLdsOut) {
-                if (gstore) { // the group's full chunks, one contiguous burst per lane
-#pragma unroll
-                    for (int r = 0; r < G; r++) {
-                        const int k = step0 + r - skew;
-                        if (step0 + r < nsteps_of(nchunks, max_skew) && row_ok && k >= 0 && k < nchunks &&
-                            static_cast<uint32_t>(k + 1) * C <= ps.width)
-                            store16(gcast<gv4>(out_row + static_cast<size_t>(k) * 16), gv4{gw[r][0], gw[r][1], gw[r][2], gw[r][3]});
-                    }
-                }
             }
         };
 
@@ -813,82 +736,7 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
                 load_dwords<GD>(b, rsrc, off);
             }
         };
-        if constexpr (kCoopLoad) {
-            // Cooperative group loads: in round i, lanes 8j..8j+7 load row
-            // 8i+j's 128-byte window (16 bytes each), so a load instruction
-            // covers 8 rows' contiguous lines instead of 16 bytes of 64 rows.
-            // The windows go through LDS to the lane that owns the row.
-            // Row r's group starts at dword-aligned offset base_r + step0*CB.
-            int wbase[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const int r = 8 * i + (lane >> 3);
-                const int ro = static_cast<int>(delta) + r * static_cast<int>(rb + 1); // filter byte of row r
-                const int dof = ro + 1 - ((ro + 1) & 3);
-                wbase[i] = dof - __shfl(skew, r) * CB;
-            }
-            const int wmine = data_off - skew * CB; // my row's group start at step 0
-            u32x4 R[8], R8;
-            auto coop_load = [&](int step0) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    // a negative offset (a row still in its skew) must not reach
-                    // the instruction's immediate: select it out of range instead
-                    const int o = ((wbase[i] + step0 * CB) & ~15) + 16 * (lane & 7);
-                    R[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
-                }
-                if constexpr (NP > 8) { // 16-byte chunks: a ninth piece, my own row's
-                    const int o = ((wmine + step0 * CB) & ~15) + 16 * 8;
-                    R8 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o < 0 ? 0x7fffffff : o, 0, 0);
-                }
-            };
-            auto stage_in = [&](uint32_t (&b)[GD], int step0) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int r = 8 * i + (lane >> 3);
-                    *reinterpret_cast<u32x4 *>(&in_lds[r * kStageDw + 4 * (lane & 7)]) = R[i];
-                }
-                if constexpr (NP > 8) *reinterpret_cast<u32x4 *>(&in_lds[lane * kStageDw + 32]) = R8;
-                const int w = ((data_off + (step0 - skew) * CB) & 15) >> 2; // my first dword in my window
-#pragma unroll
-                for (int j = 0; j < GD; j++) b[j] = in_lds[lane * kStageDw + w + j];
-            };
-            // pipeline: group g+1's window is staged and read back into
-            // registers before group g runs (its LDS latency hides behind g),
-            // and group g+2's loads are in flight meanwhile
-            uint32_t inA[GD], inB[GD];
-            coop_load(0);
-            stage_in(inA, 0);
-            coop_load(G);
-            for (int step0 = 0; step0 < nsteps; step0 += 2 * G) {
-                stage_in(inB, step0 + G);
-                coop_load(step0 + 2 * G);
-                run_group(inA, step0);
-                if (step0 + G >= nsteps) break;
-                stage_in(inA, step0 + 2 * G);
-                coop_load(step0 + 3 * G);
-                run_group(inB, step0 + G);
-            }
-        } else if constexpr (kPairLoads) {
-            // two groups' bursts back to back: the line they share is requested
-            // twice within a few cycles and fetched from HBM once
-            uint32_t b0[GD], b1[GD], b2[GD], b3[GD];
-            load_group(b0, 0);
-            load_group(b1, G);
-            for (int step0 = 0; step0 < nsteps; step0 += 4 * G) {
-                load_group(b2, step0 + 2 * G);
-                load_group(b3, step0 + 3 * G);
-                run_group(b0, step0);
-                if (step0 + G >= nsteps) break;
-                run_group(b1, step0 + G);
-                if (step0 + 2 * G >= nsteps) break;
-                load_group(b0, step0 + 4 * G);
-                load_group(b1, step0 + 5 * G);
-                run_group(b2, step0 + 2 * G);
-                if (step0 + 3 * G >= nsteps) break;
-                run_group(b3, step0 + 3 * G);
-            }
-        } else {
+        {
             uint32_t bufA[GD], bufB[GD];
             load_group(bufA, 0);
             for (int step0 = 0; step0 < nsteps; step0 += 2 * G) {

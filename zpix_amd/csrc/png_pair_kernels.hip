@@ -68,9 +68,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gptr(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
 constexpr int kG = 8; // steps per group (input burst)
-#ifndef ZPX_PNG_SLEEP
-#define ZPX_PNG_SLEEP 2
-#endif
+constexpr int kSleep = 2; // s_sleep between boundary polls (units of 64 cycles; 0 / 1 measured equal)
 
 template <int DEPTH> struct PairTraits;
 #define ZPX_PAIR_TRAITS(D, BPP_, OBPX_)                                        \
@@ -311,24 +309,13 @@ __device__ __noinline__ Polled poll_window(Rsrc rsrc, int o, int need, uint32_t 
             if (lane == 0) atomicOr(status, 1u);
             return Polled{w, 1u};
         }
-        __builtin_amdgcn_s_sleep(ZPX_PNG_SLEEP);
+        __builtin_amdgcn_s_sleep(kSleep);
         w = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 16 /* sc1 */);
         const bool ok = (2 * lane >= need || w[1] == epoch) && (2 * lane + 1 >= need || w[3] == epoch);
         if (__ballot(!ok) == 0) return Polled{w, 0u};
     }
 }
 
-// ZPX_PNG_TRACE=1 (diagnostic builds only): per ticket, lane 0 records the
-// band's start and end (s_memrealtime, 100 MHz), its wave's HW_ID and XCC_ID
-// and the wave's first ticket, read back with zpx_debug_png_trace.  No output
-// value depends on it.
-#ifndef ZPX_PNG_TRACE
-#define ZPX_PNG_TRACE 0
-#endif
-#if ZPX_PNG_TRACE
-constexpr int kTraceMax = 1 << 14;
-__device__ uint64_t g_png_trace[kTraceMax * 4];
-#endif
 
 // Cache policy of the boundary hand-off (agent scope, the data is the flag):
 // sc1 on the loads and stores (MI355X_MICROARCH.md, inter-workgroup visibility)
@@ -367,9 +354,6 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         t = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
         if (t >= nsched) break;
         const DevPngBand bd = sched[t];
-#if ZPX_PNG_TRACE
-        const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
         const DevPngPass ps = passes[bd.pass];
         const uint32_t rb = ps.row_bytes;
         // Adam7 pass 6 (the only strided pass this kernel takes), in the
@@ -724,15 +708,6 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             }
         }
         wave_lds_sync();
-#if ZPX_PNG_TRACE
-        if (lane == 0 && t < static_cast<uint32_t>(kTraceMax)) {
-            g_png_trace[4 * t] = trace_t0;
-            g_png_trace[4 * t + 1] = __builtin_amdgcn_s_memrealtime();
-            g_png_trace[4 * t + 2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32 |
-                                     static_cast<uint32_t>(__builtin_amdgcn_s_getreg(0xF804));
-            g_png_trace[4 * t + 3] = static_cast<uint64_t>(nsteps) << 32 | static_cast<uint32_t>(max_skew);
-        }
-#endif
     }
 }
 
@@ -768,13 +743,6 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
 
 } // namespace
 
-#if ZPX_PNG_TRACE
-extern "C" int zpx_debug_png_trace(uint64_t *out, size_t n)
-{
-    if (n > size_t(kTraceMax) * 4) n = size_t(kTraceMax) * 4;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_png_trace), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride)
 {
