@@ -26,15 +26,22 @@
 // so up = alignbit(out, dpp_shr1(out), 16) = [lane j-1 hi, own lo].
 //
 // Per byte pair the whole filter set is one path: the Paeth keys
-// dist * 128 + code (code = the byte position of a / b / c in a v_perm
+// dist * 8 + code (code = the byte position of a / b / c in a v_perm
 // source pair; a and b tie harmlessly, c loses every tie -- the reference's
 // a < b < c rule), the smallest key's code picks the predictor byte, and a
 // per-half (KEEP, FORCE) pair overrides the code for None / Sub / Up / Avg
-// (Avg's (a + b) >> 1 is a fourth byte of the same v_perm source):
-//   pa = |b-c|, pb = |a-c|, pc = |a+b-2c|  (packed max - min)
-//   sel = (min(ka, kb, kc) & KEEP) | FORCE;  t = perm(c | avg << 8, a | b << 8, sel)
-//   out = (f + t) & 0x00ff00ff
-// about 23 instructions per byte PAIR, against ~21 per byte one row per lane.
+// (Avg's (a + b) >> 1 is a fourth byte of the same v_perm source).  The
+// distances come from packed fp16 arithmetic on the bytes read as fp16
+// denormals (the u16 value n is n * 2^-24; the kernel runs with f16
+// denormals preserved, .amdhsa_float_denorm_mode_16_64 3): every
+// difference and sum of them is exact, and the result's bits are sign |
+// magnitude with the magnitude the integer distance, so one v_pk_mad_u16
+// (x * 8 + code, mod 2^16: the sign bit shifts out) makes each key:
+//   va = b - c, vb = a - c, vc = va + vb        (v_pk_add_f16, neg modifiers)
+//   k* = v* * 8 + code*;  sel = (min3(ka, kb, kc) & KEEP) | FORCE
+//   t = perm(c | lerp_u8(a, b) << 8, a | b << 8, sel);  out = (f + t) & 0x00ff00ff
+// 14 instructions per byte PAIR (23 with packed-integer max - min distances
+// and a separate add and shift for Avg), against ~21 per byte one row per lane.
 //
 // Memory: every lane burst-loads its two rows' next group of kG = 8 chunks one
 // group ahead through buffer descriptors (every load and store of the group
@@ -64,7 +71,6 @@ namespace {
 typedef ZPX_GLOBAL uint8_t gu8;
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gptr(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
 constexpr int kG = 8; // steps per group (input burst)
@@ -105,20 +111,18 @@ struct PairShape {
     static constexpr int W = FL == 4 ? 2 : 1;
 };
 
-// ---- packed 16-bit helpers (v_pk_*_u16)
-__device__ __forceinline__ u16x2 as16(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ uint32_t as32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ uint32_t pk_absdiff(uint32_t x, uint32_t y)
+// ---- packed 16-bit helpers (v_pk_*_u16, v_pk_add_f16)
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 ash(uint32_t x) { return __builtin_bit_cast(h16x2, x); }
+__device__ __forceinline__ uint32_t hbits(h16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+// key of a packed fp16 distance: |d| * 8 + code per half, one v_pk_mad_u16
+// (hipcc splits the C form into a shift and an or)
+__device__ __forceinline__ uint32_t pk_key(h16x2 d, uint32_t code)
 {
-    const u16x2 a = as16(x), b = as16(y);
-    return as32(__builtin_elementwise_max(a, b) - __builtin_elementwise_min(a, b));
+    uint32_t k;
+    asm("v_pk_mad_u16 %0, %1, 8, %2 op_sel_hi:[1,0,1]" : "=v"(k) : "v"(hbits(d)), "s"(code));
+    return k;
 }
-__device__ __forceinline__ uint32_t pk_min(uint32_t x, uint32_t y)
-{
-    return as32(__builtin_elementwise_min(as16(x), as16(y)));
-}
-__device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) { return as32(as16(x) + as16(y)); }
-__device__ __forceinline__ uint32_t pk_shr1(uint32_t x) { return as32(as16(x) >> (unsigned short)1); }
 
 // Paeth key codes: the byte position of each candidate in perm(cav, ab):
 // ab = [a.lo, b.lo, a.hi, b.hi] (bytes 0-3), cav = [c.lo, avg.lo, c.hi, avg.hi]
@@ -144,18 +148,19 @@ __device__ __forceinline__ PairFilter half_filter(int ft, int h)
 }
 
 // One byte pair: out = (f + predictor) mod 256 per half (zero where vmask says so).
-__device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, uint32_t ka,
-                                               uint32_t c2, PairFilter pf, uint32_t vmask)
+__device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, PairFilter pf,
+                                               uint32_t vmask)
 {
-    const uint32_t pb = pk_absdiff(a, c);
-    const uint32_t s = pk_add(a, b);
-    const uint32_t pc = pk_absdiff(s, c2);
-    const uint32_t kb = (pb << 7) | kKB;
-    const uint32_t kc = (pc << 7) | kKC;
-    const uint32_t m = pk_min(pk_min(ka, kb), kc);
+    const h16x2 va = ash(b) - ash(c); // b - c: pa = |va|
+    const h16x2 vb = ash(a) - ash(c); // a - c: pb = |vb|
+    const h16x2 vc = va + vb;         // a + b - 2c: pc = |vc|
+    // the keys (<= 510 * 8 + 7) are positive fp16 bit patterns, ordered as
+    // the integers: one v_pk_minimum3_f16 takes the smallest
+    const uint32_t m = hbits(__builtin_elementwise_minimum(
+        __builtin_elementwise_minimum(ash(pk_key(va, kKA)), ash(pk_key(vb, kKB))), ash(pk_key(vc, kKC))));
     const uint32_t sel = (m & pf.keep) | pf.force;
     const uint32_t ab = a | (b << 8);
-    const uint32_t cav = c | (pk_shr1(s) << 8);
+    const uint32_t cav = c | (__builtin_amdgcn_lerp(a, b, 0u) << 8); // avg = (a + b) >> 1 per byte (v_lerp_u8)
     const uint32_t t = __builtin_amdgcn_perm(cav, ab, sel);
     return (f + t) & vmask; // vmask: 0x00ff per half, 0 while a row is before its first chunk
 }
@@ -612,9 +617,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 for (int i = 0; i < CB; i++) {
                     const uint32_t a = i < BPP ? left[i] : o[i < BPP ? 0 : i - BPP];
                     const uint32_t c = i < BPP ? ul[i] : up[i < BPP ? 0 : i - BPP];
-                    const uint32_t b = up[i];
-                    const uint32_t ka = (pk_absdiff(b, c) << 7) | kKA;
-                    o[i] = recon_pair(f[i], a, b, c, ka, pk_add(c, c), pf, vmask);
+                    o[i] = recon_pair(f[i], a, up[i], c, pf, vmask);
                 }
 #pragma unroll
                 for (int i = 0; i < BPP; i++) {
