@@ -1,6 +1,6 @@
 """PNG kernel probe (diagnostic): ms per launch of 64 x WxH images for several
 depth / interlace shapes, to split the Adam7 cost from the per-byte cost.
-Usage: python tools/png_probe.py [size]"""
+Usage: python tools/png_probe.py [size] [shape ...]   (ZPX_LIB_PATH selects a library build)"""
 import os
 import sys
 import time
@@ -32,7 +32,10 @@ def main():
     size = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     shapes = [("rgba16_adam7", 16, 6, 1), ("rgba16_flat", 16, 6, 0), ("rgba8_adam7", 8, 6, 1),
               ("rgba8_flat", 8, 6, 0), ("rgb8_flat", 8, 2, 0)]
+    pick = sys.argv[2:]
     for name, depth, ct, il in shapes:
+        if pick and name not in pick:
+            continue
         t0 = time.perf_counter()
         d = S.png_generic(7, size, size, depth, ct, interlace=il, filters=(1, 2, 3, 4))
         st = png.Stream(d)

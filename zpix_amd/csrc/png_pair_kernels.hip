@@ -105,10 +105,16 @@ ZPX_PAIR_TRAITS(ZPX_PNG_TCA16, 8, 8)
 // loads, 64 rows per instruction, are the limit rather than issue
 // (tools/ubench/png_load_pattern: this load shape alone reads the stream at
 // 2.2 TB/s).  So FL stays 8.
+#ifndef ZPX_AB_PAIR_FL
+#define ZPX_AB_PAIR_FL 8
+#endif
+#ifndef ZPX_AB_PAIR_W
+#define ZPX_AB_PAIR_W 1
+#endif
 template <int DEPTH, bool MERGE>
 struct PairShape {
-    static constexpr int FL = 8;
-    static constexpr int W = FL == 4 ? 2 : 1;
+    static constexpr int FL = ZPX_AB_PAIR_FL;
+    static constexpr int W = ZPX_AB_PAIR_W;
 };
 
 // ---- packed 16-bit helpers (v_pk_*_u16, v_pk_add_f16)
@@ -345,7 +351,12 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
     constexpr int WG = kG * CW;             // boundary granules of one window (kG chunks)
     static_assert(WG % 2 == 0 && WG / 2 <= 64, "window loads are granule pairs, one per lane");
     __shared__ __attribute__((aligned(16))) uint32_t ring[128 * RS + 4]; // + a trash slot
-    __shared__ __attribute__((aligned(16))) uint32_t fst[128];           // flush state, [row % RPR][row / RPR]
+    // flush state, [row % RPR][row / RPR]: the posted block (fst), and for
+    // contiguous rows its chunks' output byte offset (fso, kOOR when none)
+    // and ring byte offset (fsr), so that a flush round is two adds
+    __shared__ __attribute__((aligned(16))) uint32_t fst[128];
+    __shared__ __attribute__((aligned(16))) uint32_t fso[128];
+    __shared__ __attribute__((aligned(16))) uint32_t fsr[128];
     constexpr int kTrash = 128 * RS;
 
     const int lane = threadIdx.x;
@@ -451,10 +462,28 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // instructions per group is fixed and s_waitcnt counts stay exact:
         // a group waits only for the loads issued one group earlier
         uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
+#ifdef ZPX_AB_COAL
+        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
+            constexpr int NQ = (GD + 3) / 4;
+            const int gb = ((g0 / kG) % 96) * 2 * NQ * 1024 + lane * 16;
+#pragma unroll
+            for (int q = 0; q < NQ; q++) {
+                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
+                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if (4 * q + e < GD) {
+                        d0[4 * q + e] = a[e];
+                        d1[4 * q + e] = b[e];
+                    }
+            }
+        };
+#else
         auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
             load_dwords<GD>(d0, in_rsrc, doff0 + g0 * CB);
             load_dwords<GD>(d1, in_rsrc, doff1 + g0 * CB);
         };
+#endif
         // window of kG chunks of the previous band's last row: WG granules
         // {data, epoch}; lane l < WG/2 holds granules 2l, 2l+1 (one 16-byte
         // load), and each step hands its chunk's data dwords to lane 0's DPP
@@ -474,11 +503,41 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             const int d1 = ok1 ? min(max(t_end - skew1, 0), nchunks) : 0;
             const bool p0 = min(d0, nfull) / FL > fl0, p1 = min(d1, nfull) / FL > fl1;
             const int r0 = 2 * lane, r1 = r0 + 1; // row r's state at fst[(r % RPR) * NR + r / RPR]
-            fst[(r0 % RPR) * NR + r0 / RPR] = p0 ? static_cast<uint32_t>(fl0) : 0xffffu;
-            fst[(r1 % RPR) * NR + r1 / RPR] = p1 ? static_cast<uint32_t>(fl1) : 0xffffu;
+            const int x0 = (r0 % RPR) * NR + r0 / RPR, x1 = (r1 % RPR) * NR + r1 / RPR;
+            if (ps.xf == 1) {
+                fso[x0] = p0 ? static_cast<uint32_t>(r0) * static_cast<uint32_t>(orow_bytes) + fl0 * (FL * 16) : kOOR;
+                fso[x1] = p1 ? static_cast<uint32_t>(r1) * static_cast<uint32_t>(orow_bytes) + fl1 * (FL * 16) : kOOR;
+                fsr[x0] = 4 * ring0 + ((fl0 * FL) & (kSlots - 1)) * 16;
+                fsr[x1] = 4 * ring1 + ((fl1 * FL) & (kSlots - 1)) * 16;
+            } else {
+                fst[x0] = p0 ? static_cast<uint32_t>(fl0) : 0xffffu;
+                fst[x1] = p1 ? static_cast<uint32_t>(fl1) : 0xffffu;
+            }
             fl0 += p0 ? 1 : 0;
             fl1 += p1 ? 1 : 0;
             wave_lds_sync();
+            if (ps.xf == 1) { // contiguous rows: every round's ring read first, then the 16-byte stores
+                uint32_t so[NR], sr[NR];
+#pragma unroll
+                for (int q = 0; q < NR / 4; q++) {
+                    const v4u a = *reinterpret_cast<const v4u *>(&fso[(lane / FL) * NR + 4 * q]);
+                    const v4u b = *reinterpret_cast<const v4u *>(&fsr[(lane / FL) * NR + 4 * q]);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        so[4 * q + e] = a[e];
+                        sr[4 * q + e] = b[e];
+                    }
+                }
+                const uint32_t lo = (lane % FL) * 16u;
+                v4u e[NR];
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                    e[i] = *reinterpret_cast<const v4u *>(reinterpret_cast<const uint8_t *>(ring) + sr[i] + lo);
+#pragma unroll
+                for (int i = 0; i < NR; i++)
+                    __builtin_amdgcn_raw_buffer_store_b128(e[i], out_rsrc, so[i] + lo, 0, 0);
+                return;
+            }
             uint32_t blk[NR]; // this lane group's rows RPR i + g, i = 0..NR-1
 #pragma unroll
             for (int q = 0; q < NR / 4; q++) {
@@ -495,13 +554,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + (k & (kSlots - 1)) * 4]);
                 store(post, r * static_cast<int>(orow_bytes), k, v);
             };
-            if (ps.xf == 1) { // contiguous rows: one 16-byte store per chunk
-#pragma unroll
-                for (int i = 0; i < NR; i++)
-                    round(i, [&](bool post, int ro, int k, v4u v) {
-                        __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc, post ? ro + k * 16 : kOOR, 0, 0);
-                    });
-            } else if (!merge) { // Adam7 passes 1-4 into Q: pixels xf (2 or 4) apart
+            if (!merge) { // Adam7 passes 1-4 into Q: pixels xf (2 or 4) apart
 #pragma unroll
                 for (int i = 0; i < NR; i++)
                     round(i, [&](bool post, int ro, int k, v4u v) {
