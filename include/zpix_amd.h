@@ -363,6 +363,11 @@ enum zpx_png_depth {
 };
 /* Readable bytes the device input must have past its last filtered row. */
 #define ZPX_PNG_INPUT_PAD 256
+/* Layout of zpx_png_frame.filtered.  STREAM: the inflated stream as is.
+ * SLAB: the same bytes rearranged per 128-row band in the order the
+ * paired-row kernel reads them (zpx_png_stream_slab builds it on the host;
+ * only for frames that kernel takes, i.e. zpx_png_stream_slab succeeds). */
+enum zpx_png_layout { ZPX_PNG_LAYOUT_STREAM = 0, ZPX_PNG_LAYOUT_SLAB = 1 };
 
 /* One PNG image after host inflate (parseIdat, png/decoder.zig:404-545). */
 typedef struct zpx_png_frame {
@@ -371,8 +376,10 @@ typedef struct zpx_png_frame {
     int32_t interlace;       /* 0 none, 1 Adam7 */
     int32_t use_transparent; /* tRNS colour key (png/decoder.zig:547-602) */
     uint8_t transparent[6];
-    uint8_t pad[2];
-    const uint8_t *filtered; /* DEVICE: inflated stream, filter byte per row, all passes */
+    uint8_t layout;          /* zpx_png_layout of `filtered` */
+    uint8_t pad;
+    const uint8_t *filtered; /* DEVICE: inflated stream, filter byte per row, all passes
+                                (ZPX_PNG_LAYOUT_STREAM), or its band slab (ZPX_PNG_LAYOUT_SLAB) */
     uint8_t *out;            /* DEVICE: pixels of the image type readImagePass allocates */
     size_t out_stride;
     int32_t *max_index;      /* DEVICE, paletted only: receives max palette index (or NULL) */
@@ -426,6 +433,11 @@ typedef struct zpx_png_stream zpx_png_stream;
 int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **out);
 int zpx_png_stream_frame(const zpx_png_stream *s, zpx_png_frame *frame, size_t *filtered_len);
 const uint8_t *zpx_png_stream_data(const zpx_png_stream *s);
+/* The stream's band slab (ZPX_PNG_LAYOUT_SLAB; built on first use, pinned
+ * host memory owned by the stream): upload *len bytes of *data and set the
+ * frame's layout to ZPX_PNG_LAYOUT_SLAB.  ZPX_E_UNSUPPORTED when the
+ * paired-row kernel does not take the image (the stream layout still works). */
+int zpx_png_stream_slab(zpx_png_stream *s, const uint8_t **data, size_t *len);
 void zpx_png_stream_free(zpx_png_stream *s);
 
 /* ---------------------------------------------------------------------- */

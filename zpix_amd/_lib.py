@@ -87,7 +87,8 @@ class zpx_png_frame(C.Structure):
         ("interlace", C.c_int32),
         ("use_transparent", C.c_int32),
         ("transparent", C.c_uint8 * 6),
-        ("pad", C.c_uint8 * 2),
+        ("layout", C.c_uint8),  # zpx_png_layout: 0 stream, 1 band slab
+        ("pad", C.c_uint8),
         ("filtered", C.c_void_p),
         ("out", C.c_void_p),
         ("out_stride", C.c_size_t),
@@ -151,7 +152,7 @@ EXPORTS = [
     "zpx_jpeg_plan_create", "zpx_png_plan_create", "zpx_plan_launch", "zpx_plan_bytes",
     "zpx_plan_kernel_count", "zpx_plan_destroy", "zpx_dev_rgba_pixels", "zpx_jpeg_entropy_decode",
     "zpx_jpeg_coeffs_frame", "zpx_jpeg_coeffs_free", "zpx_jpeg_coeffs_widen", "zpx_png_inflate", "zpx_png_stream_frame",
-    "zpx_png_stream_data", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
+    "zpx_png_stream_data", "zpx_png_stream_slab", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
     "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config", "zpx_plan_status",
     "zpx_batch_decode_sharded", "zpx_debug_png_stall", "zpx_debug_jpeg_parallel_scans",
     "zpx_bmp_decode", "zpx_bmp_load", "zpx_bmp_probe_buffer", "zpx_qoi_decode", "zpx_qoi_load",
@@ -206,6 +207,7 @@ def lib():
         "zpx_png_inflate": (i32, [C.c_char_p, sz, C.POINTER(vp)]),
         "zpx_png_stream_frame": (i32, [vp, C.POINTER(zpx_png_frame), C.POINTER(sz)]),
         "zpx_png_stream_data": (vp, [vp]),
+        "zpx_png_stream_slab": (i32, [vp, C.POINTER(vp), C.POINTER(sz)]),
         "zpx_png_stream_free": (None, [vp]),
         "zpx_batch_decode_rgba": (i32, [vp, C.POINTER(zpx_batch_item), i32, C.POINTER(zpx_batch_opts),
                                         C.POINTER(zpx_batch_stats)]),

@@ -192,6 +192,11 @@ void Pipeline::worker()
         if (zpx_png_probe_buffer(it.buf, it.len)) {
             d->fmt = 2;
             d->status = png_parse(it.buf, it.len, d->ps, sub);
+            // the paired-row kernel's input layout, on this worker thread
+            // (the kernel reads the stream layout when this is refused)
+            if (d->status == ZPX_OK && png_use_pair(d->ps.depth, d->ps.interlace, d->ps.use_transparent,
+                                                    d->ps.width, size_t(d->ps.width) * d->ps.out_bpp))
+                (void)png_stream_build_slab(d->ps);
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
             d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, sub, jpeg_sparse_upload());
@@ -417,9 +422,13 @@ int Pipeline::issue_png(Slot &s)
     PngStream &ps = d.ps;
     const uint32_t W = ps.width, H = ps.height;
     const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
-    HIPCHK(ctx_, s.din.reserve(ps.data_len + ZPX_PNG_INPUT_PAD));
-    HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, ps.data.ptr, ps.data_len + ZPX_PNG_INPUT_PAD, hipMemcpyHostToDevice, h2d_));
-    h2d_bytes_ += double(ps.data_len);
+    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
+                                   ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
+    const bool slab = pair && ps.slab_len != 0;
+    const size_t in_len = slab ? ps.slab_len : ps.data_len + ZPX_PNG_INPUT_PAD;
+    HIPCHK(ctx_, s.din.reserve(in_len));
+    HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, slab ? ps.slab.ptr : ps.data.ptr, in_len, hipMemcpyHostToDevice, h2d_));
+    h2d_bytes_ += double(slab ? ps.slab_len : ps.data_len);
     HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
     HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
 
@@ -451,6 +460,7 @@ int Pipeline::issue_png(Slot &s)
     f.use_transparent = ps.use_transparent;
     memcpy(f.transparent, ps.transparent, 6);
     f.filtered = s.din.as<uint8_t>();
+    f.layout = slab ? ZPX_PNG_LAYOUT_SLAB : ZPX_PNG_LAYOUT_STREAM;
     f.out = img_out;
     f.out_stride = img_stride;
     f.max_index = nullptr; // palette handled below with all 256 entries
@@ -458,7 +468,6 @@ int Pipeline::issue_png(Slot &s)
     std::vector<uint32_t> rowbytes;
     uint64_t bytes = 0;
     png_frame_passes(f, passes, rowbytes, bytes);
-    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W, img_stride);
     Adam7Stage a7;
     if (pair && ps.interlace) {
         png_adam7_stage(f, static_cast<int>(ps.out_bpp), passes, 0, a7);

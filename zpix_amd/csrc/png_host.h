@@ -33,7 +33,14 @@ struct PngStream {
     PngPassInfo pass[7];
     HostBuf data;                   // inflated stream (+ZPX_PNG_INPUT_PAD)
     size_t data_len = 0;            // bytes the passes consume
+    HostBuf slab;                   // band slab of `data` (png_slab.cpp), when built
+    size_t slab_len = 0;
 };
+
+// The band slab of ps.data for the paired-row kernel (png_slab.cpp), into
+// ps.slab: ZPX_OK, ZPX_E_UNSUPPORTED when that kernel does not take the
+// image, ZPX_E_OUT_OF_MEMORY.
+int png_stream_build_slab(PngStream &ps);
 
 // Parse + inflate.  On success every row's data is present and every filter
 // byte is valid; otherwise returns the reference's error for the first row

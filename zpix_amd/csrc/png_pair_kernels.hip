@@ -389,8 +389,18 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const uint32_t band_rows = min(128u, ps.rows - base);
         const uint32_t y0 = base + 2 * lane, y1 = y0 + 1;
         const bool ok0 = 2u * lane < band_rows, ok1 = 2u * lane + 1 < band_rows;
-        const int ft0 = ok0 ? ps.filtered[static_cast<size_t>(y0) * (rb + 1)] : 0;
-        const int ft1 = ok1 ? ps.filtered[static_cast<size_t>(y1) * (rb + 1)] : 0;
+        // slab layout (png_slab.cpp): the band's region -- its 128 filter
+        // bytes, then its groups -- from the frame's band offset table
+        const bool slab = ps.slab != 0;
+        const uint8_t *region = nullptr;
+        if (slab) {
+            typedef const __attribute__((address_space(4))) uint64_t *CU64;
+            const uint64_t ro = *(reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(ps.filtered)) + ps.slab_band0 +
+                                  bd.band);
+            region = ps.filtered + ro;
+        }
+        const int ft0 = slab ? region[2 * lane] : ok0 ? ps.filtered[static_cast<size_t>(y0) * (rb + 1)] : 0;
+        const int ft1 = slab ? region[2 * lane + 1] : ok1 ? ps.filtered[static_cast<size_t>(y1) * (rb + 1)] : 0;
 
         // skew over the band's 128 rows (row 2j = low half of lane j, 2j+1 high)
         const uint64_t R0 = __ballot(!(ft0 >= 2) || lane == 0 || !ok0);
@@ -416,14 +426,21 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // byte over its rows + ZPX_PNG_INPUT_PAD.  The host routes passes with
         // rows shorter than a chunk to the one-row kernel, so no lane's group
         // ever starts before the descriptor (skew <= row index).
-        const uint8_t *band0 = ps.filtered + static_cast<size_t>(base) * (rb + 1);
+        // A slab band is its region: the 128 filter bytes, then group g's
+        // 16-byte pieces at 128 + ((2 g + h) NQ + q) KiB + 16 lane (piece q
+        // of row 2 lane + h's bytes from chunk 8 g - skew, dword aligned,
+        // zeros outside the row), so each load instruction reads 1 KiB
+        // contiguous (png_slab.cpp).
+        constexpr int NQ = 8 * CB / 16;
+        const uint8_t *band0 = slab ? region : ps.filtered + static_cast<size_t>(base) * (rb + 1);
         const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
         const uint32_t delta = static_cast<uint32_t>(band0 - base4);
-        const uint64_t extent = delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
+        const uint64_t extent = slab ? 128ull + static_cast<uint64_t>((nsteps + kG - 1) / kG) * 2 * NQ * 1024
+                                     : delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
         const Rsrc in_rsrc = make_rsrc(base4, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
         const uint32_t roff0 = delta + static_cast<uint32_t>(2 * lane) * (rb + 1); // filter byte of row 2j
         const uint32_t roff1 = roff0 + rb + 1;
-        const uint32_t mis0 = (roff0 + 1) & 3, mis1 = (roff1 + 1) & 3;
+        const uint32_t mis0 = slab ? 0u : (roff0 + 1) & 3, mis1 = slab ? 0u : (roff1 + 1) & 3;
         const int doff0 = static_cast<int>(roff0 + 1 - mis0) - skew0 * CB; // group 0's first dword, row 2j
         const int doff1 = static_cast<int>(roff1 + 1 - mis1) - skew1 * CB;
 
@@ -462,28 +479,30 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // instructions per group is fixed and s_waitcnt counts stay exact:
         // a group waits only for the loads issued one group earlier
         uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
-#ifdef ZPX_AB_COAL
+        // (both layouts issue the same loads per group -- NQ 16-byte loads
+        // and one dword per row -- so the s_waitcnt counts hold for either;
+        // a slab's dword is the unused alignbyte carry: out of range, zero)
+        static_assert(NQ * 4 + 1 == GD, "a group is NQ 16-byte pieces and the carry dword per row");
         auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
-            constexpr int NQ = (GD + 3) / 4;
-            const int gb = ((g0 / kG) % 96) * 2 * NQ * 1024 + lane * 16;
+            if (slab) {
+                const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
 #pragma unroll
-            for (int q = 0; q < NQ; q++) {
-                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
-                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
+                for (int q = 0; q < NQ; q++) {
+                    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
+                    const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
 #pragma unroll
-                for (int e = 0; e < 4; e++)
-                    if (4 * q + e < GD) {
+                    for (int e = 0; e < 4; e++) {
                         d0[4 * q + e] = a[e];
                         d1[4 * q + e] = b[e];
                     }
+                }
+                d0[GD - 1] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, kOOR, 0, 0);
+                d1[GD - 1] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, kOOR, 0, 0);
+            } else {
+                load_dwords<GD>(d0, in_rsrc, doff0 + g0 * CB);
+                load_dwords<GD>(d1, in_rsrc, doff1 + g0 * CB);
             }
         };
-#else
-        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
-            load_dwords<GD>(d0, in_rsrc, doff0 + g0 * CB);
-            load_dwords<GD>(d1, in_rsrc, doff1 + g0 * CB);
-        };
-#endif
         // window of kG chunks of the previous band's last row: WG granules
         // {data, epoch}; lane l < WG/2 holds granules 2l, 2l+1 (one 16-byte
         // load), and each step hands its chunk's data dwords to lane 0's DPP

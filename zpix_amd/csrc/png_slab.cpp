@@ -1,0 +1,188 @@
+// Band slab: the paired-row PNG kernel's input layout (png_pair_kernels.hip).
+//
+// The kernel reconstructs a band of 128 rows of a pass with lane j holding
+// rows 2j and 2j+1; at group g (steps 8g .. 8g+7) row r reads the CB-byte
+// chunks 8g - skew(r) .. 8g - skew(r) + 7 of its filtered bytes (the
+// unfilter loop of readImagePass, src/png/decoder.zig:806-842, walks each
+// row left to right; skew(r) = r - the last row <= r that restarts the
+// dependency chain: a None / Sub row or the band's first).  Read from the
+// inflated stream, each of the kernel's 16-byte loads touches 64 different
+// rows -- 64 cache lines per instruction, which caps the read at ~2.5 TB/s
+// (tools/ubench/png_load_pattern mode 0) against ~6 TB/s for 1 KiB
+// contiguous per instruction (mode 2).  The slab stores each band's bytes in
+// the order the kernel reads them:
+//
+//   slab   = u64 region offset per band (every band of every non-empty pass,
+//            Adam7 order), then the regions, 256-byte aligned
+//   region = the band's 128 filter-type bytes (0 for rows past the pass),
+//            then per group g, row half h (row 2 lane + h), piece q < NQ:
+//            1 KiB = 64 lanes x 16 bytes, the bytes [16 q, 16 q + 16) of the
+//            row's group window (chunk 8 g - skew(r) on, zeros outside the row)
+//
+// NQ = 8 CB / 16 (6 for 3- and 6-byte pixels, else 8), and a band has
+// ceil((chunks + max skew) / 8) groups, exactly the groups the kernel walks.
+// The host builds it after inflate (one pass over the bytes); the skew rule
+// here and in the kernel must agree (tests/test_abi.py checks the layout
+// against a Python model, every -m gpu PNG test the kernel on it).
+#include <algorithm>
+#include <cstring>
+
+#include "api_internal.h"
+#include "device_types.h"
+#include "png_host.h"
+
+namespace zpx {
+
+namespace {
+
+struct SlabGeom {
+    int bpp = 0, cb = 16;
+};
+
+SlabGeom slab_geom(int depth)
+{
+    SlabGeom g;
+    switch (depth) {
+    case ZPX_PNG_G8: g.bpp = 1; break;
+    case ZPX_PNG_G16: g.bpp = 2; break;
+    case ZPX_PNG_TC8: g.bpp = 3; g.cb = 12; break;
+    case ZPX_PNG_TCA8: g.bpp = 4; break;
+    case ZPX_PNG_TC16: g.bpp = 6; g.cb = 12; break;
+    case ZPX_PNG_TCA16: g.bpp = 8; break;
+    default: break;
+    }
+    return g;
+}
+
+constexpr size_t kRegionAlign = 256;
+size_t align_up(size_t x) { return (x + kRegionAlign - 1) & ~(kRegionAlign - 1); }
+
+// skew(r) of the band's 128 rows, as the kernel computes them (ballots over
+// rows that restart: row 0, a None / Sub row, a row past the pass); returns
+// the largest skew of a row inside the pass
+int band_skews(const uint8_t *ft, uint32_t rows, int skew[128])
+{
+    int last = 0, mx = 0;
+    for (int r = 0; r < 128; r++) {
+        const bool in = static_cast<uint32_t>(r) < rows;
+        if (r == 0 || !in || ft[r] < 2) last = r;
+        skew[r] = r - last;
+        if (in) mx = std::max(mx, skew[r]);
+    }
+    return mx;
+}
+
+} // namespace
+
+size_t png_slab_layout(const zpx_png_frame &f, std::vector<uint64_t> &band_off)
+{
+    band_off.clear();
+    const SlabGeom sg = slab_geom(f.depth);
+    if (!sg.bpp) return 0;
+    std::vector<DevPngPass> passes;
+    std::vector<uint32_t> rowbytes;
+    uint64_t bytes = 0;
+    zpx_png_frame hf = f;
+    hf.layout = ZPX_PNG_LAYOUT_STREAM;
+    png_frame_passes(hf, passes, rowbytes, bytes);
+    const int c = sg.cb / sg.bpp, nq = 8 * sg.cb / 16;
+    size_t nb = 0;
+    for (const DevPngPass &p : passes) nb += (p.rows + 127) / 128;
+    size_t off = align_up(nb * sizeof(uint64_t));
+    for (const DevPngPass &p : passes) {
+        const uint32_t rb = p.row_bytes;
+        const int nchunks = static_cast<int>((p.width + c - 1) / c);
+        for (uint32_t base = 0; base < p.rows; base += 128) {
+            const uint32_t rows = std::min(128u, p.rows - base);
+            uint8_t ft[128] = {};
+            for (uint32_t r = 0; r < rows; r++) ft[r] = p.filtered[size_t(base + r) * (rb + 1)];
+            int skew[128];
+            const int ngroups = (nchunks + band_skews(ft, rows, skew) + 7) / 8;
+            band_off.push_back(off);
+            off = align_up(off + 128 + size_t(ngroups) * 2 * nq * 1024);
+        }
+    }
+    return off;
+}
+
+void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, uint8_t *out)
+{
+    const SlabGeom sg = slab_geom(f.depth);
+    std::vector<DevPngPass> passes;
+    std::vector<uint32_t> rowbytes;
+    uint64_t bytes = 0;
+    zpx_png_frame hf = f;
+    hf.layout = ZPX_PNG_LAYOUT_STREAM;
+    png_frame_passes(hf, passes, rowbytes, bytes);
+    const int c = sg.cb / sg.bpp, nq = 8 * sg.cb / 16;
+    const size_t nb = band_off.size();
+    memcpy(out, band_off.data(), nb * sizeof(uint64_t));
+    memset(out + nb * sizeof(uint64_t), 0, align_up(nb * sizeof(uint64_t)) - nb * sizeof(uint64_t));
+    size_t b = 0;
+    for (const DevPngPass &p : passes) {
+        const uint32_t rb = p.row_bytes;
+        const int nchunks = static_cast<int>((p.width + c - 1) / c);
+        for (uint32_t base = 0; base < p.rows; base += 128, b++) {
+            const uint32_t rows = std::min(128u, p.rows - base);
+            uint8_t *region = out + band_off[b];
+            uint8_t *ft = region;
+            memset(ft, 0, 128);
+            for (uint32_t r = 0; r < rows; r++) ft[r] = p.filtered[size_t(base + r) * (rb + 1)];
+            int skew[128];
+            const int ngroups = (nchunks + band_skews(ft, rows, skew) + 7) / 8;
+            const size_t gbytes = size_t(2) * nq * 1024;
+            uint8_t *groups = region + 128;
+            for (int r = 0; r < 128; r++) {
+                const int lane = r / 2, h = r % 2;
+                const uint8_t *row = static_cast<uint32_t>(r) < rows
+                                         ? p.filtered + size_t(base + r) * (rb + 1) + 1
+                                         : nullptr;
+                for (int g = 0; g < ngroups; g++) {
+                    const int64_t start = (int64_t(8) * g - skew[r]) * sg.cb; // first byte of the group window
+                    uint8_t *dst = groups + size_t(g) * gbytes + size_t(h) * nq * 1024 + size_t(lane) * 16;
+                    for (int q = 0; q < nq; q++, dst += 1024) {
+                        const int64_t s0 = start + 16 * q;
+                        if (row && s0 >= 0 && s0 + 16 <= int64_t(rb)) {
+                            memcpy(dst, row + s0, 16);
+                            continue;
+                        }
+                        for (int i = 0; i < 16; i++) {
+                            const int64_t x = s0 + i;
+                            dst[i] = (row && x >= 0 && x < int64_t(rb)) ? row[x] : 0;
+                        }
+                    }
+                }
+            }
+            // the region's alignment tail
+            const size_t end = band_off[b] + 128 + size_t(ngroups) * gbytes;
+            const size_t next = b + 1 < nb ? band_off[b + 1] : align_up(end);
+            memset(out + end, 0, next - end);
+        }
+    }
+}
+
+int png_stream_build_slab(PngStream &ps)
+{
+    if (ps.slab_len) return ZPX_OK;
+    if (!png_pair_supported(ps.depth, ps.interlace, ps.use_transparent, ps.width, size_t(ps.width) * ps.out_bpp))
+        return ZPX_E_UNSUPPORTED;
+    zpx_png_frame f;
+    memset(&f, 0, sizeof(f));
+    f.width = ps.width;
+    f.height = ps.height;
+    f.depth = ps.depth;
+    f.interlace = ps.interlace;
+    f.use_transparent = ps.use_transparent ? 1 : 0;
+    memcpy(f.transparent, ps.transparent, 6);
+    f.filtered = static_cast<const uint8_t *>(ps.data.ptr);
+    f.out_stride = size_t(ps.width) * ps.out_bpp;
+    std::vector<uint64_t> off;
+    const size_t n = png_slab_layout(f, off);
+    if (!n) return ZPX_E_UNSUPPORTED;
+    if (!ps.slab.alloc(n, false)) return ZPX_E_OUT_OF_MEMORY;
+    png_slab_fill(f, off, static_cast<uint8_t *>(ps.slab.ptr));
+    ps.slab_len = n;
+    return ZPX_OK;
+}
+
+} // namespace zpx

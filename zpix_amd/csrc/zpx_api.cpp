@@ -464,6 +464,7 @@ void zpx::png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &pass
     default: bits = 64; break;
     }
     size_t off = 0;
+    uint32_t slab_band = 0; // (slab layout: bands of 128 rows, png_slab.cpp)
     const int np = f.interlace ? 7 : 1;
     for (int p = 0; p < np; p++) {
         DevPngPass d{};
@@ -478,7 +479,10 @@ void zpx::png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &pass
             if (w == 0 || h == 0) continue;
         }
         const uint32_t rb = static_cast<uint32_t>((uint64_t(bits) * w + 7) / 8);
-        d.filtered = f.filtered + off;
+        d.filtered = f.layout == ZPX_PNG_LAYOUT_SLAB ? f.filtered : f.filtered + off;
+        d.slab = f.layout == ZPX_PNG_LAYOUT_SLAB ? 1 : 0;
+        d.slab_band0 = slab_band;
+        slab_band += (h + 127) / 128;
         d.out = f.out;
         d.max_index = f.max_index;
         d.out_stride = f.out_stride;
@@ -524,6 +528,11 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
         const bool trns = frames[i].use_transparent != 0;
         const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, trns, frames[i].width,
                                        frames[i].out_stride);
+        if (frames[i].layout > ZPX_PNG_LAYOUT_SLAB) return ZPX_E_INVALID_ARGUMENT;
+        if (frames[i].layout == ZPX_PNG_LAYOUT_SLAB && !pair) {
+            ctx->last_error = "png: a slab-layout frame needs the paired-row kernel (zpx_png_stream_slab)";
+            return ZPX_E_INVALID_ARGUMENT;
+        }
         by_depth[{frames[i].depth, pair, pair && trns}].push_back(i);
     }
     uint64_t bytes = 0;
@@ -754,6 +763,17 @@ extern "C" const uint8_t *zpx_png_stream_data(const zpx_png_stream *s)
 {
     return s ? static_cast<const uint8_t *>(s->s.data.ptr) : nullptr;
 }
+extern "C" int zpx_png_stream_slab(zpx_png_stream *s, const uint8_t **data, size_t *len)
+{
+    if (!s || !data || !len) return ZPX_E_INVALID_ARGUMENT;
+    return guarded([&] {
+        if (!s->s.slab_len)
+            if (int e = png_stream_build_slab(s->s)) return e;
+        *data = static_cast<const uint8_t *>(s->s.slab.ptr);
+        *len = s->s.slab_len;
+        return static_cast<int>(ZPX_OK);
+    });
+}
 extern "C" void zpx_png_stream_free(zpx_png_stream *s) { delete s; }
 
 // ------------------------------------------------------------------ jpeg.decode
@@ -956,8 +976,14 @@ static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint
     if (int e = png_parse(buf, len, ps, png_inflate_threads())) return e;
     const size_t out_len = size_t(ps.width) * ps.height * ps.out_bpp;
     DevBuf din, dout, dmax;
-    HIPCHK(ctx, din.alloc(ps.data_len + ZPX_PNG_INPUT_PAD));
-    HIPCHK(ctx, hipMemcpyAsync(din.ptr, ps.data.ptr, ps.data_len + ZPX_PNG_INPUT_PAD, hipMemcpyHostToDevice, ctx->stream));
+    // the paired-row kernel reads the band slab (png_slab.cpp)
+    const bool slab = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, ps.width,
+                                   size_t(ps.width) * ps.out_bpp) &&
+                      png_stream_build_slab(ps) == ZPX_OK;
+    const void *hin = slab ? ps.slab.ptr : ps.data.ptr;
+    const size_t in_len = slab ? ps.slab_len : ps.data_len + ZPX_PNG_INPUT_PAD;
+    HIPCHK(ctx, din.alloc(in_len));
+    HIPCHK(ctx, hipMemcpyAsync(din.ptr, hin, in_len, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, dout.alloc(out_len));
     HIPCHK(ctx, dmax.alloc(16));
     HIPCHK(ctx, hipMemsetAsync(dmax.ptr, 0, 16, ctx->stream));
@@ -970,6 +996,7 @@ static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint
     f.use_transparent = ps.use_transparent;
     memcpy(f.transparent, ps.transparent, 6);
     f.filtered = din.as<uint8_t>();
+    f.layout = slab ? ZPX_PNG_LAYOUT_SLAB : ZPX_PNG_LAYOUT_STREAM;
     f.out = dout.as<uint8_t>();
     f.out_stride = size_t(ps.width) * ps.out_bpp;
     f.max_index = ps.kind == ZPX_PALETTED ? dmax.as<int32_t>() : nullptr;

@@ -175,14 +175,21 @@ class PngBatch:
     """A batch of PNG images resident in HBM, unfiltered + stored by one plan."""
 
     def __init__(self, items: list[Stream], slots: list[int] | None = None, device: int = 0,
-                 ctx: context.Context | None = None):
+                 ctx: context.Context | None = None, layout: str = "auto"):
+        """layout: "auto" uploads each image's band slab where the
+        paired-row kernel takes it (Stream.slab, what the decode and batch
+        paths do), else the inflated stream; "stream" always the stream."""
         torch = _torch()
         self.ctx = ctx or context.default(device)
         self.device = torch.device("cuda", self.ctx.device)
         self.items = items
         self.slots = list(range(len(items))) if slots is None else list(slots)
         frames = (_lib.zpx_png_frame * len(self.slots))()
-        in_sizes = [_align(items[i].filtered_len + INPUT_PAD) for i in self.slots]
+        inputs = {}
+        for i in set(self.slots):
+            sl = items[i].slab() if layout == "auto" else None
+            inputs[i] = (sl, 1) if sl is not None else (items[i].filtered(), 0)
+        in_sizes = [_align(len(inputs[i][0])) for i in self.slots]
         out_sizes = [_align(items[i].frame.out_stride * items[i].frame.height) for i in self.slots]
         self.in_arena = torch.empty(max(sum(in_sizes), 1), dtype=torch.uint8, device=self.device)
         self.out_arena = torch.zeros(max(sum(out_sizes), 1), dtype=torch.uint8, device=self.device)
@@ -193,8 +200,10 @@ class PngBatch:
             st = items[i]
             f = frames[s]
             C.pointer(f)[0] = st.frame
-            self.in_arena[oi:oi + st.filtered_len + INPUT_PAD].copy_(torch.from_numpy(st.filtered()))
+            data, lay = inputs[i]
+            self.in_arena[oi:oi + len(data)].copy_(torch.from_numpy(data))
             f.filtered = self.in_arena.data_ptr() + oi
+            f.layout = lay
             f.out = self.out_arena.data_ptr() + oo
             f.max_index = self.max_index.data_ptr() + 16 * s
             self.out_offsets.append(oo)

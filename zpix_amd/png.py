@@ -73,6 +73,17 @@ class Stream:
         ptr = _lib.lib().zpx_png_stream_data(self.handle)
         return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(self.filtered_len + INPUT_PAD,))
 
+    def slab(self):
+        """The band slab (ZPX_PNG_LAYOUT_SLAB: the paired-row kernel's input
+        layout, png_slab.cpp) as a host numpy view, or None when that kernel
+        does not take the image."""
+        p, n = C.c_void_p(), C.c_size_t(0)
+        rc = _lib.lib().zpx_png_stream_slab(self.handle, C.byref(p), C.byref(n))
+        if rc and _lib.error_name(rc) == "Unsupported":
+            return None
+        _lib.check(rc)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n.value,))
+
     def close(self):
         if self.handle:
             _lib.lib().zpx_png_stream_free(self.handle)
