@@ -422,9 +422,11 @@ int Pipeline::issue_png(Slot &s)
     PngStream &ps = d.ps;
     const uint32_t W = ps.width, H = ps.height;
     const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
-    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
-                                   ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
-    const bool slab = pair && ps.slab_len != 0;
+    // the paired-row kernel reads the band slab the worker built; without
+    // one the one-row-per-lane kernel reads the stream
+    const bool slab = ps.slab_len != 0 && png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
+                                                        ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
+    const bool pair = slab;
     const size_t in_len = slab ? ps.slab_len : ps.data_len + ZPX_PNG_INPUT_PAD;
     HIPCHK(ctx_, s.din.reserve(in_len));
     HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, slab ? ps.slab.ptr : ps.data.ptr, in_len, hipMemcpyHostToDevice, h2d_));

@@ -153,9 +153,8 @@ __device__ __forceinline__ PairFilter half_filter(int ft, int h)
     return PairFilter{keep << sh, force << sh};
 }
 
-// One byte pair: out = (f + predictor) mod 256 per half (zero where vmask says so).
-__device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, PairFilter pf,
-                                               uint32_t vmask)
+// One byte pair: out = (f + predictor) mod 256 per half.
+__device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, PairFilter pf)
 {
     const h16x2 va = ash(b) - ash(c); // b - c: pa = |va|
     const h16x2 vb = ash(a) - ash(c); // a - c: pb = |vb|
@@ -168,7 +167,7 @@ __device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t 
     const uint32_t ab = a | (b << 8);
     const uint32_t cav = c | (__builtin_amdgcn_lerp(a, b, 0u) << 8); // avg = (a + b) >> 1 per byte (v_lerp_u8)
     const uint32_t t = __builtin_amdgcn_perm(cav, ab, sel);
-    return (f + t) & vmask; // vmask: 0x00ff per half, 0 while a row is before its first chunk
+    return (f + t) & 0x00ff00ffu;
 }
 
 // ---- output of one chunk: the 16 bytes store_chunk writes (readImagePass
@@ -267,32 +266,6 @@ __device__ __forceinline__ Rsrc make_rsrc(const void *base, uint32_t bytes)
     return __builtin_amdgcn_make_buffer_rsrc(ua, 0, static_cast<int>(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
 }
 
-// N dwords from byte offset `off` (dword aligned, >= 0) into d[]
-template <int N>
-__device__ __forceinline__ void load_dwords(uint32_t (&d)[N], Rsrc rsrc, int off)
-{
-#pragma unroll
-    for (int i = 0; i + 4 <= N; i += 4) {
-        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 4 * i, 0, 0);
-        d[i] = v[0];
-        d[i + 1] = v[1];
-        d[i + 2] = v[2];
-        d[i + 3] = v[3];
-    }
-    constexpr int T = N & ~3;
-    if constexpr (N - T == 1) {
-        d[T] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4 * T, 0, 0);
-    } else if constexpr (N - T == 2) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, off + 4 * T, 0, 0);
-        d[T] = v[0];
-        d[T + 1] = v[1];
-    } else if constexpr (N - T == 3) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rsrc, off + 4 * T, 0, 0);
-        d[T] = v[0];
-        d[T + 1] = v[1];
-        d[T + 2] = v[2];
-    }
-}
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -342,7 +315,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
 {
     using T = PairTraits<DEPTH>;
     constexpr int BPP = T::BPP, CB = T::CB, CW = T::CW, C = T::C;
-    constexpr int GD = kG * CW + 1;         // input dwords per row per group (+1: alignbyte carry)
+    constexpr int GD = kG * CW;             // input dwords per row per group
     constexpr int FL = PairShape<DEPTH, MERGE>::FL; // chunks per flushed block, steps between flushes
     constexpr int kSlots = 2 * FL;          // ring slots per row
     constexpr int RPR = 64 / FL;            // rows per flush round (FL lanes each)
@@ -387,20 +360,13 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const int nfull = static_cast<int>(ps.width / C); // chunks whose pixels are all inside the row
         const uint32_t base = bd.band * 128;
         const uint32_t band_rows = min(128u, ps.rows - base);
-        const uint32_t y0 = base + 2 * lane, y1 = y0 + 1;
         const bool ok0 = 2u * lane < band_rows, ok1 = 2u * lane + 1 < band_rows;
-        // slab layout (png_slab.cpp): the band's region -- its 128 filter
-        // bytes, then its groups -- from the frame's band offset table
-        const bool slab = ps.slab != 0;
-        const uint8_t *region = nullptr;
-        if (slab) {
-            typedef const __attribute__((address_space(4))) uint64_t *CU64;
-            const uint64_t ro = *(reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(ps.filtered)) + ps.slab_band0 +
-                                  bd.band);
-            region = ps.filtered + ro;
-        }
-        const int ft0 = slab ? region[2 * lane] : ok0 ? ps.filtered[static_cast<size_t>(y0) * (rb + 1)] : 0;
-        const int ft1 = slab ? region[2 * lane + 1] : ok1 ? ps.filtered[static_cast<size_t>(y1) * (rb + 1)] : 0;
+        // the band's slab region (png_slab.cpp): its 128 filter bytes, then
+        // its groups, from the frame's band offset table (scalar loads)
+        typedef const __attribute__((address_space(4))) uint64_t *CU64;
+        const uint8_t *region =
+            ps.filtered + *(reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(ps.filtered)) + ps.slab_band0 + bd.band);
+        const int ft0 = region[2 * lane], ft1 = region[2 * lane + 1]; // (0 past the pass)
 
         // skew over the band's 128 rows (row 2j = low half of lane j, 2j+1 high)
         const uint64_t R0 = __ballot(!(ft0 >= 2) || lane == 0 || !ok0);
@@ -426,23 +392,17 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // byte over its rows + ZPX_PNG_INPUT_PAD.  The host routes passes with
         // rows shorter than a chunk to the one-row kernel, so no lane's group
         // ever starts before the descriptor (skew <= row index).
-        // A slab band is its region: the 128 filter bytes, then group g's
-        // 16-byte pieces at 128 + ((2 g + h) NQ + q) KiB + 16 lane (piece q
-        // of row 2 lane + h's bytes from chunk 8 g - skew, dword aligned,
-        // zeros outside the row), so each load instruction reads 1 KiB
-        // contiguous (png_slab.cpp).
+        // band input: the region's groups -- group g's 16-byte pieces at
+        // 128 + ((2 g + h) NQ + q) KiB + 16 lane (piece q of row 2 lane + h's
+        // bytes from chunk 8 g - skew on, zeros outside the row), so each
+        // load instruction reads 1 KiB contiguous, and a row's chunks before
+        // its first (k < 0) are zeros: it outputs zeros there, the zero
+        // left / up / up-left its first chunk starts from.  The prefetch past
+        // the last group reads out of range (zeros).
         constexpr int NQ = 8 * CB / 16;
-        const uint8_t *band0 = slab ? region : ps.filtered + static_cast<size_t>(base) * (rb + 1);
-        const uint8_t *base4 = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(band0) & ~uintptr_t(3));
-        const uint32_t delta = static_cast<uint32_t>(band0 - base4);
-        const uint64_t extent = slab ? 128ull + static_cast<uint64_t>((nsteps + kG - 1) / kG) * 2 * NQ * 1024
-                                     : delta + static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD;
-        const Rsrc in_rsrc = make_rsrc(base4, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
-        const uint32_t roff0 = delta + static_cast<uint32_t>(2 * lane) * (rb + 1); // filter byte of row 2j
-        const uint32_t roff1 = roff0 + rb + 1;
-        const uint32_t mis0 = slab ? 0u : (roff0 + 1) & 3, mis1 = slab ? 0u : (roff1 + 1) & 3;
-        const int doff0 = static_cast<int>(roff0 + 1 - mis0) - skew0 * CB; // group 0's first dword, row 2j
-        const int doff1 = static_cast<int>(roff1 + 1 - mis1) - skew1 * CB;
+        static_assert(NQ * 4 == GD, "a group is NQ 16-byte pieces per row");
+        const uint64_t extent = 128ull + static_cast<uint64_t>((nsteps + kG - 1) / kG) * 2 * NQ * 1024;
+        const Rsrc in_rsrc = make_rsrc(region, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
 
         // boundary hand-off: the previous band's last row (read by lanes
         // 0..WG/2-1, one granule pair each; offsets out of range otherwise)
@@ -479,28 +439,17 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // instructions per group is fixed and s_waitcnt counts stay exact:
         // a group waits only for the loads issued one group earlier
         uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
-        // (both layouts issue the same loads per group -- NQ 16-byte loads
-        // and one dword per row -- so the s_waitcnt counts hold for either;
-        // a slab's dword is the unused alignbyte carry: out of range, zero)
-        static_assert(NQ * 4 + 1 == GD, "a group is NQ 16-byte pieces and the carry dword per row");
         auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
-            if (slab) {
-                const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
+            const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
 #pragma unroll
-                for (int q = 0; q < NQ; q++) {
-                    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
-                    const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
+            for (int q = 0; q < NQ; q++) {
+                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
+                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
 #pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        d0[4 * q + e] = a[e];
-                        d1[4 * q + e] = b[e];
-                    }
+                for (int e = 0; e < 4; e++) {
+                    d0[4 * q + e] = a[e];
+                    d1[4 * q + e] = b[e];
                 }
-                d0[GD - 1] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, kOOR, 0, 0);
-                d1[GD - 1] = __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, kOOR, 0, 0);
-            } else {
-                load_dwords<GD>(d0, in_rsrc, doff0 + g0 * CB);
-                load_dwords<GD>(d1, in_rsrc, doff1 + g0 * CB);
             }
         };
         // window of kG chunks of the previous band's last row: WG granules
@@ -626,7 +575,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // entry and back edge), so the same number of dropped stores follows
         // the first loads here.
         {
-            const Rsrc none = make_rsrc(base4, 0u); // extent 0: every store is dropped
+            const Rsrc none = make_rsrc(region, 0u); // extent 0: every store is dropped
 #pragma unroll
             for (int i = 0; i < 2 * kG + (kG / FL) * NR; i++) // distinct, unmergeable offsets
                 __builtin_amdgcn_raw_buffer_store_b32(0u, none, 4096 * i + lane * 4, 0, 0);
@@ -673,23 +622,18 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 // ---- filtered bytes of both rows' chunks, packed
                 uint32_t f[CB];
 #pragma unroll
-                for (int w = 0; w < CW; w++) {
-                    const uint32_t lo = __builtin_amdgcn_alignbyte(A0[st * CW + w + 1], A0[st * CW + w], mis0);
-                    const uint32_t hi = __builtin_amdgcn_alignbyte(A1[st * CW + w + 1], A1[st * CW + w], mis1);
+                for (int w = 0; w < CW; w++)
 #pragma unroll
                     for (int b = 0; b < 4; b++)
-                        f[4 * w + b] = __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | (4u + b) << 16 | static_cast<uint32_t>(b));
-                }
-                // ---- a row outputs zeros until its first chunk (k < 0), so
-                // that chunk starts from zero left / up / up-left
-                const uint32_t vmask = (k0 >= 0 ? 0x000000ffu : 0u) | (k1 >= 0 ? 0x00ff0000u : 0u);
+                        f[4 * w + b] = __builtin_amdgcn_perm(A1[st * CW + w], A0[st * CW + w],
+                                                             0x0c000c00u | (4u + b) << 16 | static_cast<uint32_t>(b));
                 // ---- reconstruct CB byte pairs, left to right
                 uint32_t o[CB];
 #pragma unroll
                 for (int i = 0; i < CB; i++) {
                     const uint32_t a = i < BPP ? left[i] : o[i < BPP ? 0 : i - BPP];
                     const uint32_t c = i < BPP ? ul[i] : up[i < BPP ? 0 : i - BPP];
-                    o[i] = recon_pair(f[i], a, up[i], c, pf, vmask);
+                    o[i] = recon_pair(f[i], a, up[i], c, pf);
                 }
 #pragma unroll
                 for (int i = 0; i < BPP; i++) {
@@ -705,11 +649,14 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                     plo[w] = __builtin_amdgcn_perm(x23, x01, 0x05040100u);
                     phi[w] = __builtin_amdgcn_perm(x23, x01, 0x07060302u);
                 }
-                const bool act0 = ok0 && k0 >= 0 && k0 < nchunks, act1 = ok1 && k1 >= 0 && k1 < nchunks;
-                *reinterpret_cast<v4u *>(&ring[act0 ? ring0 + (k0 & (kSlots - 1)) * 4 : kTrash]) =
+                // (a chunk k < 0 lands in the slot of chunk k + 16, which
+                // overwrites it before any flush reads it; past the row's end
+                // the trash slot keeps its unflushed last chunks)
+                *reinterpret_cast<v4u *>(&ring[k0 < nchunks ? ring0 + (k0 & (kSlots - 1)) * 4 : kTrash]) =
                     expand_chunk<DEPTH, TRNS>(ps, plo);
-                *reinterpret_cast<v4u *>(&ring[act1 ? ring1 + (k1 & (kSlots - 1)) * 4 : kTrash]) =
+                *reinterpret_cast<v4u *>(&ring[k1 < nchunks ? ring1 + (k1 & (kSlots - 1)) * 4 : kTrash]) =
                     expand_chunk<DEPTH, TRNS>(ps, phi);
+                const bool act1 = ok1 && k1 >= 0 && k1 < nchunks;
                 // ---- publish the band's last row (row 127: lane 63's high
                 // half) as {data, epoch} granules: the data is the flag
                 {

@@ -526,13 +526,16 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
     for (int i = 0; i < n_frames; i++) {
         if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
         const bool trns = frames[i].use_transparent != 0;
-        const bool pair = png_use_pair(frames[i].depth, frames[i].interlace, trns, frames[i].width,
-                                       frames[i].out_stride);
+        // the paired-row kernel reads band slabs only; stream-layout frames
+        // take the one-row-per-lane kernel
+        const bool pair_ok = png_use_pair(frames[i].depth, frames[i].interlace, trns, frames[i].width,
+                                          frames[i].out_stride);
         if (frames[i].layout > ZPX_PNG_LAYOUT_SLAB) return ZPX_E_INVALID_ARGUMENT;
-        if (frames[i].layout == ZPX_PNG_LAYOUT_SLAB && !pair) {
+        if (frames[i].layout == ZPX_PNG_LAYOUT_SLAB && !pair_ok) {
             ctx->last_error = "png: a slab-layout frame needs the paired-row kernel (zpx_png_stream_slab)";
             return ZPX_E_INVALID_ARGUMENT;
         }
+        const bool pair = frames[i].layout == ZPX_PNG_LAYOUT_SLAB;
         by_depth[{frames[i].depth, pair, pair && trns}].push_back(i);
     }
     uint64_t bytes = 0;
@@ -1151,18 +1154,26 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
     const uint32_t W = 64, H = 2 * band_rows, rb = W * 3;
     std::vector<uint8_t> filt(size_t(H) * (rb + 1) + ZPX_PNG_INPUT_PAD, 0);
     for (uint32_t y = 0; y < H; y++) filt[size_t(y) * (rb + 1)] = 2;
-    DevBuf din, dout, ctl, bound, dpass, dsched;
-    HIPCHK(ctx, din.alloc(filt.size()));
-    HIPCHK(ctx, hipMemcpy(din.ptr, filt.data(), filt.size(), hipMemcpyHostToDevice));
-    HIPCHK(ctx, dout.alloc(size_t(W) * H * 4));
     zpx_png_frame f;
     memset(&f, 0, sizeof(f));
     f.width = W;
     f.height = H;
     f.depth = ZPX_PNG_TC8;
+    f.out_stride = size_t(W) * 4;
+    if (pair) { // the paired-row kernel reads the band slab (png_slab.cpp)
+        std::vector<uint64_t> off;
+        f.filtered = filt.data();
+        std::vector<uint8_t> slab(png_slab_layout(f, off));
+        png_slab_fill(f, off, slab.data());
+        filt.swap(slab);
+        f.layout = ZPX_PNG_LAYOUT_SLAB;
+    }
+    DevBuf din, dout, ctl, bound, dpass, dsched;
+    HIPCHK(ctx, din.alloc(filt.size()));
+    HIPCHK(ctx, hipMemcpy(din.ptr, filt.data(), filt.size(), hipMemcpyHostToDevice));
+    HIPCHK(ctx, dout.alloc(size_t(W) * H * 4));
     f.filtered = din.as<uint8_t>();
     f.out = dout.as<uint8_t>();
-    f.out_stride = size_t(W) * 4;
     std::vector<DevPngPass> passes;
     std::vector<uint32_t> rbs;
     uint64_t bytes = 0;
