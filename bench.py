@@ -294,12 +294,19 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
             raise SystemExit("parity failure: Adam7 RGBA16 PNG != oracle")
     wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, 1, ws)
     pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
+    atraffic = None
+    try:
+        ta = json.load(open(args.traffic_json)).get("adam7_rgba16", {})
+        if ta.get("images") == args.images and ta.get("size") == args.size:
+            atraffic = ta.get("hbm_bytes_per_launch")
+    except Exception:
+        atraffic = None
     out["png_adam7_rgba16"] = {
         "value": round(pb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
         "kernel_ms_per_launch": round(kern_ms, 3),
         "roofline": {"bound": "hbm", "achieved": round(pb.bytes / (kern_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(pb.bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                     "algorithmic_bytes_per_launch": pb.bytes},
+                     "traffic": atraffic, "algorithmic_bytes_per_launch": pb.bytes},
         "host_inflate_mpix_s": round(W * H / t_inf / 1e6, 1),
         "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64, configs[4]"}}
     del pb

@@ -4,8 +4,9 @@
 //     a lower ticket (the kernels' no-deadlock rule), and tickets go longest
 //     row first;
 //   - png_adam7_stage / png_adam7_rebase: passes 1-5 redirected into the
-//     quarter image Q (every Q pixel written exactly once), passes 6-7
-//     writing the image, pass 6 pointing at a merge job naming Q, and
+//     staging areas Q2 / S4 / S5 (every even-row, even-column pixel written
+//     exactly once, where pass 6's merge looks it up), passes 6-7 writing
+//     the image, pass 6 pointing at its merge job, and
 //     png_plan_bands putting passes 6-7 (and only those) in the second
 //     launch's schedule;
 //   - dev_jpeg_frame: the quant-pair tables of the block kernel's row pass.
@@ -99,29 +100,45 @@ int main()
     uint8_t *base = reinterpret_cast<uint8_t *>((reinterpret_cast<uintptr_t>(staging.data()) + 255) & ~uintptr_t(255));
     std::vector<DevAdam7Merge> jobs_dev(2);
     png_adam7_rebase(passes, st, base, jobs_dev.data());
-    // passes 1-5 write the quarter image Q (pixel (2X, 2Y) at Q[Y][X]): in
-    // Q's coordinates, inside the image's own Q, and together they cover every
-    // Q pixel exactly once
+    // passes 1-5 write the staging areas of DevAdam7Merge (S5: pass 5 as
+    // is, S4: pass 4 as is, Q2[Y][X] = pixel (4X, 4Y): passes 1-3), inside
+    // the staging, every even-row / even-column pixel exactly once, at the
+    // place pass 6's merge (png_pair_kernels.hip a7_even) looks it up
     static const uint32_t kA7[5][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4}, {0, 2, 2, 4}};
     for (int k = 0; k < 2; k++) {
         const DevAdam7Merge &m = st.jobs[k];
-        const uint32_t qw = (imgs[k].w + 1) / 2, qh = (imgs[k].h + 1) / 2;
-        CHECK(m.width == imgs[k].w && m.qstride % 128 == 0 && m.qstride >= uint64_t(qw) * 8);
-        CHECK((reinterpret_cast<uintptr_t>(m.q) & 255) == 0 && m.q >= base && m.q + m.qstride * qh <= base + st.bytes);
-        std::vector<int> cover(size_t(qw) * qh, 0);
+        const uint32_t W = imgs[k].w, H = imgs[k].h, ob = imgs[k].obpx;
+        CHECK(m.width == W);
+        const uint8_t *areas[3] = {m.q2, m.s4, m.s5};
+        const uint64_t strides[3] = {m.q2stride, m.s4stride, m.s5stride};
+        const uint64_t aw[3] = {(W + 3) / 4, (W - 2 + 3) / 4, (W + 1) / 2}, ah[3] = {(H + 3) / 4, (H + 3) / 4, (H - 2 + 3) / 4};
+        for (int a = 0; a < 3; a++) {
+            CHECK((reinterpret_cast<uintptr_t>(areas[a]) & 255) == 0 && strides[a] % 128 == 0 && strides[a] >= aw[a] * ob);
+            CHECK(areas[a] >= base && areas[a] + strides[a] * ah[a] <= base + st.bytes);
+        }
+        // the merge's lookup of image pixel (x = 2X, y even)
+        auto lookup = [&](uint32_t x, uint32_t y) -> const uint8_t * {
+            const uint32_t X = x / 2;
+            if (y & 2) return m.s5 + uint64_t((y - 2) >> 2) * m.s5stride + uint64_t(X) * ob;
+            if (X & 1) return m.s4 + uint64_t(y >> 2) * m.s4stride + uint64_t(X >> 1) * ob;
+            return m.q2 + uint64_t(y >> 2) * m.q2stride + uint64_t(X >> 1) * ob;
+        };
+        std::map<const uint8_t *, int> written;
         for (int p = 0; p < 5; p++) {
             const DevPngPass &d = passes[first_of[k] + p];
-            CHECK(d.out == m.q && d.out_stride == m.qstride && !d.launch2 && d.merge == nullptr);
-            CHECK(d.xo * 2 == kA7[p][0] && d.yo * 2 == kA7[p][1] && d.xf * 2 == kA7[p][2] && d.yf * 2 == kA7[p][3]);
+            CHECK(!d.launch2 && d.merge == nullptr);
+            CHECK(d.out == (p <= 2 ? m.q2 : p == 3 ? m.s4 : m.s5));
             for (uint32_t r = 0; r < d.rows; r++)
                 for (uint32_t c = 0; c < d.width; c++) {
-                    const uint32_t X = c * d.xf + d.xo, Y = r * d.yf + d.yo;
-                    CHECK(X < qw && Y < qh);
-                    if (X < qw && Y < qh) cover[size_t(Y) * qw + X]++;
+                    const uint8_t *at = d.out + uint64_t(r * d.yf + d.yo) * d.out_stride + uint64_t(c * d.xf + d.xo) * ob;
+                    const uint32_t x = c * kA7[p][2] + kA7[p][0], y = r * kA7[p][3] + kA7[p][1];
+                    CHECK(x < W && y < H && x % 2 == 0 && y % 2 == 0 && at == lookup(x, y));
+                    written[at]++;
                 }
         }
+        CHECK(written.size() == size_t((W + 1) / 2) * ((H + 1) / 2));
         bool once = true;
-        for (int c : cover) once &= c == 1;
+        for (auto &kv : written) once &= kv.second == 1;
         CHECK(once);
     }
     // passes 6 and 7 of each Adam7 image still write the image: pass 7 the

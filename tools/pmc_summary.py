@@ -54,6 +54,28 @@ if len(sys.argv) > 2 and jk in out:
         tr["coeff_bits"] = json.load(open(os.path.join(base, "fetch.json")))["config"]["coeff_bits"]
     except Exception:
         tr["coeff_bits"] = 16
+    # the paired-row PNG kernel reads the band slab (png_slab.cpp): 1 KiB
+    # contiguous per load instruction, the streaming shape the x2 is
+    # calibrated on (tools/ubench/png_load_pattern mode 2 reads that shape)
+    if "png_pair" in out:
+        p = out["png_pair"]
+        tr["png"] = {"kernel": "png_pair_kernel<TC8>", "images": tr["images"], "size": tr["size"],
+                     "fetch_bytes_per_launch": 2 * p["FETCH_SIZE"] * 1024,
+                     "write_bytes_per_launch": p["WRITE_SIZE"] * 1024,
+                     "note": "FETCH_SIZE x2 (slab loads: 1 KiB contiguous per instruction) + WRITE_SIZE, "
+                             "KiB -> B, mean per dispatch"}
+        tr["png"]["hbm_bytes_per_launch"] = tr["png"]["fetch_bytes_per_launch"] + tr["png"]["write_bytes_per_launch"]
+    if "png_pair_d15" in out and "png_pair_d15_merge" in out:
+        a, b = out["png_pair_d15"], out["png_pair_d15_merge"]
+        tr["adam7_rgba16"] = {
+            "kernel": "png_pair_kernel<TCA16> x2 (passes 1-5 to staging; passes 6-7 merging it)",
+            "images": tr["images"], "size": tr["size"],
+            "fetch_bytes_per_launch": 2 * (a["FETCH_SIZE"] + b["FETCH_SIZE"]) * 1024,
+            "write_bytes_per_launch": (a["WRITE_SIZE"] + b["WRITE_SIZE"]) * 1024,
+            "note": "both launches of one plan launch; FETCH_SIZE x2 (slab loads 1 KiB contiguous per "
+                    "instruction; pass 6's staging reads 64 B contiguous per 8 lanes) + WRITE_SIZE"}
+        t = tr["adam7_rgba16"]
+        t["hbm_bytes_per_launch"] = t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"]
     if "png_unfilter" in out:
         p = out["png_unfilter"]
         tr["png_unfilter"] = {"fetch_bytes_per_launch": 2 * p["FETCH_SIZE"] * 1024,

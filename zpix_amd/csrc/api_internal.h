@@ -256,18 +256,21 @@ inline PngBandPlan png_plan_bands(int depth, bool pair, std::vector<DevPngPass> 
 }
 
 
-// Adam7 through a staging area (paired-row kernel).  The pixels of passes
-// 1-5 are exactly those with an even row and an even column: they are
-// unfiltered into the quarter image Q[Y][X] = pixel (2X, 2Y) -- pass 5 its
-// odd rows whole, passes 1-4 its even rows, 2 or 4 pixels apart -- and pass
-// 6 then writes every even row y of the image whole: its own pixels at the
-// odd columns, row y / 2 of Q at the even ones (16-byte loads, whole lines).
-// Pass 7 writes the odd rows directly.  Passes 6 and 7 run in a second
-// launch of the kernel over their own band schedule (PngBandPlan::sched2),
-// so Q is complete and visible when pass 6 reads it.  Every row of the
-// image is then written once, whole: the scatter of all passes xf apart
-// into the image took 8.1 ms per 64 x 4K RGBA16, staging passes 1-6 plus a
-// merge kernel 6.5.
+// Adam7 through staging areas (paired-row kernel).  The pixels of passes
+// 1-5 are exactly those with an even row and an even column; they are
+// unfiltered into staging (DevAdam7Merge): pass 5 as is (S5), pass 4 as is
+// (S4), passes 1-3 into Q2[Y][X] = pixel (4X, 4Y) -- pass 3 its odd rows
+// whole, passes 1 and 2 its even rows, 2 pixels apart -- and pass 6 then
+// writes every even row y of the image whole: its own pixels at the odd
+// columns, the staged ones at the even columns (two 8-byte loads per 16
+// output bytes, whole-line stores).  Pass 7 writes the odd rows directly.
+// Passes 6 and 7 run in a second launch of the kernel over their own band
+// schedule (PngBandPlan::sched2), so the staging is complete and visible
+// when pass 6 reads it.  Every row of the image is then written once, whole:
+// the scatter of all passes xf apart into the image took 8.1 ms per 64 x 4K
+// RGBA16, staging passes 1-6 plus a merge kernel 6.5, passes 1-4 stored
+// 2-4 pixels apart into one quarter image Q 5.43 (1.76 ms of it the first
+// launch; 1.03 with their stores contiguous).
 struct Adam7Stage {
     std::vector<DevAdam7Merge> jobs; // q relative to the staging base until png_adam7_rebase
     std::vector<size_t> merge_pass;  // jobs[j]'s pass 6 (index into passes)
@@ -284,14 +287,18 @@ inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPng
     for (size_t i = first; i < passes.size(); i++)
         if (passes[i].xo == 1 && passes[i].xf == 2) p6 = i;
     if (p6 == ~size_t(0)) return; // (no pass 6: a 1-pixel-wide image, which png_pair_supported never takes)
-    const uint64_t qw = (uint64_t(f.width) + 1) / 2, qh = (uint64_t(f.height) + 1) / 2;
-    const uint64_t qstride = (qw * obpx + 127) & ~uint64_t(127);
-    st.bytes = (st.bytes + 255) & ~size_t(255);
-    const size_t q = st.bytes;
-    st.bytes += qstride * qh;
+    const uint64_t W = f.width, H = f.height;
+    auto area = [&](uint64_t w, uint64_t h, uint64_t &stride) {
+        stride = (w * obpx + 127) & ~uint64_t(127);
+        st.bytes = (st.bytes + 255) & ~size_t(255);
+        const size_t at = st.bytes;
+        st.bytes += stride * h;
+        return reinterpret_cast<const uint8_t *>(static_cast<uintptr_t>(at));
+    };
     DevAdam7Merge m{};
-    m.q = reinterpret_cast<const uint8_t *>(static_cast<uintptr_t>(q));
-    m.qstride = qstride;
+    m.q2 = area((W + 3) / 4, (H + 3) / 4, m.q2stride);                     // pixel (4X, 4Y)
+    m.s4 = area(W > 2 ? (W - 2 + 3) / 4 : 0, (H + 3) / 4, m.s4stride);     // pass 4
+    m.s5 = area((W + 1) / 2, H > 2 ? (H - 2 + 3) / 4 : 0, m.s5stride);     // pass 5
     m.width = f.width;
     for (size_t i = first; i < passes.size(); i++) {
         DevPngPass &d = passes[i];
@@ -302,13 +309,19 @@ inline void png_adam7_stage(const zpx_png_frame &f, int obpx, std::vector<DevPng
             d.launch2 = 1;
             continue;
         }
-        // passes 1-5 in Q's coordinates: (x, y) -> (x / 2, y / 2)
-        d.out = reinterpret_cast<uint8_t *>(static_cast<uintptr_t>(q));
-        d.out_stride = qstride;
-        d.xo /= 2;
-        d.yo /= 2;
-        d.xf /= 2;
-        d.yf /= 2;
+        if (pno <= 2) { // passes 1-3 in Q2's coordinates: (x, y) -> (x / 4, y / 4)
+            d.out = const_cast<uint8_t *>(m.q2);
+            d.out_stride = m.q2stride;
+            d.xo /= 4;
+            d.yo /= 4;
+            d.xf /= 4;
+            d.yf /= 4;
+        } else { // passes 4, 5: their own pixels, as is
+            d.out = const_cast<uint8_t *>(pno == 3 ? m.s4 : m.s5);
+            d.out_stride = pno == 3 ? m.s4stride : m.s5stride;
+            d.xo = d.yo = 0;
+            d.xf = d.yf = 1;
+        }
         st.staged.push_back(i);
     }
     // (a placeholder until png_adam7_rebase points it at the device job:
@@ -323,7 +336,9 @@ inline void png_adam7_rebase(std::vector<DevPngPass> &passes, Adam7Stage &st, ui
 {
     for (size_t i : st.staged) passes[i].out = base + reinterpret_cast<uintptr_t>(passes[i].out);
     for (size_t j = 0; j < st.jobs.size(); j++) {
-        st.jobs[j].q = base + reinterpret_cast<uintptr_t>(st.jobs[j].q);
+        st.jobs[j].q2 = base + reinterpret_cast<uintptr_t>(st.jobs[j].q2);
+        st.jobs[j].s4 = base + reinterpret_cast<uintptr_t>(st.jobs[j].s4);
+        st.jobs[j].s5 = base + reinterpret_cast<uintptr_t>(st.jobs[j].s5);
         passes[st.merge_pass[j]].merge = jobs + j;
     }
 }

@@ -45,13 +45,18 @@ struct DevPngPass {
 };
 
 // Adam7 on the paired-row kernel, per interlaced image: passes 1-5 are
-// unfiltered into the quarter image Q[Y][X] = pixel (2X, 2Y) -- the
-// even-row, even-column pixels, which are exactly theirs -- and pass 6 (the
-// odd columns of the even rows) writes every even row y whole, taking its
-// even columns from row y / 2 of Q (png_pair_kernels.hip).
+// unfiltered into staging -- exactly the even-row, even-column pixels -- and
+// pass 6 (the odd columns of the even rows) writes every even row y whole,
+// taking its even columns x = 2X from the staging (png_pair_kernels.hip):
+//   y = 2 mod 4:            pass 5 as is, S5[(y - 2) / 4][X]
+//   y = 0 mod 4, X odd:     pass 4 as is, S4[y / 4][(X - 1) / 2]
+//   y = 0 mod 4, X even:    Q2[y / 4][X / 2], Q2[Y][X'] = pixel (4X', 4Y):
+//                           pass 3 its odd rows whole, passes 1 and 2 its
+//                           even rows' even and odd columns
+// so only passes 1 and 2 (1/32 of the pixels) store pixels apart.
 struct DevAdam7Merge {
-    const uint8_t *q;         // Q, ceil(W / 2) x ceil(H / 2) pixels
-    uint64_t qstride;         // bytes between rows of Q
+    const uint8_t *q2, *s4, *s5;
+    uint64_t q2stride, s4stride, s5stride; // bytes between rows
     uint32_t width;           // image width in pixels
     uint32_t pad;
 };

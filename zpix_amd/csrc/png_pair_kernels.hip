@@ -229,19 +229,38 @@ __device__ __forceinline__ void put_partial(const DevPngPass &ps, gu8 *orow, int
     }
 }
 
-// ---- Adam7 pass 6 (xo 1, xf 2, yo 0, yf 2) merged with the quarter image Q
-// of passes 1-5 (`interlacing`, png/decoder.zig:59-67; mergePassInto
-// :1289-1373): the pixel at even column x = 2p of even image row y is
-// Q[y / 2][p].
+// ---- Adam7 pass 6 (xo 1, xf 2, yo 0, yf 2) merged with the staged passes
+// 1-5 (`interlacing`, png/decoder.zig:59-67; mergePassInto :1289-1373;
+// DevAdam7Merge): the pixel at even column x = 2X of even image row y.
 struct A7Src {
-    const uint8_t *q;
-    uint64_t qstride;
+    const uint8_t *q2, *s4, *s5;
+    uint64_t q2stride, s4stride, s5stride;
     uint32_t width; // image pixels
 };
 template <int OBPX>
-__device__ __forceinline__ const ZPX_GLOBAL uint8_t *a7_even(const A7Src &a, uint32_t p, uint32_t y)
+__device__ __forceinline__ const ZPX_GLOBAL uint8_t *a7_even(const A7Src &a, uint32_t X, uint32_t y)
 {
-    return (const ZPX_GLOBAL uint8_t *)(a.q + static_cast<uint64_t>(y >> 1) * a.qstride + static_cast<uint64_t>(p) * OBPX);
+    const uint8_t *p;
+    if (y & 2) p = a.s5 + static_cast<uint64_t>((y - 2) >> 2) * a.s5stride + static_cast<uint64_t>(X) * OBPX;
+    else if (X & 1) p = a.s4 + static_cast<uint64_t>(y >> 2) * a.s4stride + static_cast<uint64_t>(X >> 1) * OBPX;
+    else p = a.q2 + static_cast<uint64_t>(y >> 2) * a.q2stride + static_cast<uint64_t>(X >> 1) * OBPX;
+    return (const ZPX_GLOBAL uint8_t *)p;
+}
+// the staged pixels X = C k .. C k + C - 1 (C = 16 / OBPX) of even row y as
+// two 8-byte loads, in X order
+template <int OBPX>
+__device__ __forceinline__ v4u a7_chunk(const A7Src &a, uint32_t k, uint32_t y)
+{
+    const uint32_t X0 = k * (16 / OBPX);
+    const bool s5 = (y & 2) != 0;
+    const uint64_t row = s5 ? (y - 2) >> 2 : y >> 2;
+    const uint8_t *pa = s5 ? a.s5 + row * a.s5stride + static_cast<uint64_t>(X0) * OBPX
+                           : a.q2 + row * a.q2stride + static_cast<uint64_t>(X0 >> 1) * OBPX;
+    const uint8_t *pb = s5 ? pa + 8 : a.s4 + row * a.s4stride + static_cast<uint64_t>(X0 >> 1) * OBPX;
+    const v2u va = *reinterpret_cast<const ZPX_GLOBAL v2u *>((const ZPX_GLOBAL uint8_t *)pa);
+    const v2u vb = *reinterpret_cast<const ZPX_GLOBAL v2u *>((const ZPX_GLOBAL uint8_t *)pb);
+    if constexpr (OBPX == 8) return v4u{va[0], va[1], vb[0], vb[1]};
+    else return s5 ? v4u{va[0], va[1], vb[0], vb[1]} : v4u{va[0], vb[0], va[1], vb[1]}; // Q2 / S4 alternate
 }
 // one pixel's OBPX bytes (4 or 8) as dwords
 template <int OBPX>
@@ -352,8 +371,12 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         A7Src a7{};
         if (merge) {
             const DevAdam7Merge &m = *ps.merge;
-            a7.q = m.q;
-            a7.qstride = m.qstride;
+            a7.q2 = m.q2;
+            a7.s4 = m.s4;
+            a7.s5 = m.s5;
+            a7.q2stride = m.q2stride;
+            a7.s4stride = m.s4stride;
+            a7.s5stride = m.s5stride;
             a7.width = m.width;
         }
         const int nchunks = static_cast<int>(((rb + BPP - 1) / BPP + C - 1) / C);
@@ -472,7 +495,12 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             const bool p0 = min(d0, nfull) / FL > fl0, p1 = min(d1, nfull) / FL > fl1;
             const int r0 = 2 * lane, r1 = r0 + 1; // row r's state at fst[(r % RPR) * NR + r / RPR]
             const int x0 = (r0 % RPR) * NR + r0 / RPR, x1 = (r1 % RPR) * NR + r1 / RPR;
-            if (ps.xf == 1) {
+#ifdef ZPX_AB_NOSCATTER
+            const bool xf1 = !merge;
+#else
+            const bool xf1 = ps.xf == 1;
+#endif
+            if (xf1) {
                 fso[x0] = p0 ? static_cast<uint32_t>(r0) * static_cast<uint32_t>(orow_bytes) + fl0 * (FL * 16) : kOOR;
                 fso[x1] = p1 ? static_cast<uint32_t>(r1) * static_cast<uint32_t>(orow_bytes) + fl1 * (FL * 16) : kOOR;
                 fsr[x0] = 4 * ring0 + ((fl0 * FL) & (kSlots - 1)) * 16;
@@ -484,7 +512,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             fl0 += p0 ? 1 : 0;
             fl1 += p1 ? 1 : 0;
             wave_lds_sync();
-            if (ps.xf == 1) { // contiguous rows: every round's ring read first, then the 16-byte stores
+            if (xf1) { // contiguous rows: every round's ring read first, then the 16-byte stores
                 uint32_t so[NR], sr[NR];
 #pragma unroll
                 for (int q = 0; q < NR / 4; q++) {
@@ -538,15 +566,15 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                         }
                     });
             } else if constexpr (MERGE) { // Adam7 pass 6: 32 contiguous bytes per lane, whole lines per lane group
-                // every round's Q pixels first (one 16-byte load each, in flight together), then the stores
+                // every round's staged pixels first (two 8-byte loads each, in flight together), then the stores
                 v4u e[NR];
 #pragma unroll
                 for (int i = 0; i < NR; i++) {
                     const int r = RPR * i + lane / FL;
                     const bool post = blk[i] != 0xffffu;
-                    const uint32_t k = (post ? blk[i] : 0u) * FL + lane % FL;
+                    const uint32_t k = post ? blk[i] * FL + lane % FL : 0u;
                     const uint32_t y = post ? 2 * (base + r) : 0u; // (row 0, pixel 0: a valid address)
-                    e[i] = *reinterpret_cast<const ZPX_GLOBAL v4u *>(a7_even<T::OBPX>(a7, post ? k * C : 0u, y));
+                    e[i] = a7_chunk<T::OBPX>(a7, k, y);
                 }
 #pragma unroll
                 for (int i = 0; i < NR; i++)
