@@ -556,6 +556,10 @@ def main():
         t0 = time.perf_counter()
         streams = [png.Stream(d) for d in pdatas]
         t_inf = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for st in streams:  # the paired-row kernel's band slab (host, png_slab.cpp; PngBatch reuses it)
+            st.slab()
+        t_slab = time.perf_counter() - t0
         log(f"[rank {rank}] PNG generated in {t_gen:.1f}s, host inflate {args.distinct * W * H / t_inf / 1e6:.1f} MPix/s")
         slots = [i % args.distinct for i in range(args.images)]
         pb = device.PngBatch(streams, slots=slots, ctx=ctx)
@@ -585,7 +589,8 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": ptraffic, "kernel": pkernel,
                              "kernel_ms_per_launch": round(kern_ms, 3), "algorithmic_bytes_per_launch": pb.bytes},
-                "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1)}
+                "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1),
+                "host_slab_mpix_s": round(args.distinct * W * H / t_slab / 1e6, 1)}
         if result:
             result["png"] = pres
         else:
