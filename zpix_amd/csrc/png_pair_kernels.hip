@@ -251,6 +251,9 @@ __device__ __forceinline__ const ZPX_GLOBAL uint8_t *a7_even(const A7Src &a, uin
 template <int OBPX>
 __device__ __forceinline__ v4u a7_chunk(const A7Src &a, uint32_t k, uint32_t y)
 {
+#ifdef ZPX_AB_NOMERGELOAD
+    return v4u{k, y, k, y};
+#endif
     const uint32_t X0 = k * (16 / OBPX);
     const bool s5 = (y & 2) != 0;
     const uint64_t row = s5 ? (y - 2) >> 2 : y >> 2;
