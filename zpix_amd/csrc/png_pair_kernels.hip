@@ -105,16 +105,10 @@ ZPX_PAIR_TRAITS(ZPX_PNG_TCA16, 8, 8)
 // loads, 64 rows per instruction, are the limit rather than issue
 // (tools/ubench/png_load_pattern: this load shape alone reads the stream at
 // 2.2 TB/s).  So FL stays 8.
-#ifndef ZPX_AB_PAIR_FL
-#define ZPX_AB_PAIR_FL 8
-#endif
-#ifndef ZPX_AB_PAIR_W
-#define ZPX_AB_PAIR_W 1
-#endif
 template <int DEPTH, bool MERGE>
 struct PairShape {
-    static constexpr int FL = ZPX_AB_PAIR_FL;
-    static constexpr int W = ZPX_AB_PAIR_W;
+    static constexpr int FL = 8;
+    static constexpr int W = 1;
 };
 
 // ---- packed 16-bit helpers (v_pk_*_u16, v_pk_add_f16)
@@ -251,9 +245,6 @@ __device__ __forceinline__ const ZPX_GLOBAL uint8_t *a7_even(const A7Src &a, uin
 template <int OBPX>
 __device__ __forceinline__ v4u a7_chunk(const A7Src &a, uint32_t k, uint32_t y)
 {
-#ifdef ZPX_AB_NOMERGELOAD
-    return v4u{k, y, k, y};
-#endif
     const uint32_t X0 = k * (16 / OBPX);
     const bool s5 = (y & 2) != 0;
     const uint64_t row = s5 ? (y - 2) >> 2 : y >> 2;
@@ -498,11 +489,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             const bool p0 = min(d0, nfull) / FL > fl0, p1 = min(d1, nfull) / FL > fl1;
             const int r0 = 2 * lane, r1 = r0 + 1; // row r's state at fst[(r % RPR) * NR + r / RPR]
             const int x0 = (r0 % RPR) * NR + r0 / RPR, x1 = (r1 % RPR) * NR + r1 / RPR;
-#ifdef ZPX_AB_NOSCATTER
-            const bool xf1 = !merge;
-#else
             const bool xf1 = ps.xf == 1;
-#endif
             if (xf1) {
                 fso[x0] = p0 ? static_cast<uint32_t>(r0) * static_cast<uint32_t>(orow_bytes) + fl0 * (FL * 16) : kOOR;
                 fso[x1] = p1 ? static_cast<uint32_t>(r1) * static_cast<uint32_t>(orow_bytes) + fl1 * (FL * 16) : kOOR;
@@ -569,7 +556,10 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                         }
                     });
             } else if constexpr (MERGE) { // Adam7 pass 6: 32 contiguous bytes per lane, whole lines per lane group
-                // every round's staged pixels first (two 8-byte loads each, in flight together), then the stores
+                // every round's staged pixels first (two 8-byte loads each, in flight together), then the
+                // stores.  (Issuing the loads one step before the stores -- a posted block's ring slots
+                // survive that step -- measured no faster, 3.65 against 3.60 ms per second launch: the
+                // launch moves 17.2 GB at ~4.8 TB/s, and the staged pixels' 2.15 GB of reads are its cost.)
                 v4u e[NR];
 #pragma unroll
                 for (int i = 0; i < NR; i++) {
