@@ -171,20 +171,22 @@ def test_png_adam7_rgba16_4k_matches_oracle():
         assert np.array_equal(got.reshape(-1)[:want.size], want.reshape(-1))
 
 
-@pytest.mark.parametrize("layout", ["stream", "auto"])
+@pytest.mark.parametrize("layout", ["stream", "auto", "mixed"])
 @pytest.mark.parametrize("depth,ct,il", [(8, 2, 0), (8, 6, 1), (16, 6, 1), (16, 2, 0), (8, 0, 0), (16, 0, 0),
                                          (8, 2, 1)])
 def test_png_plan_layouts(layout, depth, ct, il):
     """zpx_png_plan on both input layouts: the band slab (paired-row kernel,
     zpx_png_stream_slab) and the inflated stream (one-row-per-lane kernel),
-    bit-exact against the oracle, in one ragged batch of four sizes."""
+    and both in one plan (two launches), bit-exact against the oracle, in
+    one ragged batch of four sizes."""
     datas = [S.png_generic(depth * 100 + ct * 10 + il + k, w, h, depth, ct, interlace=il, filters=(0, 1, 2, 3, 4))
              for k, (w, h) in enumerate([(17, 5), (130, 200), (33, 129), (300, 260)])]
     streams = [P.Stream(d) for d in datas]
     b = device.PngBatch(streams, layout=layout)
     # (auto: a slab wherever the paired-row kernel takes the image -- not
     # the smallest Adam7 passes -- and always the 300 x 260 one)
-    assert [f.layout for f in b.frames] == [int(layout == "auto" and st.slab() is not None) for st in streams]
+    slab = [layout == "auto" or (layout == "mixed" and i % 2 == 0) for i in range(4)]
+    assert [f.layout for f in b.frames] == [int(s and st.slab() is not None) for s, st in zip(slab, streams)]
     assert b.frames[3].layout == (1 if layout == "auto" else 0)
     b.launch(torch.cuda.current_stream().cuda_stream)
     b.status(torch.cuda.current_stream().cuda_stream)

@@ -178,7 +178,8 @@ class PngBatch:
                  ctx: context.Context | None = None, layout: str = "auto"):
         """layout: "auto" uploads each image's band slab where the
         paired-row kernel takes it (Stream.slab, what the decode and batch
-        paths do), else the inflated stream; "stream" always the stream."""
+        paths do), else the inflated stream; "stream" always the stream;
+        "mixed" (tests) slabs for even item indices, streams for odd ones."""
         torch = _torch()
         self.ctx = ctx or context.default(device)
         self.device = torch.device("cuda", self.ctx.device)
@@ -187,7 +188,7 @@ class PngBatch:
         frames = (_lib.zpx_png_frame * len(self.slots))()
         inputs = {}
         for i in set(self.slots):
-            sl = items[i].slab() if layout == "auto" else None
+            sl = items[i].slab() if layout == "auto" or (layout == "mixed" and i % 2 == 0) else None
             inputs[i] = (sl, 1) if sl is not None else (items[i].filtered(), 0)
         in_sizes = [_align(len(inputs[i][0])) for i in self.slots]
         out_sizes = [_align(items[i].frame.out_stride * items[i].frame.height) for i in self.slots]
