@@ -165,7 +165,7 @@ void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, s
 // Band slab (png_slab.cpp) of a frame whose `filtered` is the HOST stream:
 // the region offset of every band (returned size = slab bytes), then the fill.
 size_t png_slab_layout(const zpx_png_frame &f, std::vector<uint64_t> &band_off);
-void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, uint8_t *out);
+void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, uint8_t *out, int threads = 1);
 DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette);
 // planes + colour pass for frames the fused kernel does not take (async on st)
 int jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, DevBuf &planes, DevBuf &desc,

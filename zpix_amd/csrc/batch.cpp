@@ -196,7 +196,7 @@ void Pipeline::worker()
             // (the kernel reads the stream layout when this is refused)
             if (d->status == ZPX_OK && png_use_pair(d->ps.depth, d->ps.interlace, d->ps.use_transparent,
                                                     d->ps.width, size_t(d->ps.width) * d->ps.out_bpp))
-                (void)png_stream_build_slab(d->ps);
+                (void)png_stream_build_slab(d->ps, sub);
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
             d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, sub, jpeg_sparse_upload());

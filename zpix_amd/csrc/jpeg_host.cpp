@@ -1014,7 +1014,7 @@ int Decoder::restart_parallel(const Scan &sc, bool &done)
     if (k != nseg - 1) return 0;
     const int nthr = std::min<int>(threads_, nseg);
     std::atomic<bool> ok{true};
-    std::vector<FixedSink> sinks(static_cast<size_t>(nthr), FixedSink{o_});
+    std::vector<FixedSink> sinks(static_cast<size_t>(nthr), FixedSink{o_, {0, 0, 0, 0}, {}});
     // segment s: MCUs [s * ri, min(total, (s + 1) * ri)) from byte start[s]
     auto run_segment = [&](Decoder &d, FixedSink &sink, int32_t s) -> bool {
         d.pos_ = start[static_cast<size_t>(s)];

@@ -38,9 +38,9 @@ struct PngStream {
 };
 
 // The band slab of ps.data for the paired-row kernel (png_slab.cpp), into
-// ps.slab: ZPX_OK, ZPX_E_UNSUPPORTED when that kernel does not take the
-// image, ZPX_E_OUT_OF_MEMORY.
-int png_stream_build_slab(PngStream &ps);
+// ps.slab, bands split over `threads` threads: ZPX_OK, ZPX_E_UNSUPPORTED
+// when that kernel does not take the image, ZPX_E_OUT_OF_MEMORY.
+int png_stream_build_slab(PngStream &ps, int threads = 1);
 
 // Parse + inflate.  On success every row's data is present and every filter
 // byte is valid; otherwise returns the reference's error for the first row

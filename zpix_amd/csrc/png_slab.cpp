@@ -27,7 +27,9 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 
 #include "api_internal.h"
 #include "device_types.h"
@@ -107,7 +109,63 @@ size_t png_slab_layout(const zpx_png_frame &f, std::vector<uint64_t> &band_off)
     return off;
 }
 
-void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, uint8_t *out)
+namespace {
+
+// one band's region: filter bytes, the groups in the kernel's read order,
+// the alignment tail
+void fill_band(const DevPngPass &p, const SlabGeom &sg, uint32_t base, uint8_t *slab, size_t off)
+{
+    uint8_t *region = slab + off;
+    const int c = sg.cb / sg.bpp, nq = 8 * sg.cb / 16;
+    const uint32_t rb = p.row_bytes;
+    const int nchunks = static_cast<int>((p.width + c - 1) / c);
+    const uint32_t rows = std::min(128u, p.rows - base);
+    uint8_t *ft = region;
+    memset(ft, 0, 128);
+    for (uint32_t r = 0; r < rows; r++) ft[r] = p.filtered[size_t(base + r) * (rb + 1)];
+    int skew[128];
+    const int ngroups = (nchunks + band_skews(ft, rows, skew) + 7) / 8;
+    const size_t gbytes = size_t(2) * nq * 1024;
+    uint8_t *groups = region + 128;
+    const uint8_t *rowp[128];
+    for (int r = 0; r < 128; r++)
+        rowp[r] = static_cast<uint32_t>(r) < rows ? p.filtered + size_t(base + r) * (rb + 1) + 1 : nullptr;
+    // destination order: each (g, h) tile of NQ KiB is written whole,
+    // lane by lane, from 64 rows x 16 NQ bytes (21 ms per 4K tc8
+    // image on the build host, memcpy of the same bytes 6.5;
+    // non-temporal stores, 16 bytes a line at a time: 53 ms)
+    for (int g = 0; g < ngroups; g++)
+        for (int h = 0; h < 2; h++) {
+            uint8_t *gdst = groups + size_t(g) * gbytes + size_t(h) * nq * 1024;
+            for (int lane = 0; lane < 64; lane++) {
+                const int r = 2 * lane + h;
+                const uint8_t *row = rowp[r];
+                const int64_t start = (int64_t(8) * g - skew[r]) * sg.cb; // the group window's first byte
+                uint8_t *dst = gdst + size_t(lane) * 16;
+                if (row && start >= 0 && start + 16 * nq <= int64_t(rb)) {
+                    for (int q = 0; q < nq; q++)
+                        _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + q * 1024),
+                                         _mm_loadu_si128(reinterpret_cast<const __m128i *>(row + start + 16 * q)));
+                    continue;
+                }
+                for (int q = 0; q < nq; q++) {
+                    alignas(16) uint8_t piece[16];
+                    for (int i = 0; i < 16; i++) {
+                        const int64_t x = start + 16 * q + i;
+                        piece[i] = (row && x >= 0 && x < int64_t(rb)) ? row[x] : 0;
+                    }
+                    _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + q * 1024),
+                                     _mm_load_si128(reinterpret_cast<const __m128i *>(piece)));
+                }
+            }
+        }
+    const size_t end = off + 128 + size_t(ngroups) * gbytes; // (the next region starts at its alignment)
+    memset(slab + end, 0, align_up(end) - end);
+}
+
+} // namespace
+
+void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, uint8_t *out, int threads)
 {
     const SlabGeom sg = slab_geom(f.depth);
     std::vector<DevPngPass> passes;
@@ -116,65 +174,33 @@ void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off
     zpx_png_frame hf = f;
     hf.layout = ZPX_PNG_LAYOUT_STREAM;
     png_frame_passes(hf, passes, rowbytes, bytes);
-    const int c = sg.cb / sg.bpp, nq = 8 * sg.cb / 16;
     const size_t nb = band_off.size();
     memcpy(out, band_off.data(), nb * sizeof(uint64_t));
     memset(out + nb * sizeof(uint64_t), 0, align_up(nb * sizeof(uint64_t)) - nb * sizeof(uint64_t));
-    size_t b = 0;
-    for (const DevPngPass &p : passes) {
-        const uint32_t rb = p.row_bytes;
-        const int nchunks = static_cast<int>((p.width + c - 1) / c);
-        for (uint32_t base = 0; base < p.rows; base += 128, b++) {
-            const uint32_t rows = std::min(128u, p.rows - base);
-            uint8_t *region = out + band_off[b];
-            uint8_t *ft = region;
-            memset(ft, 0, 128);
-            for (uint32_t r = 0; r < rows; r++) ft[r] = p.filtered[size_t(base + r) * (rb + 1)];
-            int skew[128];
-            const int ngroups = (nchunks + band_skews(ft, rows, skew) + 7) / 8;
-            const size_t gbytes = size_t(2) * nq * 1024;
-            uint8_t *groups = region + 128;
-            const uint8_t *rowp[128];
-            for (int r = 0; r < 128; r++)
-                rowp[r] = static_cast<uint32_t>(r) < rows ? p.filtered + size_t(base + r) * (rb + 1) + 1 : nullptr;
-            // destination order: each (g, h) tile of NQ KiB is written whole,
-            // lane by lane, from 64 rows x 16 NQ bytes (21 ms per 4K tc8
-            // image on the build host, memcpy of the same bytes 6.5;
-            // non-temporal stores, 16 bytes a line at a time: 53 ms)
-            for (int g = 0; g < ngroups; g++)
-                for (int h = 0; h < 2; h++) {
-                    uint8_t *gdst = groups + size_t(g) * gbytes + size_t(h) * nq * 1024;
-                    for (int lane = 0; lane < 64; lane++) {
-                        const int r = 2 * lane + h;
-                        const uint8_t *row = rowp[r];
-                        const int64_t start = (int64_t(8) * g - skew[r]) * sg.cb; // the group window's first byte
-                        uint8_t *dst = gdst + size_t(lane) * 16;
-                        if (row && start >= 0 && start + 16 * nq <= int64_t(rb)) {
-                            for (int q = 0; q < nq; q++)
-                                _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + q * 1024),
-                                                 _mm_loadu_si128(reinterpret_cast<const __m128i *>(row + start + 16 * q)));
-                            continue;
-                        }
-                        for (int q = 0; q < nq; q++) {
-                            alignas(16) uint8_t piece[16];
-                            for (int i = 0; i < 16; i++) {
-                                const int64_t x = start + 16 * q + i;
-                                piece[i] = (row && x >= 0 && x < int64_t(rb)) ? row[x] : 0;
-                            }
-                            _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + q * 1024),
-                                             _mm_load_si128(reinterpret_cast<const __m128i *>(piece)));
-                        }
-                    }
-                }
-            // the region's alignment tail
-            const size_t end = band_off[b] + 128 + size_t(ngroups) * gbytes;
-            const size_t next = b + 1 < nb ? band_off[b + 1] : align_up(end);
-            memset(out + end, 0, next - end);
-        }
+    struct Job {
+        const DevPngPass *p;
+        uint32_t base;
+    };
+    std::vector<Job> jobs;
+    for (const DevPngPass &p : passes)
+        for (uint32_t base = 0; base < p.rows; base += 128) jobs.push_back(Job{&p, base});
+    auto run = [&](size_t b) { fill_band(*jobs[b].p, sg, jobs[b].base, out, band_off[b]); };
+    const int nthr = std::max(1, std::min<int>(threads, static_cast<int>(nb)));
+    std::atomic<size_t> next_job{0};
+    auto worker = [&] {
+        for (size_t b; (b = next_job.fetch_add(1)) < nb;) run(b);
+    };
+    std::vector<std::thread> pool;
+    try {
+        for (int i = 1; i < nthr; i++) pool.emplace_back(worker);
+    } catch (...) {
+        // (thread creation failed: this thread does the remaining bands)
     }
+    worker();
+    for (auto &t : pool) t.join();
 }
 
-int png_stream_build_slab(PngStream &ps)
+int png_stream_build_slab(PngStream &ps, int threads)
 {
     if (ps.slab_len) return ZPX_OK;
     if (!png_pair_supported(ps.depth, ps.interlace, ps.use_transparent, ps.width, size_t(ps.width) * ps.out_bpp))
@@ -193,7 +219,7 @@ int png_stream_build_slab(PngStream &ps)
     const size_t n = png_slab_layout(f, off);
     if (!n) return ZPX_E_UNSUPPORTED;
     if (!ps.slab.alloc(n, false)) return ZPX_E_OUT_OF_MEMORY;
-    png_slab_fill(f, off, static_cast<uint8_t *>(ps.slab.ptr));
+    png_slab_fill(f, off, static_cast<uint8_t *>(ps.slab.ptr), threads);
     ps.slab_len = n;
     return ZPX_OK;
 }

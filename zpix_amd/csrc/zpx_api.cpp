@@ -771,7 +771,7 @@ extern "C" int zpx_png_stream_slab(zpx_png_stream *s, const uint8_t **data, size
     if (!s || !data || !len) return ZPX_E_INVALID_ARGUMENT;
     return guarded([&] {
         if (!s->s.slab_len)
-            if (int e = png_stream_build_slab(s->s)) return e;
+            if (int e = png_stream_build_slab(s->s, png_inflate_threads())) return e;
         *data = static_cast<const uint8_t *>(s->s.slab.ptr);
         *len = s->s.slab_len;
         return static_cast<int>(ZPX_OK);
@@ -982,7 +982,7 @@ static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint
     // the paired-row kernel reads the band slab (png_slab.cpp)
     const bool slab = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, ps.width,
                                    size_t(ps.width) * ps.out_bpp) &&
-                      png_stream_build_slab(ps) == ZPX_OK;
+                      png_stream_build_slab(ps, png_inflate_threads()) == ZPX_OK;
     const void *hin = slab ? ps.slab.ptr : ps.data.ptr;
     const size_t in_len = slab ? ps.slab_len : ps.data_len + ZPX_PNG_INPUT_PAD;
     HIPCHK(ctx, din.alloc(in_len));
