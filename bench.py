@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--no-config5", action="store_true",
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
     ap.add_argument("--no-strip", action="store_true",
-                    help="skip the strip-kernel fallback line (4094-wide 4:2:0 frames the block kernel refuses)")
+                    help="skip the odd-width line (4094-wide 4:2:0 frames: block kernel, and the strip-kernel fallback forced)")
     ap.add_argument("--gather-chunks", type=int, default=8,
                     help="N>1: the end-to-end gather moves each rank's shard in this many chunks, each as soon "
                          "as it is decoded (1: one gather after the whole decode)")
@@ -315,36 +315,51 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
 
 
 def bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg):
-    """The fused kernel's fallback: frames the block-per-lane kernel refuses
-    take the strip kernel (jpeg_kernels.hip) -- here 4094x4096 4:2:0 (width
-    % 4 != 0, so its RGBA rows are not 16-byte pieces); the reference runs
-    reconstructBlock on every frame shape (decoder.zig:1553-1634).  A batch
-    of `images` slots of one frame, slot 0 checked against the oracle."""
+    """4094x4096 4:2:0 frames (width % 4 != 0: rows only dword aligned, each
+    row's last 4-pixel piece partial), `images` slots of one frame, slot 0
+    checked against the oracle: on the block kernel (its partial-piece path),
+    and -- the fused path's fallback, what every frame the block kernel
+    refuses (int32, non-narrow, 4:1:1, 2x2 chroma) takes -- on the strip
+    kernel through the test switch "jpeg_strip" (zpx_debug_option).  The
+    reference runs reconstructBlock on every frame shape
+    (decoder.zig:1553-1634)."""
+    from zpix_amd import _lib
+
     W, H = args.size - 2, args.size
     d = S.jpeg_420(3000 + rank, W, H, args.quality)
     co = jpeg.Coefficients(d)
-    jb = device.JpegBatch([co], slots=[0] * args.images, output="rgba", ctx=ctx)
-    if rank == 0:
-        import oracle_py as O
+    out = None
+    for kernel, strip in (("jpeg_block_kernel", 0), ("jpeg_rgba_kernel", 1)):
+        prev = _lib.lib().zpx_debug_option(b"jpeg_strip", strip)
+        try:
+            jb = device.JpegBatch([co], slots=[0] * args.images, output="rgba", ctx=ctx)
+            if rank == 0:
+                import oracle_py as O
 
-        jb.launch(torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        want = O.jpeg_decode(d).rgba_pixels()
-        if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want)):
-            raise SystemExit("parity failure: strip-kernel JPEG != oracle")
-    steps = max(3, args.steps // 2)
-    wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, 1, ws)
-    ach = jb.bytes / (kern_ms * 1e-3) / 1e9
-    out = {"value": round(jb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
-           "kernel_ms_per_launch": round(kern_ms, 3),
-           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "jpeg_rgba_kernel",
-                        "algorithmic_bytes_per_launch": jb.bytes},
-           "coeff_bits": int(co.frame.coeff_bits),
-           "config": {"workload": f"{args.images}x {W}x{H} baseline 4:2:0 JPEG -> RGBA through the strip kernel "
-                                  "(block kernel refuses width % 4 != 0)"}}
-    del jb
-    torch.cuda.empty_cache()
+                jb.launch(torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                want = O.jpeg_decode(d).rgba_pixels()
+                if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want)):
+                    raise SystemExit(f"parity failure: {kernel} on a width % 4 != 0 JPEG != oracle")
+            steps = max(3, args.steps // 2)
+            wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, 1, ws)
+        finally:
+            _lib.lib().zpx_debug_option(b"jpeg_strip", prev)
+        ach = jb.bytes / (kern_ms * 1e-3) / 1e9
+        line = {"value": round(jb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
+                "kernel_ms_per_launch": round(kern_ms, 3),
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": kernel,
+                             "algorithmic_bytes_per_launch": jb.bytes},
+                "coeff_bits": int(co.frame.coeff_bits),
+                "config": {"workload": f"{args.images}x {W}x{H} baseline 4:2:0 JPEG -> RGBA (width % 4 != 0) "
+                                       f"through {kernel}"}}
+        del jb
+        torch.cuda.empty_cache()
+        if out is None:
+            out = line
+        else:
+            out["strip_kernel"] = line
     return out
 
 
@@ -601,7 +616,7 @@ def main():
     if not args.no_config5 and not args.png_only:
         result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)
     if not args.no_strip and not args.png_only:
-        result["strip_fallback"] = bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg)
+        result["odd_width"] = bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg)
     if not args.no_e2e and not args.png_only:
         result["end_to_end"] = bench_e2e(args, torch, dist, ws, rank, ctx, S, threads)
     # ------------------------------------------------------------ CPU baseline (rank 0, N=1)

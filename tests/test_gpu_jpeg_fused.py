@@ -152,15 +152,15 @@ GEOMS = {
 @pytest.mark.parametrize("geom", list(GEOMS))
 @pytest.mark.parametrize("bits", [8, 16])
 def test_fused_random_grids_ycbcr(geom, bits):
-    """A ragged batch of three frames per geometry: two block-kernel sizes
-    (one wider than a 64-block task, one ending mid-MCU) and a width that
-    forces the strip kernel, all narrow."""
+    """A ragged batch of three frames per geometry: two sizes (one wider than
+    a 64-block task, one ending mid-MCU) and a width % 4 != 0 in a plan of
+    its own, all narrow."""
     rng = np.random.default_rng(sum(map(ord, geom)) * 31 + bits)
     ragged = [
         _frame_data(rng, GEOMS[geom], YCBCR, 1032, 40, bits, True),
         _frame_data(rng, GEOMS[geom], YCBCR, 100, 70, bits, True),
     ]
-    odd = [_frame_data(rng, GEOMS[geom], YCBCR, 77, 33, bits, True)]  # (a plan of its own: width % 4 != 0)
+    odd = [_frame_data(rng, GEOMS[geom], YCBCR, 77, 33, bits, True)]  # (width % 4 != 0)
     for frames in (ragged, odd):
         for fd, got in zip(frames, _run(frames)):
             assert np.array_equal(got, _expected(fd)), (fd["width"], fd["height"])
@@ -192,6 +192,20 @@ def test_fused_random_grids_wide(bits, narrow):
               _frame_data(rng, GEOMS["444"], YCBCR, 64, 16, bits, narrow)]
     for fd, got in zip(frames, _run(frames)):
         assert np.array_equal(got, _expected(fd))
+
+
+@pytest.mark.parametrize("geom", ["420", "444", "422"])
+@pytest.mark.parametrize("stride_pad", [0, 4])
+def test_fused_odd_widths_one_plan(geom, stride_pad):
+    """Widths % 4 != 0 on the block kernel (its partial last 4-pixel piece
+    leaves as dwords; rows only dword aligned take cached 16-byte stores), in
+    one ragged plan with aligned ones: the last piece in the first, a middle
+    and the last task of a row; nothing written past a row's pixels."""
+    rng = np.random.default_rng(len(geom) * 7 + stride_pad)
+    frames = [_frame_data(rng, GEOMS[geom], YCBCR, w, h, 8, True)
+              for w, h in [(1030, 24), (77, 33), (513, 16), (96, 8), (1021, 9), (5, 3)]]
+    for fd, got in zip(frames, _run(frames, stride_pad=stride_pad)):
+        assert np.array_equal(got, _expected(fd)), (fd["width"], fd["height"])
 
 
 def test_fused_padded_stride():

@@ -26,8 +26,8 @@ p=d.get('png');
 if p: print('png', p['ms_per_step'], p['roofline']['kernel_ms_per_launch'], p['roofline']['frac'])
 c=d.get('config5',{})
 for k,v in c.items(): print(k, v.get('kernel_ms_per_launch'), v['roofline']['frac'])
-s=d.get('strip_fallback')
-if s: print('strip', s['kernel_ms_per_launch'], s['roofline']['frac'])
+s=d.get('odd_width')
+if s: print('odd_width', s['kernel_ms_per_launch'], s['roofline']['frac'], 'strip', s['strip_kernel']['kernel_ms_per_launch'], s['strip_kernel']['roofline']['frac'])
 "
 fi
 echo iter done

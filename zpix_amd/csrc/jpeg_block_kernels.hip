@@ -4,8 +4,8 @@
 // YCbCr->RGB (Image.rgbaPixels over a YCbCrImage: image.zig:103-130, YCbCrAt
 // :614-630, Color.toRGBA .ycbcr color.zig:90-113).  It takes the common
 // frames -- int8/int16 coefficients within the 24-bit bound ("narrow"),
-// 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4 / gray, RGBA rows 16-byte aligned with a
-// width divisible by 4 -- and the strip kernel (jpeg_kernels.hip) the rest.
+// 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4 / gray, dword-aligned RGBA rows of any
+// width -- and the strip kernel (jpeg_kernels.hip) the rest.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -344,6 +344,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         uint8_t *rgba;
         int gwy, gwc, myy, width, height;
         uint32_t stride;
+        bool aligned; // RGBA rows 16-byte aligned: non-temporal whole-line stores, else cached ones
     };
     // (every field through readfirstlane: hipcc reads the descriptor with
     // vector loads, and a use of their results after the rare frame-change
@@ -376,6 +377,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         s.width = static_cast<int>(u32(static_cast<uint32_t>(fr.width)));
         s.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
         s.stride = u32(static_cast<uint32_t>(fr.rgba_stride));
+        s.aligned = ((s.stride | static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s.rgba))) & 15) == 0;
         s.qp = reinterpret_cast<uint64_t>(ptr(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(&fr.qp[0][0]))));
         return s;
     };
@@ -490,6 +492,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             reinterpret_cast<void *>(static_cast<uintptr_t>(oa_hi << 32 | oa_lo)), 0,
             __builtin_amdgcn_readfirstlane(rows_here * static_cast<int>(ostride)), 0x00020000);
         const bool y_present = ts.g[0] != nullptr;
+        // the task holding the image's last 4-pixel piece when that piece is
+        // partial (W % 4 != 0): its 1-3 pixels leave as dwords (uniform)
+        const int X0 = mx0 * H0 * 8;
+        const bool edge = (W & 3) != 0 && (W & ~3) >= X0 && (W & ~3) < X0 + 512;
 
         static_for<NP>([&](auto P) __attribute__((always_inline)) {
             constexpr int p = decltype(P)::value;
@@ -607,8 +613,8 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                         px[x] = rgba_pixel<COLOR>(s[8 * y + x], cb, cr, t);
                     }
                     const uint32_t rowoff = static_cast<uint32_t>(yr * 8 + y) * ostride;
-                    // (the host sends only frames with 16-byte aligned rows and
-                    // W % 4 == 0: a 4-pixel piece is wholly inside or outside)
+                    // (a 4-pixel piece wholly inside the row leaves as one
+                    // 16-byte store, the partial last one as dwords)
                     // the row's 512 pixels through the LDS row tile (swizzled,
                     // see otile): each store instruction then writes 1 KiB
                     // contiguous (whole lines)
@@ -618,11 +624,29 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     const u32x4 va = *reinterpret_cast<const u32x4 *>(otile + ra);
                     const u32x4 vb = *reinterpret_cast<const u32x4 *>(otile + 1024 + ra);
                     wave_lds_order();
-                    const int xa = mx0 * H0 * 8 + 4 * lane, xb = xa + 256;
-                    __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, xa < W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop,
-                                                           0, kStoreAux);
-                    __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, xb < W ? rowoff + static_cast<uint32_t>(xb) * 4 : kDrop,
-                                                           0, kStoreAux);
+                    const int xa = X0 + 4 * lane, xb = xa + 256;
+                    const uint32_t oa = xa + 4 <= W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop;
+                    const uint32_t ob = xb + 4 <= W ? rowoff + static_cast<uint32_t>(xb) * 4 : kDrop;
+                    if (ts.aligned) {
+                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, oa, 0, kStoreAux);
+                        __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, ob, 0, kStoreAux);
+                    } else { // dword-aligned rows (a width % 4 != 0 is the common case): cached stores
+                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, oa, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, ob, 0, 0);
+                    }
+                    if (edge) {
+                        // (extra stores after the pass's DMA: the next pass's
+                        // vmcnt wait then waits for more than it must, never less)
+#pragma unroll
+                        for (int u = 0; u < 3; u++) {
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                va[u], orsrc, xa + 4 > W && xa + u < W ? rowoff + static_cast<uint32_t>(xa + u) * 4 : kDrop,
+                                0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                vb[u], orsrc, xb + 4 > W && xb + u < W ? rowoff + static_cast<uint32_t>(xb + u) * 4 : kDrop,
+                                0, 0);
+                        }
+                    }
                 }
             }
         });

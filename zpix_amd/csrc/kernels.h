@@ -15,8 +15,8 @@ namespace zpx {
 int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh, int coeff_bits,
                        bool narrow, hipStream_t stream);
 bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc);
-// vec_out: every frame's RGBA rows are 16-byte aligned and its width is a
-// multiple of 4 (the block-per-lane kernel's store layout)
+// vec_out: every frame's RGBA rows are dword aligned (jpeg_rgba_vec_out:
+// the block-per-lane kernel's store layout)
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
                      int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, hipStream_t stream);
 

@@ -220,7 +220,9 @@ int zpx::launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_f
 
 bool zpx::jpeg_rgba_vec_out(const zpx_jpeg_frame &f)
 {
-    return (f.rgba_stride & 15) == 0 && (reinterpret_cast<uintptr_t>(f.rgba) & 15) == 0 && (f.width & 3) == 0;
+    // dword-aligned RGBA rows, any width (the block kernel stores a row's
+    // partial last 4-pixel piece as dwords)
+    return (f.rgba_stride & 3) == 0 && (reinterpret_cast<uintptr_t>(f.rgba) & 3) == 0;
 }
 // jpeg.decode's planes (reconstructBlock into makeImg's layout) followed by
 // the colour pass of Image.rgbaPixels, for the frames the fused kernel does
@@ -311,7 +313,7 @@ struct JpegGroup {
     bool narrow = true;
     int color = 0, h0 = 1, v0 = 1, hc = 1, vc = 1;
     int max_gw = 0, max_gh = 0, max_mxx = 0, max_myy = 0;
-    bool vec_out = true; // every frame: 16-byte aligned RGBA rows, width % 4 == 0
+    bool vec_out = true; // every frame: dword-aligned RGBA rows (jpeg_rgba_vec_out)
 };
 struct PngGroup {
     int depth = 0;
