@@ -151,6 +151,14 @@ __device__ __forceinline__ uint32_t pk_mul16(uint32_t a, uint32_t b)
 {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2u16, a) * __builtin_bit_cast(v2u16, b));
 }
+// (asm: hipcc turns select(m, x * a, x * b) into x * select(m, a, b), which
+// for scalar a, b costs two v_mov and a v_cndmask a dword)
+__device__ __forceinline__ uint32_t pk_mul16_asm(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
+    return r;
+}
 
 // Quant-pair rows (DevJpegFrame::qp, built by the host): per row r, four
 // dwords holding (q[r][1], q[r][7]), (q[r][5], q[r][3]), (q[r][2], q[r][6]),
@@ -192,10 +200,8 @@ __device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT
 {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const u32x4 q = qrow(r);
-        const u32x4 c = row_coef_pairs<CoefT>(raw, r);
-        const uint32_t p17 = pk_mul16(c[0], q[0]), p53 = pk_mul16(c[1], q[1]);
-        const uint32_t p26 = pk_mul16(c[2], q[2]), p04 = pk_mul16(c[3], q[3]);
+        const u32x4 p = qrow(r, row_coef_pairs<CoefT>(raw, r));
+        const uint32_t p17 = p[0], p53 = p[1], p26 = p[2], p04 = p[3];
         int32_t x4 = dot2<W1, W7>(p17), x5 = dot2<W7, -W1>(p17);
         int32_t x6 = dot2<W5, W3>(p53), x7 = dot2<W3, -W5>(p53);
         int32_t x8 = dot2<2048, 2048>(p04, 128), x0 = dot2<2048, -2048>(p04, 128);
@@ -282,6 +288,55 @@ __device__ __forceinline__ uint32_t rgba_pixel(int32_t Yv, int32_t cb, int32_t c
     }
 }
 
+// Two horizontally adjacent YCbCr pixels (color.zig:90-113 as rgba_pixel):
+// byte = clamp(v, 0, 0xffffff) >> 16 = clamp(v >> 16, 0, 255), so bytes 2-3
+// of each channel's v (v >> 16 as i16: |v| < 2^25) pair up in one dword and
+// v_sat_pk_u8_i16 clamps two at once -- 7 instructions a pixel instead of 8
+// (3 x v_med3_i32 + 2 x v_perm_b32 after the three v_mad_i32_i24).
+__device__ __forceinline__ uint32_t sat_pk_u8(uint32_t x)
+{
+    uint32_t r;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ void ycbcr_pair(int32_t y0, int32_t y1, ChromaTerms t0, ChromaTerms t1, uint32_t &p0,
+                                           uint32_t &p1)
+{
+    const uint32_t r0 = static_cast<uint32_t>(__mul24(y0, 0x10101) + t0.r), r1 = static_cast<uint32_t>(__mul24(y1, 0x10101) + t1.r);
+    const uint32_t g0 = static_cast<uint32_t>(__mul24(y0, 0x10101) + t0.g), g1 = static_cast<uint32_t>(__mul24(y1, 0x10101) + t1.g);
+    const uint32_t b0 = static_cast<uint32_t>(__mul24(y0, 0x10101) + t0.b), b1 = static_cast<uint32_t>(__mul24(y1, 0x10101) + t1.b);
+    const uint32_t s0 = sat_pk_u8(__builtin_amdgcn_perm(g0, r0, 0x07060302u)); // R0 G0
+    const uint32_t s1 = sat_pk_u8(__builtin_amdgcn_perm(g1, r1, 0x07060302u)); // R1 G1
+    const uint32_t sb = sat_pk_u8(__builtin_amdgcn_perm(b1, b0, 0x07060302u)); // B0 B1
+    p0 = __builtin_amdgcn_perm(sb, s0, 0x0d040100u);
+    p1 = __builtin_amdgcn_perm(sb, s1, 0x0d050100u);
+}
+
+// The same from the pixels' own signed-domain chroma samples (4:4:4: no
+// chroma terms to share), Y * 0x10101 + the level shift computed once a
+// pixel: 5 v_mad_i32_i24 instead of 3 + chroma_terms' 4.
+__device__ __forceinline__ void ycbcr_pair_direct(int32_t y0, int32_t y1, int32_t cb0, int32_t cr0, int32_t cb1,
+                                                  int32_t cr1, uint32_t &p0, uint32_t &p1)
+{
+    constexpr int32_t kY = 128 * 0x10101;
+    // (asm for G's chain: hipcc makes it two v_mul_i32_i24 + v_add3_u32)
+    auto mad = [](int32_t a, int32_t k, int32_t c) {
+        int32_t r;
+        asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+        return r;
+    };
+    const int32_t yk0 = __mul24(y0, 0x10101) + kY, yk1 = __mul24(y1, 0x10101) + kY;
+    const uint32_t r0 = static_cast<uint32_t>(__mul24(91881, cr0) + yk0), r1 = static_cast<uint32_t>(__mul24(91881, cr1) + yk1);
+    const uint32_t g0 = static_cast<uint32_t>(mad(cb0, -22554, mad(cr0, -46802, yk0)));
+    const uint32_t g1 = static_cast<uint32_t>(mad(cb1, -22554, mad(cr1, -46802, yk1)));
+    const uint32_t b0 = static_cast<uint32_t>(__mul24(116130, cb0) + yk0), b1 = static_cast<uint32_t>(__mul24(116130, cb1) + yk1);
+    const uint32_t s0 = sat_pk_u8(__builtin_amdgcn_perm(g0, r0, 0x07060302u));
+    const uint32_t s1 = sat_pk_u8(__builtin_amdgcn_perm(g1, r1, 0x07060302u));
+    const uint32_t sb = sat_pk_u8(__builtin_amdgcn_perm(b1, b0, 0x07060302u));
+    p0 = __builtin_amdgcn_perm(sb, s0, 0x0d040100u);
+    p1 = __builtin_amdgcn_perm(sb, s1, 0x0d050100u);
+}
+
 template <typename F, int... I>
 __device__ __forceinline__ void static_for_impl(F &f, std::integer_sequence<int, I...>)
 {
@@ -311,6 +366,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     constexpr int CTILE = (kGray || kInLane) ? 16 : CBH * 8 * CPX;
     constexpr int PXH = V0 * 8;                                 // task height in pixels
     constexpr int NS = 8 / RX;                                  // chroma samples per block row
+    constexpr bool kDirect = !kGray && RX == 1 && RY == 1;      // 4:4:4: no chroma terms shared between pixels
     static_assert(T * H0 == 64, "a task spans 64 luma block columns");
     // pass p: kind 0 = luma row, 1 = chroma through LDS, 2 = Cb in lane, 3 = Cr in lane
     constexpr auto kind = [](int p) {
@@ -344,7 +400,6 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         uint8_t *rgba;
         int gwy, gwc, myy, width, height;
         uint32_t stride;
-        bool aligned; // RGBA rows 16-byte aligned: non-temporal whole-line stores, else cached ones
     };
     // (every field through readfirstlane: hipcc reads the descriptor with
     // vector loads, and a use of their results after the rare frame-change
@@ -377,7 +432,6 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         s.width = static_cast<int>(u32(static_cast<uint32_t>(fr.width)));
         s.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
         s.stride = u32(static_cast<uint32_t>(fr.rgba_stride));
-        s.aligned = ((s.stride | static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s.rgba))) & 15) == 0;
         s.qp = reinterpret_cast<uint64_t>(ptr(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(&fr.qp[0][0]))));
         return s;
     };
@@ -522,14 +576,23 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 // (constant address space: s_load, outside the vmcnt the kernel counts)
                 typedef const __attribute__((address_space(4))) u32x4 *cq;
                 const uint64_t q0 = ts.qp + 128 * c0, q2 = ts.qp + 256;
-                idct_block_pairs<CoefT>(raw, [&](int r) __attribute__((always_inline)) {
+                // dequantized pairs of row r: coefficient pairs c x the row's quant pairs
+                idct_block_pairs<CoefT>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
                     const u32x4 a = *reinterpret_cast<cq>(q0 + 16 * r);
                     if constexpr (kind(p) == 1 && kCb > 0 && kCb < 64) {
                         const u32x4 b = *reinterpret_cast<cq>(q2 + 16 * r);
-                        return lane < kCb ? a : b;
+                        // (both products, then the select: 3 instructions a
+                        // dword against 4 for selecting the scalar quant pair)
+                        u32x4 o;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const uint32_t pa = pk_mul16_asm(c[i], a[i]), pb = pk_mul16_asm(c[i], b[i]);
+                            o[i] = lane < kCb ? pa : pb;
+                        }
+                        return o;
                     } else {
                         (void)q2;
-                        return a;
+                        return u32x4{pk_mul16(c[0], a[0]), pk_mul16(c[1], a[1]), pk_mul16(c[2], a[2]), pk_mul16(c[3], a[3])};
                     }
                 }, s);
             }
@@ -592,7 +655,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                                     cs[0][1] = *reinterpret_cast<const uint16_t *>(c1);
                                 }
                             }
-                            if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) {
+                            if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR && !kDirect) {
 #pragma unroll
                                 for (int u = 0; u < NS; u++)
                                     ct[u] = chroma_terms(sbyte(cs[u >> 2][0], u & 3), sbyte(cs[u >> 2][1], u & 3));
@@ -600,6 +663,17 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                         }
                     }
                     uint32_t px[8];
+                    if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR && kDirect) {
+#pragma unroll
+                        for (int x = 0; x < 8; x += 2)
+                            ycbcr_pair_direct(s[8 * y + x], s[8 * y + x + 1], sbyte(cs[x >> 2][0], x & 3),
+                                              sbyte(cs[x >> 2][1], x & 3), sbyte(cs[x >> 2][0], (x + 1) & 3),
+                                              sbyte(cs[x >> 2][1], (x + 1) & 3), px[x], px[x + 1]);
+                    } else if constexpr (COLOR == ZPX_JPEG_COLOR_YCBCR) {
+#pragma unroll
+                        for (int x = 0; x < 8; x += 2)
+                            ycbcr_pair(s[8 * y + x], s[8 * y + x + 1], ct[x / RX], ct[(x + 1) / RX], px[x], px[x + 1]);
+                    } else
 #pragma unroll
                     for (int x = 0; x < 8; x++) {
                         const int u = x / RX;
@@ -627,13 +701,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     const int xa = X0 + 4 * lane, xb = xa + 256;
                     const uint32_t oa = xa + 4 <= W ? rowoff + static_cast<uint32_t>(xa) * 4 : kDrop;
                     const uint32_t ob = xb + 4 <= W ? rowoff + static_cast<uint32_t>(xb) * 4 : kDrop;
-                    if (ts.aligned) {
-                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, oa, 0, kStoreAux);
-                        __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, ob, 0, kStoreAux);
-                    } else { // dword-aligned rows (a width % 4 != 0 is the common case): cached stores
-                        __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, oa, 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, ob, 0, 0);
-                    }
+                    // (non-temporal on dword-aligned rows too: 64 x 4094x4096
+                    // 1.61 -> 1.53 ms against cached stores there)
+                    __builtin_amdgcn_raw_buffer_store_b128(va, orsrc, oa, 0, kStoreAux);
+                    __builtin_amdgcn_raw_buffer_store_b128(vb, orsrc, ob, 0, kStoreAux);
                     if (edge) {
                         // (extra stores after the pass's DMA: the next pass's
                         // vmcnt wait then waits for more than it must, never less)
