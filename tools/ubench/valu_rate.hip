@@ -1,5 +1,5 @@
 // Microbenchmark (diagnostic, not product code): issue cost of the VALU
-// instructions the PNG kernels use, on gfx950, for 1 and 2 waves per SIMD.
+// instructions the PNG and JPEG kernels use, on gfx950, for 1, 2 and 4 waves per SIMD.
 // Each wave runs 8 independent chains of one instruction; cycles per
 // instruction per wave from s_memtime.  Build: hipcc --offload-arch=gfx950 -O3
 #include <hip/hip_runtime.h>
@@ -54,6 +54,15 @@ DEF_KERNEL(k_dot2, "v_dot2_i32_i16 %0, %0, %1, 0")
 DEF_KERNEL(k_pk_mul, "v_pk_mul_lo_u16 %0, %0, %1")
 DEF_KERNEL(k_med3, "v_med3_i32 %0, %0, %1, %1")
 DEF_KERNEL(k_dpp_add_wshr, "v_add_u32_dpp %0, %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf")
+// encoding size against operation: the same add as VOP3 (8 bytes), VOP2 with
+// a literal (8 bytes), VOP2 with an inline constant; a VOP1; a VOP2 shift
+DEF_KERNEL(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+DEF_KERNEL(k_add_lit, "v_add_u32_e32 %0, 0x1234, %0")
+DEF_KERNEL(k_add_inl, "v_add_u32_e32 %0, 7, %0")
+DEF_KERNEL(k_sat_pk, "v_sat_pk_u8_i16 %0, %0")
+DEF_KERNEL(k_ashr, "v_ashrrev_i32_e32 %0, 3, %0")
+DEF_KERNEL(k_mul24_e32, "v_mul_i32_i24_e32 %0, %1, %0")
+DEF_KERNEL(k_mul24_lit, "v_mul_i32_i24_e32 %0, 0x968, %0")
 
 typedef void (*KFn)(uint32_t *, uint64_t *, int);
 int main()
@@ -64,7 +73,10 @@ int main()
         {"v_alignbit_b32", k_alignbit}, {"v_sad_u16", k_sad}, {"v_min3_u32", k_min3}, {"v_bfe_u32", k_bfe},
         {"v_mov_dpp wave_shr:1", k_dpp_wshr}, {"v_mov_dpp row_shr:1", k_dpp_rshr},
         {"v_add_dpp wave_shr:1", k_dpp_add_wshr}, {"v_mul_lo_u32", k_mul_lo}, {"v_mad_i32_i24", k_mad24},
-        {"v_lshl_add_u32", k_lshl_add}, {"v_dot2_i32_i16", k_dot2}, {"v_pk_mul_lo_u16", k_pk_mul}, {"v_med3_i32", k_med3}};
+        {"v_lshl_add_u32", k_lshl_add}, {"v_dot2_i32_i16", k_dot2}, {"v_pk_mul_lo_u16", k_pk_mul}, {"v_med3_i32", k_med3},
+        {"v_add_u32_e64 (VOP3)", k_add_e64}, {"v_add_u32 literal", k_add_lit}, {"v_add_u32 inline", k_add_inl},
+        {"v_sat_pk_u8_i16 (VOP1)", k_sat_pk}, {"v_ashrrev_i32 (VOP2)", k_ashr}, {"v_mul_i32_i24_e32", k_mul24_e32},
+        {"v_mul_i32_i24 literal", k_mul24_lit}};
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int iters = 2000;
