@@ -583,7 +583,8 @@ int zpx_debug_option(const char *name, int value);
 int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, int32_t *grids, size_t grid_elems);
 /* Test hook: the speculative multi-threaded inflate of one zlib stream (the
  * PNG host stage for large single images).  1 when it decoded
- * the first `want` bytes into out on `threads` threads, 0 when it declined. */
+ * the first `want` bytes into out on `threads` threads, 0 when it declined;
+ * threads = 1 runs the serial fast decoder instead. */
 int zpx_debug_inflate_parallel(const uint8_t *z, size_t len, uint8_t *out, size_t want, int threads);
 
 #ifdef __cplusplus

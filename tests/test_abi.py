@@ -519,10 +519,12 @@ def _zstream(raw: bytes, level: int, strategy: int = 0, wbits: int = 15) -> byte
     return c.compress(raw) + c.flush()
 
 
-@pytest.mark.parametrize("threads", [2, 3, 8])
+@pytest.mark.parametrize("threads", [1, 2, 3, 8])
 def test_parallel_inflate_matches_zlib(threads):
     """The speculative multi-threaded inflate returns zlib's
-    bytes whenever it accepts a stream; it accepts the usual PNG streams."""
+    bytes whenever it accepts a stream; it accepts the usual PNG streams.
+    threads = 1 is the serial fast decoder (literal-pair tables), which must
+    accept every regular stream."""
     import ctypes as C
 
     rng = np.random.default_rng(threads)
@@ -552,4 +554,4 @@ def test_parallel_inflate_matches_zlib(threads):
             except zlib.error:
                 pytest.fail("accepted a stream whose first bytes zlib rejects")
             assert len(ref) >= len(raw) and out[:len(raw)].tobytes() == ref[:len(raw)]
-    assert accepted >= 8  # dynamic-block streams decode in parallel
+    assert accepted >= (16 if threads == 1 else 8)  # dynamic-block streams decode in parallel

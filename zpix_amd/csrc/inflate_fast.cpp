@@ -13,8 +13,9 @@
 // Design: 64-bit bit buffer refilled 8 bytes at a time; two-level decode
 // tables of 32-bit entries (an 11-bit literal/length root and an 8-bit
 // distance root, subtables for longer codes) whose entries carry the decoded
-// result -- literal byte, or length / distance base and extra-bit count -- so
-// a symbol costs one or two lookups and no bit loop.  A "fast zone" loop runs
+// result -- literal byte (or two, see pair_literals), or length / distance
+// base and extra-bit count -- so a symbol costs one or two lookups and no bit
+// loop.  A "fast zone" loop runs
 // while at least 32 input bytes and 258 + 8 output bytes remain: there no
 // literal needs an end-of-input or end-of-output check.
 #include "inflate_fast.h"
@@ -28,7 +29,7 @@
 namespace zpx {
 namespace {
 
-constexpr int kLitBits = 11, kDistBits = 8;
+constexpr int kLitBits = 12, kDistBits = 8;
 
 // entry: bits 0-4 = bits to drop; bits 5-8 = extra-bit count (length /
 // distance) or index bits (subtable); flags in bits 9-12; payload in bits
@@ -38,6 +39,7 @@ constexpr uint32_t kLiteral = 1u << 9;
 constexpr uint32_t kSub = 1u << 10;
 constexpr uint32_t kEob = 1u << 11;     // end of block
 constexpr uint32_t kInvalid = 1u << 12; // symbol 286/287 or distance 30/31
+constexpr uint32_t kLiteral2 = 1u << 13; // (with kLiteral) two literals: payload = first | second << 8
 inline uint32_t drop_of(uint32_t e) { return e & 31; }
 inline uint32_t extra_of(uint32_t e) { return (e >> 5) & 15; }
 inline uint32_t payload(uint32_t e) { return e >> 16; }
@@ -153,6 +155,34 @@ bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind
         }
     }
     return true;
+}
+
+// Literal pairs in the root table: an entry whose bits hold a literal of l1
+// bits followed by one of l2 bits, l1 + l2 <= root, decodes both (drop
+// l1 + l2) -- one lookup for two bytes.  The second code is read from the
+// entry at the index shifted by l1, which is valid when l2 <= root - l1
+// (the entry then depends only on its low l2 bits).  Noisy truecolor IDAT
+// streams are ~80 % literals of 5-8 bits.
+void pair_literals(uint32_t *t, int root)
+{
+    // (downwards: k >> l1 < k, so the entry read is still a single one)
+    for (int k = (1 << root) - 1; k > 0; k--) {
+        const uint32_t e1 = t[k];
+        if (!(e1 & kLiteral)) continue; // (subtable pointers never carry kLiteral)
+        const uint32_t l1 = drop_of(e1);
+        const uint32_t e2 = t[k >> l1];
+        if (!(e2 & kLiteral) || l1 + drop_of(e2) > uint32_t(root)) continue;
+        t[k] = kLiteral | kLiteral2 | (payload(e1) | payload(e2) << 8) << 16 | (l1 + drop_of(e2));
+    }
+}
+
+// One or two literals (a kLiteral entry) at o, in the fast zone: the second
+// slot is written either way (a single literal's is overwritten next)
+template <typename T> inline T *put_literals(T *o, uint32_t e)
+{
+    o[0] = static_cast<T>(payload(e) & 0xff);
+    o[1] = static_cast<T>(payload(e) >> 8);
+    return o + 1 + ((e >> 13) & 1);
 }
 
 struct Bits {
@@ -363,6 +393,7 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
         } else {
             return Run::Error;
         }
+        pair_literals(lit, kLitBits);
         if (b.overrun()) return Run::Error;
         // ---- the block's symbols
         T *o = out.p + out.o;
@@ -376,13 +407,13 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
                 b.refill_fast();
                 e = decode(b, lit, kLitBits);
                 if (e & kLiteral) {
-                    *o++ = static_cast<T>(payload(e));
+                    o = put_literals(o, e);
                     e = decode(b, lit, kLitBits);
                     if (e & kLiteral) {
-                        *o++ = static_cast<T>(payload(e));
+                        o = put_literals(o, e);
                         e = decode(b, lit, kLitBits);
                         if (e & kLiteral) {
-                            *o++ = static_cast<T>(payload(e));
+                            o = put_literals(o, e);
                             continue;
                         }
                     }
@@ -410,9 +441,11 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
             if (b.overrun() || (e & kInvalid)) return Run::Error;
             if (e & kLiteral) {
                 if (done >= want) break;
-                if (!out.room(1)) return Run::Error;
-                out.p[done] = static_cast<T>(payload(e));
-                o = out.p + done + 1;
+                const size_t n = std::min<size_t>((e & kLiteral2) ? 2 : 1, want - done);
+                if (!out.room(n)) return Run::Error;
+                out.p[done] = static_cast<T>(payload(e) & 0xff);
+                if (n == 2) out.p[done + 1] = static_cast<T>(payload(e) >> 8);
+                o = out.p + done + n;
                 continue;
             }
             if (e & kEob) break;

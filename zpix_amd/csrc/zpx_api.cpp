@@ -1298,13 +1298,16 @@ extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, i
     });
 }
 
-// Test hook for the speculative parallel inflate (inflate_parallel): 1 when it
-// decoded the first `want` bytes of the zlib stream `z` on `threads` threads,
-// 0 when it declined (the PNG path then decodes serially).
+// Test hook for the host inflate's fast decoders: 1 when the speculative
+// parallel inflate (threads >= 2; inflate_parallel) or, for threads = 1, the
+// serial fast decoder (inflate_fast) decoded the first `want` bytes of the
+// zlib stream `z`; 0 when it declined (the PNG path then falls back: to the
+// serial decoder, or from it to system zlib).
 extern "C" int zpx_debug_inflate_parallel(const uint8_t *z, size_t len, uint8_t *out, size_t want, int threads)
 {
     return guarded([&] {
         size_t produced = 0;
+        if (threads == 1) return inflate_fast(z, len, out, want, &produced) && produced == want ? 1 : 0;
         return inflate_parallel(z, len, out, want, &produced, threads) && produced == want ? 1 : 0;
     });
 }
