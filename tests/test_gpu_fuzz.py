@@ -1,0 +1,117 @@
+"""Randomized GPU parity: many small random images through the product paths,
+each bit-exact against the oracle.
+
+The other -m gpu tests pin chosen shapes; these draw shapes, depths,
+sampling geometries, qualities, filter mixes, widths that are not multiples
+of 4 and ragged batches from a seeded generator, so a shape rule no one
+thought of (a partial chunk, an odd Adam7 pass, a 4:2:2 frame next to a
+4:4:4 one in the same plan) meets the kernels.  Seeds are fixed: a failure
+names its case and reproduces.  The oracle restates decoder.zig /
+image.zig (tests/oracle_py.py); sizes stay small so the CPU side takes
+seconds.
+"""
+import numpy as np
+import pytest
+
+import oracle_py as O
+from tools import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from zpix_amd import device  # noqa: E402
+from zpix_amd import jpeg as J  # noqa: E402
+from zpix_amd import png as P  # noqa: E402
+
+# (bit depth, colour type) pairs PNG allows (png/decoder.zig:297-329)
+PNG_COMBOS = [(1, 0), (2, 0), (4, 0), (8, 0), (16, 0), (8, 2), (16, 2), (1, 3), (2, 3), (4, 3), (8, 3),
+              (8, 4), (16, 4), (8, 6), (16, 6)]
+
+
+def _png_case(rng):
+    depth, ct = PNG_COMBOS[int(rng.integers(len(PNG_COMBOS)))]
+    w, h = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+    il = int(rng.integers(2))
+    nf = int(rng.integers(1, 6))
+    filters = tuple(int(f) for f in rng.choice(5, nf, replace=False))
+    pal = bytes(rng.integers(0, 256, 3 * min(1 << depth, 200), dtype=np.uint8)) if ct == 3 else None
+    seed = int(rng.integers(1 << 30))
+    return (depth, ct, w, h, il, filters), S.png_generic(seed, w, h, depth, ct, interlace=il, filters=filters,
+                                                          palette=pal)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_png_decode_random(block):
+    """P.decode (the single-image path: inflate, plan, kernel choice per
+    image) on 40 random images a block."""
+    rng = np.random.default_rng(1000 + block)
+    for _ in range(40):
+        case, data = _png_case(rng)
+        want = O.png_decode(data)
+        got = P.decode(data)
+        assert got.kind == want.kind and tuple(got.rect) == tuple(want.rect), case
+        assert np.array_equal(got.pixels, want.pixels), case
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_png_batch_random(block):
+    """Ragged PngBatch plans of 8 random images (slab and stream layouts, one
+    or two kernels in one plan) against the oracle's pixels."""
+    rng = np.random.default_rng(2000 + block)
+    for _ in range(4):
+        cases, datas = zip(*[_png_case(rng) for _ in range(8)])
+        streams = [P.Stream(d) for d in datas]
+        layout = ("auto", "stream", "mixed")[int(rng.integers(3))]
+        b = device.PngBatch(streams, layout=layout)
+        b.launch(torch.cuda.current_stream().cuda_stream)
+        b.status(torch.cuda.current_stream().cuda_stream)
+        for s, d in enumerate(datas):
+            want = O.png_decode(d).pixels.reshape(-1)  # the image's own layout (out_stride x height)
+            got = b.output_tensor(s).cpu().numpy().reshape(-1)[:want.size]
+            assert np.array_equal(got, want), (layout, cases[s])
+
+
+def _jpeg_case(rng):
+    w, h = int(rng.integers(1, 260)), int(rng.integers(1, 260))
+    q = int(rng.integers(5, 101))
+    prog = bool(rng.integers(2))
+    seed = int(rng.integers(1 << 30))
+    if rng.random() < 0.15:
+        return ("gray", w, h, q, prog), S.jpeg_gray(seed, w, h, quality=q, progressive=prog)
+    sub = int(rng.integers(3))  # Pillow: 0 = 4:4:4, 1 = 4:2:2, 2 = 4:2:0
+    return (sub, w, h, q, prog), S.jpeg_subsampled(seed, w, h, sub, quality=q, progressive=prog)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_jpeg_decode_rgba_random(block):
+    """J.decode_rgba (host entropy decode, fused reconstruct + rgbaPixels) on
+    30 random JPEGs a block: sizes 1-259 (any width), qualities 5-100,
+    baseline and progressive, 4:4:4 / 4:2:2 / 4:2:0 / gray."""
+    rng = np.random.default_rng(3000 + block)
+    for _ in range(30):
+        case, data = _jpeg_case(rng)
+        want = O.jpeg_decode(data).rgba_pixels().reshape(-1)
+        got = J.decode_rgba(data).reshape(-1)
+        assert np.array_equal(got, want), case
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_jpeg_batch_random(block):
+    """Ragged JpegBatch plans of 6 random frames (mixed geometries, widths,
+    int8 / int16 transports: the block and strip kernels in one plan)."""
+    rng = np.random.default_rng(4000 + block)
+    for _ in range(4):
+        cases, datas = zip(*[_jpeg_case(rng) for _ in range(6)])
+        items = []
+        for d in datas:
+            co = J.Coefficients(d)
+            if co.frame.coeff_bits == 8 and rng.random() < 0.4:
+                co.widen(16)
+            items.append(co)
+        b = device.JpegBatch(items, output="rgba")
+        b.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for s, d in enumerate(datas):
+            want = O.jpeg_decode(d).rgba_pixels().reshape(-1)
+            got = b.output_tensor(s).cpu().numpy().reshape(-1)
+            assert np.array_equal(got[:want.size], want), (cases[s], items[s].frame.coeff_bits)
