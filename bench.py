@@ -268,7 +268,7 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want)):
             raise SystemExit("parity failure: progressive 4:4:4 JPEG != oracle")
     steps = max(3, args.steps // 2)
-    wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, 1, ws)
+    wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, args.warmup, ws)
     out["jpeg_progressive_444"] = {
         "value": round(jb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
         "kernel_ms_per_launch": round(kern_ms, 3),
@@ -292,7 +292,7 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         got = pb.output_tensor(0).cpu().numpy()
         if not np.array_equal(got.reshape(-1)[:want.size], want.reshape(-1)):
             raise SystemExit("parity failure: Adam7 RGBA16 PNG != oracle")
-    wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, 1, ws)
+    wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, args.warmup, ws)
     pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
     atraffic = None
     try:
@@ -342,7 +342,7 @@ def bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg):
                 if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), torch.from_numpy(want)):
                     raise SystemExit(f"parity failure: {kernel} on a width % 4 != 0 JPEG != oracle")
             steps = max(3, args.steps // 2)
-            wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, 1, ws)
+            wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, args.warmup, ws)
         finally:
             _lib.lib().zpx_debug_option(b"jpeg_strip", prev)
         ach = jb.bytes / (kern_ms * 1e-3) / 1e9
@@ -585,7 +585,7 @@ def main():
             got = pb.output_tensor(0).cpu().numpy().reshape(H, W, 4)
             if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
                 raise SystemExit("parity failure: GPU PNG unfilter != source pixels")
-        wall, kern_ms = timed_steps(torch, dist, pb.launch, max(3, args.steps // 2), 1, ws)
+        wall, kern_ms = timed_steps(torch, dist, pb.launch, max(3, args.steps // 2), args.warmup, ws)
         pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
         steps = max(3, args.steps // 2)
         pv = pb.pixels * ws * steps / wall / 1e6
@@ -609,7 +609,7 @@ def main():
         if result:
             result["png"] = pres
         else:
-            result = dict(pres, n_gpus=ws, warmup=1, higher_is_better=True, scaling="weak", vs_baseline=None,
+            result = dict(pres, n_gpus=ws, warmup=args.warmup, higher_is_better=True, scaling="weak", vs_baseline=None,
                           dtype="u8", data="synthetic PNG")
         del pb
     # ------------------------------------------------------------ configs[4] and end to end
