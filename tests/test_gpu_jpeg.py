@@ -218,9 +218,10 @@ def test_jpeg_batch_4k_fused_matches_oracle():
 
 
 def test_jpeg_4k_strip_kernel_matches_oracle():
-    """Frames the block kernel refuses take the strip kernel: a 4094-wide
-    4:2:0 frame (width % 4 != 0; bench line "strip_fallback"), and the bench
-    frame itself with the test switch "jpeg_strip" forcing it."""
+    """A 4094-wide 4:2:0 frame (width % 4 != 0: the block kernel's edge
+    tasks; bench line "odd_width"), and the bench frame on the strip kernel,
+    which the test switch "jpeg_strip" forces (the bench's
+    odd_width.strip_kernel line does the same)."""
     from zpix_amd import _lib
 
     data = S.jpeg_420(5, 4094, 4096)

@@ -6,9 +6,9 @@ oracle: zo_jpeg_reconstruct_grids (reconstructBlock, decoder.zig:1553-1634)
 into the reference's plane layout (makeImg, decoder.zig:1708-1783), then
 zo_rgba_pixels over the YCbCr / Gray image (Image.rgbaPixels,
 image.zig:103-130), or, for Adobe RGB frames, convertToRGB
-(decoder.zig:751-783) restated below.  Widths divisible by 4 with 16-byte rows
-take the block-per-lane kernel for int8/int16 "narrow" frames of its
-geometries; every other case takes the strip kernel.  The batches mix frame
+(decoder.zig:751-783) restated below.  Dword-aligned rows of any width take
+the block-per-lane kernel for int8/int16 "narrow" frames of its geometries;
+every other case takes the strip kernel.  The batches mix frame
 sizes (a ragged plan) and include never-scanned components.
 """
 import ctypes as C

@@ -158,7 +158,7 @@ void jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes
 DevJpegFrame dev_jpeg_frame(const zpx_jpeg_frame &f);
 bool jpeg_fusable(const zpx_jpeg_frame &f); // the fused RGBA kernel takes this frame
 int launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_frame, hipStream_t st);
-// 16-byte aligned RGBA rows and width % 4 == 0 (the block-per-lane kernel takes it)
+// dword-aligned RGBA rows, any width (the block-per-lane kernel takes it)
 bool jpeg_rgba_vec_out(const zpx_jpeg_frame &f);
 void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, std::vector<uint32_t> &rowbytes,
                       uint64_t &bytes);

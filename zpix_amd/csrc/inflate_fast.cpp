@@ -11,7 +11,7 @@
 // accepts too, and DEFLATE output is unique, so the bytes are identical.
 //
 // Design: 64-bit bit buffer refilled 8 bytes at a time; two-level decode
-// tables of 32-bit entries (an 11-bit literal/length root and an 8-bit
+// tables of 32-bit entries (a 12-bit literal/length root and an 8-bit
 // distance root, subtables for longer codes) whose entries carry the decoded
 // result -- literal byte (or two, see pair_literals), or length / distance
 // base and extra-bit count -- so a symbol costs one or two lookups and no bit
