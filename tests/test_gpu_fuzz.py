@@ -6,10 +6,12 @@ sampling geometries, qualities, filter mixes, widths that are not multiples
 of 4 and ragged batches from a seeded generator, so a shape rule no one
 thought of (a partial chunk, an odd Adam7 pass, a 4:2:2 frame next to a
 4:4:4 one in the same plan) meets the kernels.  Seeds are fixed: a failure
-names its case and reproduces.  The oracle restates decoder.zig /
+names its case and reproduces (ZPX_FUZZ_SEED=k explores other seeds).  The oracle restates decoder.zig /
 image.zig (tests/oracle_py.py); sizes stay small so the CPU side takes
 seconds.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -22,6 +24,10 @@ torch = pytest.importorskip("torch")
 from zpix_amd import device  # noqa: E402
 from zpix_amd import jpeg as J  # noqa: E402
 from zpix_amd import png as P  # noqa: E402
+
+# ZPX_FUZZ_SEED moves every block to other seeds (exploration runs); the
+# committed suite runs seed 0
+SEED = int(os.environ.get("ZPX_FUZZ_SEED", "0")) * 100000
 
 # (bit depth, colour type) pairs PNG allows (png/decoder.zig:297-329)
 PNG_COMBOS = [(1, 0), (2, 0), (4, 0), (8, 0), (16, 0), (8, 2), (16, 2), (1, 3), (2, 3), (4, 3), (8, 3),
@@ -44,7 +50,7 @@ def _png_case(rng):
 def test_png_decode_random(block):
     """P.decode (the single-image path: inflate, plan, kernel choice per
     image) on 40 random images a block."""
-    rng = np.random.default_rng(1000 + block)
+    rng = np.random.default_rng(SEED + 1000 + block)
     for _ in range(40):
         case, data = _png_case(rng)
         want = O.png_decode(data)
@@ -57,7 +63,7 @@ def test_png_decode_random(block):
 def test_png_batch_random(block):
     """Ragged PngBatch plans of 8 random images (slab and stream layouts, one
     or two kernels in one plan) against the oracle's pixels."""
-    rng = np.random.default_rng(2000 + block)
+    rng = np.random.default_rng(SEED + 2000 + block)
     for _ in range(4):
         cases, datas = zip(*[_png_case(rng) for _ in range(8)])
         streams = [P.Stream(d) for d in datas]
@@ -87,7 +93,7 @@ def test_jpeg_decode_rgba_random(block):
     """J.decode_rgba (host entropy decode, fused reconstruct + rgbaPixels) on
     30 random JPEGs a block: sizes 1-259 (any width), qualities 5-100,
     baseline and progressive, 4:4:4 / 4:2:2 / 4:2:0 / gray."""
-    rng = np.random.default_rng(3000 + block)
+    rng = np.random.default_rng(SEED + 3000 + block)
     for _ in range(30):
         case, data = _jpeg_case(rng)
         want = O.jpeg_decode(data).rgba_pixels().reshape(-1)
@@ -99,7 +105,7 @@ def test_jpeg_decode_rgba_random(block):
 def test_jpeg_batch_random(block):
     """Ragged JpegBatch plans of 6 random frames (mixed geometries, widths,
     int8 / int16 transports: the block and strip kernels in one plan)."""
-    rng = np.random.default_rng(4000 + block)
+    rng = np.random.default_rng(SEED + 4000 + block)
     for _ in range(4):
         cases, datas = zip(*[_jpeg_case(rng) for _ in range(6)])
         items = []
