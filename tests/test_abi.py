@@ -120,6 +120,48 @@ def test_host_coefficient_width_is_narrowest(path):
             assert pc.coeff_bytes[c] == oc.grids[c].size * want // 8
 
 
+@pytest.mark.parametrize("block", range(3))
+def test_host_entropy_random(block):
+    """The host entropy stage (processSos / Huffman / refinement,
+    decoder.zig) on 40 random JPEGs a block, seeded: sizes 1-299, qualities
+    5-100, baseline and progressive, 4:4:4 / 4:2:2 / 4:2:0 / gray, with and
+    without restart intervals (the restart-parallel scan path) -- every
+    grid, the frame geometry and the narrowest transport width as the
+    oracle's, or the oracle's error name where the reference refuses the
+    stream."""
+    import io
+
+    from PIL import Image
+
+    rng = np.random.default_rng(5000 + block)
+    for _ in range(40):
+        w, h = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        gray = rng.random() < 0.15
+        kw = dict(quality=int(rng.integers(5, 101)), progressive=bool(rng.integers(2)))
+        if not gray:
+            kw["subsampling"] = int(rng.integers(3))
+        if rng.random() < 0.4:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 40))
+        px = S.content(int(rng.integers(1 << 30)), w, h, 1 if gray else 3)
+        b = io.BytesIO()
+        Image.fromarray(px[..., 0] if gray else px).save(b, "JPEG", **kw)
+        data = b.getvalue()
+        case = (w, h, gray, kw)
+        try:
+            oc = O.jpeg_coefficients(data)
+        except O.OracleError as e:  # the reference's error, by name
+            assert _jpeg_err_product(data) == e.name, case
+            continue
+        pc = J.Coefficients(data)
+        f = pc.frame
+        assert (f.width, f.height, f.n_comp, f.mxx, f.myy) == (oc.width, oc.height, oc.n_comp, oc.mxx, oc.myy), case
+        m = max(int(np.abs(g).max()) for g in oc.grids if g is not None)
+        assert f.coeff_bits == (8 if m <= 127 else 16 if m <= 32767 else 32), case
+        for c in range(oc.n_comp):
+            assert (f.h[c], f.v[c]) == (oc.h[c], oc.v[c]), case
+            assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32)), (case, c)
+
+
 def _jpeg_err_product(data):
     try:
         J.Coefficients(data)
