@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-adam7", action="store_true", help="configs[4]: progressive JPEG line only (A/B runs)")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
+    ap.add_argument("--no-planar", action="store_true",
+                    help="skip the planar line (jpeg.load: the headline frames into Y/Cb/Cr planes)")
     ap.add_argument("--no-strip", action="store_true",
                     help="skip the odd-width line (4094-wide 4:2:0 frames: block kernel, and the strip-kernel fallback forced)")
     ap.add_argument("--gather-chunks", type=int, default=8,
@@ -311,6 +313,48 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64, configs[4]"}}
     del pb
     torch.cuda.empty_cache()
+    return out
+
+
+def bench_planar(args, torch, dist, ws, rank, ctx, device, jpeg, datas):
+    """jpeg.load's output (SURVEY §8(d) "2-planar"): the headline's frames
+    reconstructed into makeImg's Y/Cb/Cr planes (reconstructBlock,
+    src/jpeg/decoder.zig:1553-1634, :361-370) by the planar block kernel,
+    resident batch of `images` slots, int8 and int16 transports; slot 0
+    checked against the oracle's jpeg.decode planes before timing."""
+    out = {}
+    for bits in (8, 16):
+        cos = [jpeg.Coefficients(d).widen(bits) for d in datas]
+        if any(int(c.frame.coeff_bits) != bits for c in cos):
+            continue
+        slots = [i % len(cos) for i in range(args.images)]
+        jb = device.JpegBatch(cos, slots=slots, output="planes", ctx=ctx)
+        if rank == 0:
+            import oracle_py as O
+
+            jb.launch(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            want = torch.from_numpy(O.jpeg_decode(datas[0]).pixels)
+            if not torch.equal(jb.output_tensor(0).cpu(), want):
+                raise SystemExit(f"parity failure: planar int{bits} planes != oracle")
+        wall, kern_ms = timed_steps(torch, dist, jb.launch, args.steps, args.warmup, ws)
+        ach = jb.bytes / (kern_ms * 1e-3) / 1e9
+        out[f"int{bits}"] = {
+            "value": round(jb.pixels * ws * args.steps / wall / 1e6, 1), "unit": "MPixels/sec",
+            "kernel_ms_per_launch": round(kern_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "jpeg_plane_block_kernel",
+                         "traffic": None, "algorithmic_bytes_per_launch": jb.bytes},
+            "config": {"workload": f"{args.images}x {args.size}x{args.size} baseline 4:2:0 JPEG -> Y/Cb/Cr planes "
+                                   f"(jpeg.load), int{bits} coefficients"}}
+        try:
+            tp = json.load(open(args.traffic_json)).get(f"planar_int{bits}", {})
+            if tp.get("images") == args.images and tp.get("size") == args.size:
+                out[f"int{bits}"]["roofline"]["traffic"] = tp.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+        del jb
+        torch.cuda.empty_cache()
     return out
 
 
@@ -606,12 +650,40 @@ def main():
                              "kernel_ms_per_launch": round(kern_ms, 3), "algorithmic_bytes_per_launch": pb.bytes},
                 "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1),
                 "host_slab_mpix_s": round(args.distinct * W * H / t_slab / 1e6, 1)}
+        del pb
+        torch.cuda.empty_cache()
+        # the same images from the inflated stream (what parseIdat hands
+        # readImagePass, png/decoder.zig:516-523): every launch builds the
+        # band slab on the device (png_slab_kernels.hip), then the kernel
+        sb = device.PngBatch(streams, slots=slots, ctx=ctx, layout="stream")
+        if rank == 0:
+            sb.launch(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = sb.output_tensor(0).cpu().numpy().reshape(H, W, 4)
+            if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
+                raise SystemExit("parity failure: GPU PNG from the stream (device slab) != source pixels")
+        swall, skern = timed_steps(torch, dist, sb.launch, steps, args.warmup, ws)
+        sb.status(torch.cuda.current_stream().cuda_stream)
+        sach = sb.bytes / (skern * 1e-3) / 1e9
+        pres["stream_input"] = {
+            "value": round(sb.pixels * ws * steps / swall / 1e6, 1), "unit": "MPixels/sec",
+            "kernel_ms_per_launch": round(skern, 3),
+            "roofline": {"bound": "hbm", "achieved": round(sach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(sach / PEAK_HBM_GBS, 4), "kernel": "png_slab_kernel<12> + " + pkernel,
+                         "algorithmic_bytes_per_launch": sb.bytes},
+            "note": "inflated stream in HBM -> band slab built on the device -> unfilter: both kernels inside the "
+                    "timed plan; algorithmic bytes = stream read + RGBA write (the slab's write and re-read are "
+                    "the layout's cost)"}
+        del sb
+        torch.cuda.empty_cache()
         if result:
             result["png"] = pres
         else:
             result = dict(pres, n_gpus=ws, warmup=args.warmup, higher_is_better=True, scaling="weak", vs_baseline=None,
                           dtype="u8", data="synthetic PNG")
-        del pb
+    # ------------------------------------------------------------ planar (jpeg.load)
+    if not args.no_planar and not args.png_only:
+        result["planar"] = bench_planar(args, torch, dist, ws, rank, ctx, device, jpeg, datas)
     # ------------------------------------------------------------ configs[4] and end to end
     if not args.no_config5 and not args.png_only:
         result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)

@@ -363,10 +363,14 @@ enum zpx_png_depth {
 };
 /* Readable bytes the device input must have past its last filtered row. */
 #define ZPX_PNG_INPUT_PAD 256
-/* Layout of zpx_png_frame.filtered.  STREAM: the inflated stream as is.
- * SLAB: the same bytes rearranged per 128-row band in the order the
- * paired-row kernel reads them (zpx_png_stream_slab builds it on the host;
- * only for frames that kernel takes, i.e. zpx_png_stream_slab succeeds). */
+/* Layout of zpx_png_frame.filtered.  STREAM: the inflated stream as is
+ * (what parseIdat hands readImagePass, png/decoder.zig:516-523), followed by
+ * ZPX_PNG_INPUT_PAD readable bytes.  SLAB: the same bytes rearranged per
+ * 128-row band in the order the paired-row kernel reads them
+ * (zpx_png_stream_slab builds it on the host; only for frames that kernel
+ * takes, i.e. zpx_png_stream_slab succeeds).  A STREAM frame the paired-row
+ * kernel takes gets the same slab built on the device at each launch of its
+ * plan (png_slab_kernels.hip), so both layouts run on the same kernel. */
 enum zpx_png_layout { ZPX_PNG_LAYOUT_STREAM = 0, ZPX_PNG_LAYOUT_SLAB = 1 };
 
 /* One PNG image after host inflate (parseIdat, png/decoder.zig:404-545). */
@@ -387,7 +391,13 @@ typedef struct zpx_png_frame {
 
 /* Unfilter (Sub/Up/Avg/Paeth) + per-depth pixel store (+ Adam7 merge) of
  * readImagePass (png/decoder.zig:649-1149, 1289-1373).  Filter bytes must be
- * valid (<= 4): the host checks them (InvalidFilterType) before planning. */
+ * valid (<= 4): the host checks them (InvalidFilterType) before planning.
+ * Kernels: the paired-row kernel for RGB8/RGBA8/Gray8/Gray16/RGB16/RGBA16
+ * (interlaced or not, tRNS colour keys on RGB; either layout: a STREAM frame's
+ * slab is built on the device inside the launch), the one-row-per-lane kernel
+ * for every other depth (sub-byte gray, paletted, gray+alpha) and for STREAM
+ * frames the paired-row kernel declines (png_pair_supported: e.g. rows shorter
+ * than one 12/16-byte chunk, bands past the 2 GiB buffer range). */
 int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, int n_frames, zpx_plan **out);
 
 /* Enqueue the plan's kernels on `stream` (NULL = the context's stream). */
@@ -551,6 +561,15 @@ int zpx_batch_decode_sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *ite
  * receives the slower launch's wall time, which must stay about one spin
  * limit, not one per step. */
 int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *seconds);
+
+/* Test hook: the band slab of an inflated stream as the plans build it on the
+ * device (ZPX_PNG_LAYOUT_STREAM frames on the paired-row kernel), copied back
+ * to host `out` of `cap` bytes; *len receives its size (with out == NULL only
+ * the size).  Region sizes follow the geometry's largest skew, so the table
+ * of region offsets at its start differs from zpx_png_stream_slab's; every
+ * byte the kernel reads is equal.  ZPX_E_UNSUPPORTED when the paired-row
+ * kernel does not take the image. */
+int zpx_debug_png_device_slab(zpx_ctx *ctx, const zpx_png_stream *s, uint8_t *out, size_t cap, size_t *len);
 
 /* Number of scans the host entropy stage has decoded restart-interval-
  * parallel in this process (tests: the parallel path ran, not its serial

@@ -214,6 +214,48 @@ def test_batch_decode_sharded_fake_comm_send_recv(ndev):
         _lib.lib().zpx_debug_shard_fake_comm(prev)
 
 
+def test_batch_decode_sharded_concurrent_calls_share_comms():
+    """Two threads run sharded decodes at once, each on its own contexts but
+    on the same device set, so both use the one cached communicator set: a
+    call checks the set out for its whole gather (RCCL forbids one
+    communicator on two threads at once), so the calls take turns and both
+    results are exact."""
+    import threading
+
+    from zpix_amd import shard
+
+    bufs = mixed_buffers()[-6:]
+    dims = [batch._probe_dims(b) or (1, 1) for b in bufs]
+    want = [oracle_rgba(d) for d in bufs]
+    prev = _lib.lib().zpx_debug_shard_fake_comm(1)
+    results = {}
+    try:
+        def run(t):
+            ctxs = [zpix_amd.Context(0), zpix_amd.Context(0)]
+            dst = [torch.full((h, w, 4), 0x5a, dtype=torch.uint8, device="cuda:0") for w, h in dims]
+            statuses, _, gs = shard.decode_sharded(bufs, ctxs, dst, host_threads=2)
+            torch.cuda.synchronize()
+            results[t] = (statuses, [d.cpu().numpy() for d in dst], gs.gather_bytes)
+            for c in ctxs:
+                c.close()
+
+        ths = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    finally:
+        _lib.lib().zpx_debug_shard_fake_comm(prev)
+    assert sorted(results) == [0, 1]
+    for t in range(2):
+        statuses, got, moved = results[t]
+        assert moved > 0
+        for i, (w, status) in enumerate(want):
+            assert statuses[i] == status, (t, i)
+            if status == "Ok":
+                assert np.array_equal(got[i], w), (t, i)
+
+
 def test_batch_decode_sharded_rejects_host_dst():
     """Results gather into device memory: dst_on_host is an invalid argument."""
     ctxs = [zpix_amd.context.default(0)]

@@ -150,13 +150,28 @@ UNZIG = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19
 
 @pytest.mark.parametrize("coeff_bits,scale,narrow,rule", [
     (16, 64, 1, 0), (16, 2000, 0, 0), (32, 1 << 20, 0, 0), (32, 1 << 27, 0, 1), (16, 300, 1, 2),
-    (8, 128, 1, 0), (8, 128, 0, 1), (8, 128, 1, 2),
+    (8, 128, 1, 0), (8, 128, 0, 1), (8, 128, 1, 2), (8, 128, 1, 1), (16, 300, 1, 1),
 ])
-def test_planar_kernel_random_grids(coeff_bits, scale, narrow, rule):
+@pytest.mark.parametrize("geom", ["7x5", "70x3"])
+@pytest.mark.parametrize("kernel", ["block", "strip"])
+def test_planar_kernel_random_grids(coeff_bits, scale, narrow, rule, geom, kernel):
     """Random (incl. overflowing) coefficient grids: wrap-around i32 IDCT,
-    DC-only shortcut and clamp must match the oracle bit for bit."""
+    DC-only shortcut and clamp must match the oracle bit for bit -- on the
+    planar block kernel (narrow int8/int16 frames; 70 MCUs = 140 luma block
+    columns: three 64-block tasks a row, the last ragged) and on the
+    lane-per-row kernel the test switch "jpeg_strip" forces (what int32 and
+    wide frames take)."""
     rng = np.random.default_rng(coeff_bits + scale)
-    h, v, mxx, myy, width, height = [2, 1, 1], [2, 1, 1], 7, 5, 100, 70
+    mxx, myy = (7, 5) if geom == "7x5" else (70, 3)
+    h, v, width, height = [2, 1, 1], [2, 1, 1], mxx * 16 - 12, myy * 16 - 10
+    prev = _lib.lib().zpx_debug_option(b"jpeg_strip", 1 if kernel == "strip" else 0)
+    try:
+        _planar_random_case(rng, coeff_bits, scale, narrow, rule, h, v, mxx, myy, width, height)
+    finally:
+        _lib.lib().zpx_debug_option(b"jpeg_strip", prev)
+
+
+def _planar_random_case(rng, coeff_bits, scale, narrow, rule, h, v, mxx, myy, width, height):
     grids, qz = [], []
     for c in range(3):
         nb = mxx * h[c] * myy * v[c]
@@ -254,6 +269,41 @@ def test_jpeg_batch_planes_matches_oracle():
     want = O.jpeg_decode(data)
     got = batch.output_tensor(0).cpu().numpy()
     assert np.array_equal(got, want.pixels)
+
+
+def test_jpeg_batch_planes_ragged_geometries():
+    """One planes plan over frames of different sizes and samplings (one
+    planar launch per geometry group, ragged MCU grids inside a group),
+    baseline and progressive, int8 and int16 transports."""
+    datas = [S.jpeg_subsampled(11, 333, 177, 2), S.jpeg_subsampled(12, 1030, 70, 2),
+             S.jpeg_subsampled(13, 129, 65, 0, progressive=True), S.jpeg_subsampled(14, 250, 99, 1),
+             S.jpeg_gray(15, 203, 77), S.jpeg_subsampled(16, 17, 9, 2, progressive=True)]
+    for bits in (8, 16):
+        cos = [J.Coefficients(d) for d in datas]
+        for co in cos:
+            co.widen(bits)
+        batch = device.JpegBatch(cos, slots=[0, 1, 2, 3, 4, 5, 1, 0], output="planes")
+        batch.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for s, i in enumerate(batch.slots):
+            want = O.jpeg_decode(datas[i])
+            assert np.array_equal(batch.output_tensor(s).cpu().numpy(), want.pixels), (bits, s)
+
+
+@pytest.mark.parametrize("bits", [8, 16])
+def test_jpeg_batch_4k_planes_matches_oracle(bits):
+    """jpeg.load's planes of the bench frame (4096^2 4:2:0 q75, the bench's
+    "planar" line) on the planar block kernel, both transports."""
+    data = S.jpeg_420(0, 4096, 4096)
+    co = J.Coefficients(data)
+    co.widen(bits)
+    batch = device.JpegBatch([co], slots=[0, 0], output="planes")
+    batch.launch(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = torch.from_numpy(O.jpeg_decode(data).pixels)
+    for s in range(2):
+        assert torch.equal(batch.output_tensor(s).cpu(), want)
+    assert batch.bytes == 2 * (393216 * 64 * (bits // 8) + 393216 * 64 + 3 * 256)
 
 
 def test_jpeg_progressive_444_4k_matches_oracle():

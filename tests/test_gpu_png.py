@@ -105,13 +105,17 @@ def test_png_tc8_mixed_filters(w, h):
     assert_same_png(P.decode(data), O.png_decode(data))
 
 
-def test_png_bench_size_roundtrip():
+@pytest.mark.parametrize("layout", ["auto", "stream"])
+def test_png_bench_size_roundtrip(layout):
     """4096^2 tc8 with per-row Sub/Up/Avg/Paeth: the GPU unfilter must return
-    exactly the generator's raw pixels (unfilter(filter(x)) == x)."""
+    exactly the generator's raw pixels (unfilter(filter(x)) == x), from the
+    host-built band slab ("auto") and from the inflated stream ("stream":
+    the plan builds the slab on the device at every launch)."""
     raw, filt = S.png_filtered_tc8(0, 4096, 4096)
     data = S.encode_png(4096, 4096, 8, 2, filt.tobytes())
     st = P.Stream(data)
-    batch = device.PngBatch([st], slots=[0, 0])
+    batch = device.PngBatch([st], slots=[0, 0], layout=layout)
+    assert [f.layout for f in batch.frames] == [int(layout == "auto")] * 2
     for _ in range(2):  # relaunch: scratch must be re-initialised every call
         batch.launch(torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
@@ -155,14 +159,16 @@ def test_rgba_pixels_every_kind(where, name):
     assert np.array_equal(got.rgba_pixels(), want.rgba_pixels())
 
 
-def test_png_adam7_rgba16_4k_matches_oracle():
+@pytest.mark.parametrize("layout", ["auto", "stream"])
+def test_png_adam7_rgba16_4k_matches_oracle(layout):
     """configs[4] PNG at its bench size: 4096^2 Adam7 RGBA16 -> NRGBA64 (7
     passes scattered by mergePassInto), bit-exact against the oracle, twice
-    through one plan (relaunch), plus zpx_plan_status."""
+    through one plan (relaunch), plus zpx_plan_status; host slab and
+    device-built slab."""
     data = S.png_rgba16_adam7(2000, 4096, 4096)
     want = O.png_decode(data).pixels
     st = P.Stream(data)
-    batch = device.PngBatch([st], slots=[0, 0])
+    batch = device.PngBatch([st], slots=[0, 0], layout=layout)
     for _ in range(2):
         batch.launch(torch.cuda.current_stream().cuda_stream)
     batch.status(torch.cuda.current_stream().cuda_stream)
@@ -184,7 +190,8 @@ def test_png_plan_layouts(layout, depth, ct, il):
     streams = [P.Stream(d) for d in datas]
     b = device.PngBatch(streams, layout=layout)
     # (auto: a slab wherever the paired-row kernel takes the image -- not
-    # the smallest Adam7 passes -- and always the 300 x 260 one)
+    # the smallest Adam7 passes -- and always the 300 x 260 one; a stream
+    # frame the paired-row kernel takes gets its slab built on the device)
     slab = [layout == "auto" or (layout == "mixed" and i % 2 == 0) for i in range(4)]
     assert [f.layout for f in b.frames] == [int(s and st.slab() is not None) for s, st in zip(slab, streams)]
     assert b.frames[3].layout == (1 if layout == "auto" else 0)
@@ -193,3 +200,35 @@ def test_png_plan_layouts(layout, depth, ct, il):
     for s, d in enumerate(datas):
         want = O.png_decode(d).pixels.reshape(-1)
         assert np.array_equal(b.output_tensor(s).cpu().numpy().reshape(-1)[:want.size], want)
+
+
+@pytest.mark.parametrize("depth,ct,w,h,il", [
+    (8, 2, 70, 300, 0),     # TC8: 12-byte chunks, a partial last band
+    (8, 6, 33, 130, 0),     # TCA8
+    (16, 6, 21, 40, 1),     # TCA16 Adam7
+    (16, 2, 17, 17, 1),     # TC16 Adam7, tiny passes
+    (8, 0, 100, 129, 0),    # G8
+    (16, 0, 64, 64, 0),     # G16
+    (8, 2, 1500, 300, 0),   # TC8: 375 chunks a row, several 16-group windows per band
+    (8, 6, 700, 260, 1),    # TCA8 Adam7, wide passes
+    (16, 2, 2049, 131, 0),  # TC16, odd width, rows past the band
+])
+def test_png_device_slab_matches_model(depth, ct, w, h, il):
+    """The band slab the plans build on the device from the inflated stream
+    (png_slab_kernels.hip) holds exactly the bytes the paired-row kernel
+    reads (the Python model of tests/test_png_slab.py, which also pins the
+    host builder)."""
+    import ctypes as C
+
+    from test_png_slab import check_slab
+    from zpix_amd import _lib
+
+    d = S.png_generic(3 + w, w, h, depth, ct, interlace=il, filters=(0, 1, 2, 3, 4))
+    st = P.Stream(d)
+    ctx = zpix_amd.context.default()
+    n = C.c_size_t(0)
+    _lib.check(_lib.lib().zpx_debug_png_device_slab(ctx.handle, st.handle, None, 0, C.byref(n)), ctx.handle)
+    out = np.zeros(n.value, np.uint8)
+    _lib.check(_lib.lib().zpx_debug_png_device_slab(ctx.handle, st.handle, out.ctypes.data, n.value, C.byref(n)),
+               ctx.handle)
+    check_slab(st, out)

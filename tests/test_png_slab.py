@@ -44,12 +44,15 @@ def skews(ft, rows):
     return sk, max(s for r, s in enumerate(sk) if r < rows)
 
 
-def check_slab(st):
+def check_slab(st, slab=None):
+    """The slab (the host's, st.slab(), unless given: e.g. the device-built
+    one, tests/test_gpu_png.py) holds exactly the bytes the kernel reads."""
     f = st.frame
     bpp, cb = GEOM[f.depth]
     c, nq = cb // bpp, 8 * cb // 16
     stream = st.filtered()
-    slab = st.slab()
+    if slab is None:
+        slab = st.slab()
     assert slab is not None
     ps = passes(f.width, f.height, bpp, f.interlace)
     nb = sum((p[1] + 127) // 128 for p in ps)

@@ -13,6 +13,7 @@
 
 #include "zpix_amd.h"
 #include "device_types.h"
+#include "kernels.h"
 #include "options.h"
 
 struct zpx_ctx {
@@ -153,9 +154,14 @@ typedef void (*BatchDone)(void *user, int item);
 int batch_decode_rgba_hook(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
                            zpx_batch_stats *stats, BatchDone on_done, void *user);
 
+// shard.cpp: destroy the cached gather communicators that include `device`
+// (zpx_ctx_destroy); a call still gathering on one finishes first
+void shard_release_comms(int device);
+
 // zpx_api.cpp helpers shared with the batch pipeline
 void jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes);
 DevJpegFrame dev_jpeg_frame(const zpx_jpeg_frame &f);
+JpegPlaneGeom jpeg_plane_geom(const DevJpegFrame &d); // the planar kernel geometry of one frame
 bool jpeg_fusable(const zpx_jpeg_frame &f); // the fused RGBA kernel takes this frame
 int launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_frame, hipStream_t st);
 // dword-aligned RGBA rows, any width (the block-per-lane kernel takes it)
@@ -166,6 +172,18 @@ void png_frame_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes, s
 // the region offset of every band (returned size = slab bytes), then the fill.
 size_t png_slab_layout(const zpx_png_frame &f, std::vector<uint64_t> &band_off);
 void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, uint8_t *out, int threads = 1);
+// The same layout built on the device from the stream (png_slab_kernels.hip):
+// region sizes for the largest possible skew (min(127, rows - 1)), so the
+// layout follows from the frame's geometry alone and the host never reads the
+// filtered bytes.  png_dev_slab_layout returns the slab bytes and every band's
+// region offset (the slab's leading table, which the caller copies to the
+// slab's start); png_dev_slab_jobs appends one DevSlabBand per band for the
+// DEVICE stream `d_stream` (`stream_len` readable bytes, pad included) and
+// slab `d_slab`; the largest group count of those bands goes to max_groups.
+size_t png_dev_slab_layout(const zpx_png_frame &f, std::vector<uint64_t> &band_off);
+void png_dev_slab_jobs(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, const uint8_t *d_stream,
+                       size_t stream_len, uint8_t *d_slab, std::vector<DevSlabBand> &jobs, uint32_t &max_groups);
+int png_slab_chunk_bytes(int depth); // CB of the paired-row kernel (12 or 16; 0: not one it takes)
 DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_palette);
 // planes + colour pass for frames the fused kernel does not take (async on st)
 int jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, DevBuf &planes, DevBuf &desc,

@@ -75,6 +75,7 @@ struct Decoded {
 
 struct Slot {
     DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid, dstage; // dstage: Adam7 passes 1-5 (Adam7Stage)
+    DevBuf dslab; // the paired-row kernel's band slab, built on the device (png_slab_kernels.hip)
     HostBuf hdesc, hstatus; // pinned descriptor staging, PNG status word
     hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
     std::unique_ptr<Decoded> dec;
@@ -192,11 +193,8 @@ void Pipeline::worker()
         if (zpx_png_probe_buffer(it.buf, it.len)) {
             d->fmt = 2;
             d->status = png_parse(it.buf, it.len, d->ps, sub);
-            // the paired-row kernel's input layout, on this worker thread
-            // (the kernel reads the stream layout when this is refused)
-            if (d->status == ZPX_OK && png_use_pair(d->ps.depth, d->ps.interlace, d->ps.use_transparent,
-                                                    d->ps.width, size_t(d->ps.width) * d->ps.out_bpp))
-                (void)png_stream_build_slab(d->ps, sub);
+            // (the paired-row kernel's band slab is built on the device from
+            // the uploaded stream: issue_png)
         } else if (zpx_jpeg_probe_buffer(it.buf, it.len)) {
             d->fmt = 1;
             d->status = jpeg_entropy_decode(it.buf, it.len, d->jc, sub, jpeg_sparse_upload());
@@ -422,15 +420,15 @@ int Pipeline::issue_png(Slot &s)
     PngStream &ps = d.ps;
     const uint32_t W = ps.width, H = ps.height;
     const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
-    // the paired-row kernel reads the band slab the worker built; without
-    // one the one-row-per-lane kernel reads the stream
-    const bool slab = ps.slab_len != 0 && png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
-                                                        ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
-    const bool pair = slab;
-    const size_t in_len = slab ? ps.slab_len : ps.data_len + ZPX_PNG_INPUT_PAD;
+    // the inflated stream goes up as is; the paired-row kernel's band slab
+    // is built from it on the device (png_slab_kernels.hip), else the
+    // one-row-per-lane kernel reads the stream
+    const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
+                                   ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
+    const size_t in_len = ps.data_len + ZPX_PNG_INPUT_PAD;
     HIPCHK(ctx_, s.din.reserve(in_len));
-    HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, slab ? ps.slab.ptr : ps.data.ptr, in_len, hipMemcpyHostToDevice, h2d_));
-    h2d_bytes_ += double(slab ? ps.slab_len : ps.data_len);
+    HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, ps.data.ptr, in_len, hipMemcpyHostToDevice, h2d_));
+    h2d_bytes_ += double(ps.data_len);
     HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
     HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
 
@@ -462,10 +460,20 @@ int Pipeline::issue_png(Slot &s)
     f.use_transparent = ps.use_transparent;
     memcpy(f.transparent, ps.transparent, 6);
     f.filtered = s.din.as<uint8_t>();
-    f.layout = slab ? ZPX_PNG_LAYOUT_SLAB : ZPX_PNG_LAYOUT_STREAM;
+    f.layout = ZPX_PNG_LAYOUT_STREAM;
     f.out = img_out;
     f.out_stride = img_stride;
     f.max_index = nullptr; // palette handled below with all 256 entries
+    std::vector<uint64_t> slab_off;
+    std::vector<DevSlabBand> sjobs;
+    uint32_t slab_groups = 0;
+    if (pair) {
+        const size_t slab_b = png_dev_slab_layout(f, slab_off);
+        HIPCHK(ctx_, s.dslab.reserve(slab_b));
+        png_dev_slab_jobs(f, slab_off, s.din.as<uint8_t>(), in_len, s.dslab.as<uint8_t>(), sjobs, slab_groups);
+        f.filtered = s.dslab.as<uint8_t>();
+        f.layout = ZPX_PNG_LAYOUT_SLAB;
+    }
     std::vector<DevPngPass> passes;
     std::vector<uint32_t> rowbytes;
     uint64_t bytes = 0;
@@ -479,12 +487,15 @@ int Pipeline::issue_png(Slot &s)
     const uint32_t granules = bp.granules;
     const uint32_t base = bp.nbands;
     const uint32_t ns = static_cast<uint32_t>(bp.sched.size()), ns2 = static_cast<uint32_t>(bp.sched2.size());
-    // descriptor staging: passes | sched, sched2 | palette (256 zpx_color) | Adam7 merge job
+    // descriptor staging: passes | sched, sched2 | palette (256 zpx_color) | Adam7 merge job |
+    // slab band table | slab jobs
     const size_t pass_b = align_up(passes.size() * sizeof(DevPngPass));
     const size_t sched_b = align_up(std::max<size_t>(1, ns + ns2) * sizeof(DevPngBand));
     const size_t pal_b = align_up(256 * sizeof(zpx_color));
-    const size_t merge_b = a7.jobs.size() * sizeof(DevAdam7Merge);
-    const size_t desc_b = pass_b + sched_b + pal_b + merge_b;
+    const size_t merge_b = align_up(a7.jobs.size() * sizeof(DevAdam7Merge));
+    const size_t table_b = align_up(slab_off.size() * sizeof(uint64_t));
+    const size_t sjobs_b = sjobs.size() * sizeof(DevSlabBand);
+    const size_t desc_b = pass_b + sched_b + pal_b + merge_b + table_b + sjobs_b;
     HIPCHK(ctx_, s.ddesc.reserve(desc_b));
     uint8_t *dd = s.ddesc.as<uint8_t>();
     if (!a7.jobs.empty())
@@ -496,8 +507,20 @@ int Pipeline::issue_png(Slot &s)
     if (ns) memcpy(h + pass_b, bp.sched.data(), ns * sizeof(DevPngBand));
     if (ns2) memcpy(h + pass_b + ns * sizeof(DevPngBand), bp.sched2.data(), ns2 * sizeof(DevPngBand));
     memcpy(h + pass_b + sched_b, ps.palette, 256 * sizeof(zpx_color));
-    if (merge_b) memcpy(h + pass_b + sched_b + pal_b, a7.jobs.data(), merge_b);
+    if (!a7.jobs.empty()) memcpy(h + pass_b + sched_b + pal_b, a7.jobs.data(), a7.jobs.size() * sizeof(DevAdam7Merge));
+    const size_t table_at = pass_b + sched_b + pal_b + merge_b, sjobs_at = table_at + table_b;
+    if (!slab_off.empty()) memcpy(h + table_at, slab_off.data(), slab_off.size() * sizeof(uint64_t));
+    if (sjobs_b) memcpy(h + sjobs_at, sjobs.data(), sjobs_b);
     HIPCHK(ctx_, hipMemcpyAsync(dd, h, desc_b, hipMemcpyHostToDevice, ctx_->stream));
+    if (pair) {
+        // the slab: its band table, then the bands from the stream (once the
+        // stream has landed: the compute stream waits for ev_in above)
+        HIPCHK(ctx_, hipMemcpyAsync(s.dslab.ptr, dd + table_at, slab_off.size() * sizeof(uint64_t),
+                                    hipMemcpyDeviceToDevice, ctx_->stream));
+        if (launch_png_slab(png_slab_chunk_bytes(ps.depth), reinterpret_cast<const DevSlabBand *>(dd + sjobs_at),
+                            static_cast<uint32_t>(sjobs.size()), slab_groups, ctx_->stream))
+            return hip_fail(ctx_, hipGetLastError(), "batch: png slab kernel");
+    }
     const size_t bound_b = std::max<size_t>(1, base) * granules * sizeof(uint64_t);
     if (s.dbound.bytes < bound_b) { // fresh granules carry tag 0, older than any epoch
         HIPCHK(ctx_, s.dbound.alloc(bound_b));
@@ -507,6 +530,11 @@ int Pipeline::issue_png(Slot &s)
               ps.interlace, passes.size(), ns, ns2, granules);
     const DevPngPass *dp = reinterpret_cast<const DevPngPass *>(dd);
     const DevPngBand *dsch = reinterpret_cast<const DevPngBand *>(dd + pass_b);
+    // control words {epoch, ticket, status, sticky}: each launch's ctl kernel
+    // folds the previous launch's status into `sticky`, so an Adam7 item's
+    // first launch reports through sticky -- clear it for this item (the
+    // slot's words are reused) and read both words after the last launch
+    HIPCHK(ctx_, hipMemsetAsync(s.dctl.as<uint32_t>() + 3, 0, 4, ctx_->stream));
     const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, dp, dsch, ns, s.dctl.as<uint32_t>(),
                                            s.dbound.as<uint64_t>(), granules, ctx_->stream)
                          : launch_png_unfilter(ps.depth, dp, dsch, ns, s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(),
@@ -517,7 +545,7 @@ int Pipeline::issue_png(Slot &s)
     if (ns2 && launch_png_pair_merge(ps.depth, ps.use_transparent, dp, dsch + ns, ns2, s.dctl.as<uint32_t>(),
                                      s.dbound.as<uint64_t>(), granules, ctx_->stream))
         return hip_fail(ctx_, hipGetLastError(), "batch: png adam7 merge pass");
-    HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, ctx_->stream));
+    HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost, ctx_->stream));
     s.check_png = true;
     if (rgba_native) {
         if (direct) {
@@ -585,7 +613,8 @@ void Pipeline::retire(Slot &s)
     zpx_batch_item &it = items_[s.dec->item];
     if (s.failed) {
         // it.status holds the image's error
-    } else if (s.check_png && *static_cast<volatile uint32_t *>(s.hstatus.ptr) != 0) {
+    } else if (s.check_png && (static_cast<volatile uint32_t *>(s.hstatus.ptr)[0] |
+                               static_cast<volatile uint32_t *>(s.hstatus.ptr)[1]) != 0) {
         ctx_->last_error = "png wavefront hand-off timed out";
         it.status = ZPX_E_HIP;
     } else {

@@ -17,8 +17,18 @@ struct DevJpegFrame {
     int32_t rule[4];
     int32_t n_comp, color;
     int32_t qt[4][64];       // natural order
-    uint32_t qp[3][32];      // components 0-2: quant-pair tables of the block kernel's row pass
+    uint32_t qp[4][32];      // quant-pair tables of the block kernels' row pass, per component
                              // (per row r: (q1,q7), (q5,q3), (q2,q6), (q0,q4) as u16 pairs)
+};
+
+// The planar block kernel's task space for one plan group (frames of one
+// geometry): per component c, rows[c] block rows of segs[c] 64-block
+// segments, tasks start[c] .. start[c+1) of every frame (start[c] =
+// per_frame for absent components).
+struct PlaneTaskGeom {
+    int32_t segs[4], rows[4], start[4];
+    int32_t hh[4], vv[4];    // 8 * h0 / h_c, 8 * v0 / v_c: the progressive block rule (decoder.zig:1649-1651)
+    int32_t per_frame, total;
 };
 
 // One PNG unfilter job: a (pass of a) PNG image.  Rows are processed by the
@@ -59,6 +69,18 @@ struct DevAdam7Merge {
     uint64_t q2stride, s4stride, s5stride; // bytes between rows
     uint32_t width;           // image width in pixels
     uint32_t pad;
+};
+
+// One band of the device-built band slab (png_slab_kernels.hip): the
+// paired-row kernel's input layout (png_slab.cpp) made on the device from
+// the inflated stream.
+struct DevSlabBand {
+    const uint8_t *rows0; // the band's first row (its filter byte) in the stream
+    uint8_t *region;      // the band's slab region: 128 filter bytes, then the groups
+    uint32_t avail;       // stream bytes readable from rows0 (to the stream's end + pad)
+    uint32_t rows;        // rows of the band in its pass (<= 128)
+    uint32_t rb;          // filtered bytes per row, without the filter byte
+    uint32_t nchunks;     // chunks per row
 };
 
 // A scheduled band: which pass and which band in it.  Bands are ordered so

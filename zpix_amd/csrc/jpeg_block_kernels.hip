@@ -731,6 +731,141 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     }
 }
 
+// ---------------------------------------------------------------------------
+// Planar reconstruct, one 8x8 block per lane (jpeg_plane_block_kernel):
+// jpeg.load's output, reconstructBlock into makeImg's planes
+// (src/jpeg/decoder.zig:1553-1634, :361-370; idct.zig:77-201).
+//
+// A task is 64 consecutive blocks of one block row of one component; a wave
+// runs tasks persistently.  Per task: the lane's block comes from the wave's
+// LDS coefficient image (the fused kernel's CoefImage layout, written by the
+// LDS-DMA one task ahead), the next task's DMA is issued, then dequant + the
+// dot2 row pass + the column pass with clamp run in registers, and the
+// block's 8 rows leave as 8-byte stores: lane j writes bytes 8j..8j+7 of the
+// pixel row, so each store instruction writes 512 contiguous bytes of one
+// plane row (4 whole lines), non-temporal.  Lanes whose block is outside the
+// grid or outside the component's block rule (decoder.zig:1334, :1649-1651)
+// store nothing, exactly as the reference leaves those samples at makeImg's
+// zero.  As in the fused kernel every load and store is unconditional
+// (dropped through the buffer range check), so the vmcnt count is static:
+// at a task's start the only operations issued after its DMA are the
+// previous task's 8 stores.
+// ---------------------------------------------------------------------------
+constexpr int kPlaneWavesPerEu = 4; // <= 128 VGPRs: 16 waves per CU
+
+template <typename CoefT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kPlaneWavesPerEu)))
+void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskGeom geo)
+{
+    using I = CoefImage<CoefT>;
+    constexpr int BYTES = 64 * static_cast<int>(sizeof(CoefT)); // one block's coefficients
+    __shared__ __attribute__((aligned(16))) uint8_t cimg[64 * BYTES];
+    const int lane = threadIdx.x;
+    typedef const __attribute__((address_space(4))) DevJpegFrame *CFrame;
+    auto u32 = [](uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(x)); };
+    auto uptr = [&](const void *p) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        return static_cast<uint64_t>(u32(static_cast<uint32_t>(a >> 32))) << 32 | u32(static_cast<uint32_t>(a));
+    };
+    // a task's uniform view (scalar loads of the descriptor through the
+    // constant address space, as in jpeg_block_kernel)
+    struct PTask {
+        uint64_t grid, plane, qp;
+        uint32_t stride;
+        int gw, by, bx0, rule, hh, vv, width, height;
+        bool ok;
+    };
+    auto task_of = [&](int t) __attribute__((always_inline)) {
+        PTask k;
+        const int f = t / geo.per_frame;
+        const int r = t - f * geo.per_frame;
+        const int c = (r >= geo.start[1]) + (r >= geo.start[2]) + (r >= geo.start[3]);
+        const int rr = r - geo.start[c];
+        k.by = rr / geo.segs[c];
+        k.bx0 = (rr - k.by * geo.segs[c]) * 64;
+        const auto &fr = *(reinterpret_cast<CFrame>(reinterpret_cast<uintptr_t>(frames)) + f);
+        k.grid = uptr(fr.coeffs[c]);
+        k.plane = uptr(fr.planes[c]);
+        k.qp = uptr(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(&fr.qp[c][0])));
+        k.stride = u32(static_cast<uint32_t>(fr.strides[c]));
+        k.gw = static_cast<int>(u32(static_cast<uint32_t>(fr.mxx * fr.h[c])));
+        const int gh = static_cast<int>(u32(static_cast<uint32_t>(fr.myy * fr.v[c])));
+        k.rule = static_cast<int>(u32(static_cast<uint32_t>(fr.rule[c])));
+        k.width = static_cast<int>(u32(static_cast<uint32_t>(fr.width)));
+        k.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
+        k.hh = geo.hh[c];
+        k.vv = geo.vv[c];
+        // (a ragged batch's task past a smaller frame's grid, or a component
+        // never scanned / without a plane, writes nothing)
+        k.ok = k.by < gh && k.bx0 < k.gw && k.grid != 0 && k.plane != 0 && k.rule != ZPX_BLOCKS_NONE;
+        return k;
+    };
+    // the task's 64 blocks -> cimg (see CoefImage): DMA instruction k carries
+    // blocks B*k .. B*k+B-1 of the row; past the grid's right edge clamped
+    // onto its last block, a task without blocks reads the descriptor array
+    auto issue = [&](const PTask &k) __attribute__((always_inline)) {
+        const uint8_t *row = k.ok ? reinterpret_cast<const uint8_t *>(k.grid) + static_cast<size_t>(k.by) * k.gw * BYTES
+                                  : reinterpret_cast<const uint8_t *>(frames);
+        const int last = k.ok ? k.gw - 1 : 0;
+#pragma unroll
+        for (int i = 0; i < I::P; i++) {
+            const int bx = min(k.bx0 + I::B * i + lane % I::B, last);
+            const int q = (lane / I::B + I::P - (I::P == 8 ? i : 0)) % I::P;
+            glds16<true>(row + static_cast<uint32_t>(bx * BYTES + 16 * q), cimg + 1024 * i);
+        }
+    };
+    int task;
+    {
+        const int nw = static_cast<int>(gridDim.x), w = static_cast<int>(blockIdx.x);
+        const int q = nw / 8, r = nw % 8, x = w % 8;
+        task = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8; // XCD-consecutive tasks
+    }
+    if (task >= geo.total) return;
+    const int tstride = static_cast<int>(gridDim.x);
+    PTask k = task_of(task);
+    issue(k);
+    // the loop head expects the previous task's 8 stores behind the DMA
+    const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, none, 8 * i, 0, kStoreAux);
+    constexpr uint32_t kDrop = 0x80000000u;
+    for (;;) {
+        const int tn = task + tstride;
+        const bool more = tn < geo.total;
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        u32x4 raw[I::P];
+        load_raw<CoefT>(cimg, lane, raw);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PTask kn = k;
+        if (more) {
+            kn = task_of(tn);
+            issue(kn);
+        }
+        int32_t s[64];
+        typedef const __attribute__((address_space(4))) u32x4 *cq;
+        idct_block_pairs<CoefT>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
+            const u32x4 a = *reinterpret_cast<cq>(k.qp + 16 * r);
+            return u32x4{pk_mul16(c[0], a[0]), pk_mul16(c[1], a[1]), pk_mul16(c[2], a[2]), pk_mul16(c[3], a[3])};
+        }, s);
+        const int bx = k.bx0 + lane;
+        bool live = k.ok && bx < k.gw;
+        if (k.rule == ZPX_BLOCKS_PROGRESSIVE) live = live && bx * k.hh < k.width && k.by * k.vv < k.height;
+        else if (k.rule == ZPX_BLOCKS_SCAN) live = live && bx * 8 < k.width && k.by * 8 < k.height;
+        const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void *>(k.plane + static_cast<uint64_t>(k.by) * 8 * k.stride), 0,
+            static_cast<int>(u32(k.ok ? 8 * k.stride : 0)), 0x00020000);
+        const uint32_t o0 = live ? static_cast<uint32_t>(bx) * 8 : kDrop;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const u32x2 v{pack4(s + 8 * r) ^ kBias4, pack4(s + 8 * r + 4) ^ kBias4};
+            __builtin_amdgcn_raw_buffer_store_b64(v, prsrc, live ? o0 + r * k.stride : kDrop, 0, kStoreAux);
+        }
+        if (!more) break;
+        task = tn;
+        k = kn;
+    }
+}
+
 } // namespace
 
 namespace {
@@ -785,6 +920,39 @@ int block_color(int color, int key, const DevJpegFrame *d, int n, int mxx, int m
     return -2;
 }
 } // namespace
+
+int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &g, int coeff_bits,
+                            bool narrow, hipStream_t stream)
+{
+    if (!narrow || (coeff_bits != 8 && coeff_bits != 16)) return -2;
+    if (g.ncomp < 1 || g.ncomp > 4) return -2;
+    PlaneTaskGeom geo{};
+    int64_t per = 0;
+    for (int c = 0; c < 4; c++) {
+        geo.start[c] = static_cast<int32_t>(per);
+        if (c >= g.ncomp) continue;
+        if (g.h[c] <= 0 || g.v[c] <= 0) return -2;
+        const int gw = g.max_mxx * g.h[c];
+        geo.segs[c] = (gw + 63) / 64;
+        geo.rows[c] = g.max_myy * g.v[c];
+        geo.hh[c] = 8 * (g.h[0] / g.h[c]);
+        geo.vv[c] = 8 * (g.v[0] / g.v[c]);
+        per += int64_t(geo.segs[c]) * geo.rows[c];
+    }
+    for (int c = g.ncomp; c < 4; c++) geo.start[c] = static_cast<int32_t>(per);
+    const int64_t total = per * n_frames;
+    if (total <= 0) return 0;
+    if (total >= (int64_t(1) << 31)) return -2;
+    geo.per_frame = static_cast<int32_t>(per);
+    geo.total = static_cast<int32_t>(total);
+    auto kernel = coeff_bits == 8 ? jpeg_plane_block_kernel<int8_t> : jpeg_plane_block_kernel<int16_t>;
+    static const int resident8 = resident_waves(jpeg_plane_block_kernel<int8_t>);
+    static const int resident16 = resident_waves(jpeg_plane_block_kernel<int16_t>);
+    const int resident = coeff_bits == 8 ? resident8 : resident16;
+    const int grid = total < resident ? static_cast<int>(total) : resident;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, geo);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
                       int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream)

@@ -504,9 +504,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5))) v
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh,
-                       int coeff_bits, bool narrow, hipStream_t stream)
+int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &geom, int coeff_bits,
+                       bool narrow, hipStream_t stream)
 {
+    // the block-per-lane kernel (jpeg_block_kernels.hip) takes the narrow
+    // int8 / int16 frames; the test switch "jpeg_strip" forces this one
+    if (opt(Opt::JpegStrip) == 0) {
+        const int rc = launch_jpeg_plane_block(d_frames, n_frames, geom, coeff_bits, narrow, stream);
+        if (rc != -2) return rc;
+    }
+    int max_gw = 0, max_gh = 0;
+    for (int c = 0; c < geom.ncomp; c++) {
+        max_gw = max(max_gw, geom.max_mxx * geom.h[c]);
+        max_gh = max(max_gh, geom.max_myy * geom.v[c]);
+    }
+    if (max_gw <= 0 || max_gh <= 0 || n_frames <= 0) return 0;
     dim3 grid((max_gw + 31) / 32, max_gh, n_frames * 4);
     if (coeff_bits == 8) {
         if (narrow) hipLaunchKernelGGL((jpeg_planar_kernel<int8_t, true>), grid, dim3(kThreads), 0, stream, d_frames);

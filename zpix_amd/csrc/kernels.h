@@ -12,7 +12,14 @@ namespace zpx {
 
 // jpeg_kernels.hip
 // coeff_bits: 8, 16 or 32 (int8 / int16 / int32 coefficient grids)
-int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, int max_gw, int max_gh, int coeff_bits,
+// The planar output (jpeg.load) of frames of one geometry: ncomp components
+// sampled h[c] x v[c] (gray: 1 x 1), MCU grids up to max_mxx x max_myy.
+struct JpegPlaneGeom {
+    int ncomp = 0;
+    int h[4] = {1, 1, 1, 1}, v[4] = {1, 1, 1, 1};
+    int max_mxx = 0, max_myy = 0;
+};
+int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &geom, int coeff_bits,
                        bool narrow, hipStream_t stream);
 bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc);
 // vec_out: every frame's RGBA rows are dword aligned (jpeg_rgba_vec_out:
@@ -23,6 +30,9 @@ int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int 
 // jpeg_block_kernels.hip: -2 when the frame kind is not one it takes
 int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
                       int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream);
+// the planar block kernel (narrow int8 / int16 frames); -2 for the rest
+int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &geom, int coeff_bits,
+                            bool narrow, hipStream_t stream);
 
 // png_kernels.hip
 // CUs of the current device (read once: the node's GPUs are alike; a
@@ -51,6 +61,11 @@ int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPng
 // the staged passes 1-5 into whole even rows (the 4- and 8-byte-pixel depths)
 int launch_png_pair_merge(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
                           uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s);
+
+// png_slab_kernels.hip: the band slab of `njobs` bands built on the device
+// (cb: the depth's chunk bytes, 12 or 16; max_groups: the most groups any of
+// the bands can have)
+int launch_png_slab(int cb, const DevSlabBand *jobs, uint32_t njobs, uint32_t max_groups, hipStream_t s);
 
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);
 int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s);

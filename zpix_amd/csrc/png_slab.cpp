@@ -200,10 +200,82 @@ void png_slab_fill(const zpx_png_frame &f, const std::vector<uint64_t> &band_off
     for (auto &t : pool) t.join();
 }
 
+int png_slab_chunk_bytes(int depth)
+{
+    const SlabGeom sg = slab_geom(depth);
+    return sg.bpp ? sg.cb : 0;
+}
+
+namespace {
+// the passes of f in stream layout (their `filtered` = offsets from f.filtered)
+void stream_passes(const zpx_png_frame &f, std::vector<DevPngPass> &passes)
+{
+    std::vector<uint32_t> rowbytes;
+    uint64_t bytes = 0;
+    zpx_png_frame hf = f;
+    hf.layout = ZPX_PNG_LAYOUT_STREAM;
+    png_frame_passes(hf, passes, rowbytes, bytes);
+}
+// groups of a band of `rows` rows with chunks per row `nchunks`, for its
+// largest possible skew
+uint32_t worst_groups(uint32_t nchunks, uint32_t rows)
+{
+    return (nchunks + std::min(127u, rows ? rows - 1 : 0u) + 7) / 8;
+}
+} // namespace
+
+size_t png_dev_slab_layout(const zpx_png_frame &f, std::vector<uint64_t> &band_off)
+{
+    band_off.clear();
+    const SlabGeom sg = slab_geom(f.depth);
+    if (!sg.bpp) return 0;
+    std::vector<DevPngPass> passes;
+    stream_passes(f, passes);
+    const int c = sg.cb / sg.bpp, nq = 8 * sg.cb / 16;
+    size_t nb = 0;
+    for (const DevPngPass &p : passes) nb += (p.rows + 127) / 128;
+    size_t off = align_up(nb * sizeof(uint64_t));
+    for (const DevPngPass &p : passes) {
+        const uint32_t nchunks = (p.width + c - 1) / c;
+        for (uint32_t base = 0; base < p.rows; base += 128) {
+            band_off.push_back(off);
+            off = align_up(off + 128 + size_t(worst_groups(nchunks, std::min(128u, p.rows - base))) * 2 * nq * 1024);
+        }
+    }
+    return off;
+}
+
+void png_dev_slab_jobs(const zpx_png_frame &f, const std::vector<uint64_t> &band_off, const uint8_t *d_stream,
+                       size_t stream_len, uint8_t *d_slab, std::vector<DevSlabBand> &jobs, uint32_t &max_groups)
+{
+    const SlabGeom sg = slab_geom(f.depth);
+    std::vector<DevPngPass> passes;
+    stream_passes(f, passes);
+    const int c = sg.cb / sg.bpp;
+    size_t b = 0, at = 0; // band index, stream offset of the pass
+    for (const DevPngPass &p : passes) {
+        const uint32_t nchunks = (p.width + c - 1) / c;
+        for (uint32_t base = 0; base < p.rows; base += 128, b++) {
+            DevSlabBand j{};
+            const size_t first = at + size_t(base) * (size_t(p.row_bytes) + 1);
+            j.rows0 = d_stream + first;
+            j.region = d_slab + band_off[b];
+            const size_t avail = stream_len > first ? stream_len - first : 0;
+            j.avail = static_cast<uint32_t>(std::min<size_t>(avail, 0x7fffff00u));
+            j.rows = std::min(128u, p.rows - base);
+            j.rb = p.row_bytes;
+            j.nchunks = nchunks;
+            max_groups = std::max(max_groups, worst_groups(nchunks, j.rows));
+            jobs.push_back(j);
+        }
+        at += size_t(p.rows) * (size_t(p.row_bytes) + 1);
+    }
+}
+
 int png_stream_build_slab(PngStream &ps, int threads)
 {
     if (ps.slab_len) return ZPX_OK;
-    if (!png_pair_supported(ps.depth, ps.interlace, ps.use_transparent, ps.width, size_t(ps.width) * ps.out_bpp))
+    if (!png_use_pair(ps.depth, ps.interlace, ps.use_transparent, ps.width, size_t(ps.width) * ps.out_bpp))
         return ZPX_E_UNSUPPORTED;
     zpx_png_frame f;
     memset(&f, 0, sizeof(f));

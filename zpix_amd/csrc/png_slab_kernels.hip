@@ -1,0 +1,140 @@
+// gfx950 band-slab build: the paired-row PNG kernel's input layout
+// (png_slab.cpp has the layout and the host builder) made on the device from
+// the inflated stream that parseIdat hands readImagePass
+// (src/png/decoder.zig:516-523).  So the host hands over the stream as
+// inflate produced it and keeps no transposition work.
+//
+// A workgroup takes 16 rows of one band and 16 groups (128 chunks) of them:
+//   1. the band's 128 filter bytes -> the skew of every row (the kernel's
+//      rule: row r minus the last row <= r that restarts the chain: a None /
+//      Sub row, a row past the pass, or the band's first) and the band's
+//      largest, hence its group count;
+//   2. each row's window of the 16 groups, from its first chunk 8 g0 - skew
+//      on, read as whole dwords with consecutive lanes on consecutive dwords
+//      of one row (whole lines per instruction) into an LDS tile;
+//   3. the 16-byte pieces in the slab's order (piece q of row 2 lane + h's
+//      group window at 128 + ((2 g + h) NQ + q) KiB + 16 lane of the region),
+//      eight lanes on eight consecutive pieces, so every store instruction
+//      writes whole 128-byte lines; bytes outside the row are zeros.
+// Streaming and HBM-bound: each stream byte is read once (plus the partial
+// lines at a window's ends) and each slab byte written once.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_types.h"
+#include "kernels.h"
+
+namespace zpx {
+namespace {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+constexpr int kRows = 16;   // rows per workgroup
+constexpr int kGroups = 16; // groups (8 chunks each) per workgroup
+constexpr int kOOR = 0x7ffffff0;
+
+template <int CB>
+__global__ __launch_bounds__(256) void png_slab_kernel(const DevSlabBand *__restrict__ jobs)
+{
+    constexpr int NQ = CB / 2;                  // 16-byte pieces per row and group (8 CB / 16)
+    constexpr int WIN = kGroups * 8 * CB;       // window bytes per row
+    constexpr int NDW = WIN / 4 + 1;            // dwords loaded per row (+1: the window's misalignment)
+    __shared__ uint32_t tile[kRows * NDW];
+    __shared__ uint8_t ft[128];
+    __shared__ int32_t skew[128];
+    __shared__ int32_t max_skew;
+    const int tid = threadIdx.x;
+    const int band = static_cast<int>(blockIdx.x) >> 3, R0 = (static_cast<int>(blockIdx.x) & 7) * kRows;
+    const int range = static_cast<int>(blockIdx.y);
+    typedef const __attribute__((address_space(4))) DevSlabBand *CJob;
+    const auto &j = *(reinterpret_cast<CJob>(reinterpret_cast<uintptr_t>(jobs)) + band);
+    const uint32_t rows = j.rows, rb = j.rb, rstride = rb + 1;
+    const uintptr_t r0a = reinterpret_cast<uintptr_t>(j.rows0);
+    const uint32_t delta = static_cast<uint32_t>(r0a & 3u);
+    const auto src = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(r0a - delta), 0,
+                                                       static_cast<int>(j.avail + delta), 0x00020000);
+    // 1. filter bytes and skews (png_slab.cpp band_skews; png_pair_kernel)
+    if (tid < 128) {
+        const uint32_t o = static_cast<uint32_t>(tid) < rows ? static_cast<uint32_t>(tid) * rstride + delta : kOOR;
+        ft[tid] = static_cast<uint8_t>(__builtin_amdgcn_raw_buffer_load_b8(src, o, 0, 0));
+    }
+    if (tid == 0) max_skew = 0;
+    __syncthreads();
+    if (tid < 128) {
+        int l = tid;
+        while (l > 0 && static_cast<uint32_t>(l) < rows && ft[l] >= 2) l--;
+        skew[tid] = tid - l;
+        if (static_cast<uint32_t>(tid) < rows) atomicMax(&max_skew, tid - l);
+    }
+    __syncthreads();
+    const int ngroups = (static_cast<int>(j.nchunks) + max_skew + 7) / 8;
+    const int g0 = range * kGroups;
+    if (g0 >= ngroups) return; // (uniform: past the band's groups)
+    if (range == 0 && R0 == 0 && tid < 32)
+        reinterpret_cast<uint32_t *>(j.region)[tid] = reinterpret_cast<const uint32_t *>(ft)[tid];
+    // 2. the rows' windows into LDS: consecutive threads on consecutive
+    // dwords of one row
+    for (int idx = tid; idx < kRows * NDW; idx += 256) {
+        const int rl = idx / NDW, d = idx - rl * NDW;
+        const int r = R0 + rl;
+        const int x0 = (8 * g0 - skew[r]) * CB; // the window's first byte in the row (>= -skew * CB)
+        // (>= 1: a row holds at least CB - 1 bytes, png_pair_supported, so
+        // r (rb + 1) + 1 >= skew * CB)
+        const uint32_t a = static_cast<uint32_t>(r) * rstride + 1u + static_cast<uint32_t>(x0) + delta;
+        const int o = static_cast<uint32_t>(r) < rows ? static_cast<int>((a & ~3u) + 4u * static_cast<uint32_t>(d)) : kOOR;
+        tile[idx] = __builtin_amdgcn_raw_buffer_load_b32(src, o, 0, 0);
+    }
+    __syncthreads();
+    // 3. the pieces, eight lanes per 128-byte line of the slab
+    constexpr int NPIECE = kGroups * 2 * NQ * 8;
+    uint8_t *const groups = j.region + 128;
+#pragma unroll 2
+    for (int idx = tid; idx < NPIECE; idx += 256) {
+        const int l = idx & 7, rest = idx >> 3;
+        const int q = rest % NQ, gh = rest / NQ, h = gh & 1, gl = gh >> 1;
+        const int g = g0 + gl;
+        if (g >= ngroups) continue;
+        const int rl = 2 * l + h, r = R0 + rl;
+        v4u v = v4u{0, 0, 0, 0};
+        if (static_cast<uint32_t>(r) < rows) {
+            const int sk = skew[r];
+            const uint32_t a = static_cast<uint32_t>(r) * rstride + 1u + static_cast<uint32_t>((8 * g0 - sk) * CB) + delta;
+            const uint32_t local = (a & 3u) + static_cast<uint32_t>(8 * gl * CB + 16 * q);
+            const uint32_t *t = tile + rl * NDW + (local >> 2);
+            const uint32_t sh = local & 3u;
+            const uint32_t w0 = t[0], w1 = t[1], w2 = t[2], w3 = t[3], w4 = t[4];
+            v = v4u{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+            const int p = (8 * g - sk) * CB + 16 * q; // the piece's first byte in the row
+            if (p < 0 || p + 16 > static_cast<int>(rb)) { // a row edge: zeros outside [0, rb)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const int x = p + 4 * e + b;
+                        m |= (x >= 0 && x < static_cast<int>(rb)) ? 0xffu << (8 * b) : 0u;
+                    }
+                    v[e] &= m;
+                }
+            }
+        }
+        const int lane = (R0 >> 1) + l;
+        *reinterpret_cast<v4u *>(groups + (static_cast<size_t>(2 * g + h) * NQ + q) * 1024 + lane * 16) = v;
+    }
+}
+
+} // namespace
+
+int launch_png_slab(int cb, const DevSlabBand *jobs, uint32_t njobs, uint32_t max_groups, hipStream_t s)
+{
+    if (njobs == 0) return 0;
+    const dim3 grid(njobs * 8, (max_groups + kGroups - 1) / kGroups);
+    if (cb == 12) hipLaunchKernelGGL(png_slab_kernel<12>, grid, dim3(256), 0, s, jobs);
+    else if (cb == 16) hipLaunchKernelGGL(png_slab_kernel<16>, grid, dim3(256), 0, s, jobs);
+    else return -2;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace zpx

@@ -217,24 +217,37 @@ const CommTable &table()
 std::atomic<int> g_use_fake{0};
 
 // Communicators per (table, device list), created at the first call that
-// needs them and kept for the process (ncclCommInitAll costs far more than
-// a gather; it used to run inside every call's gather window).
+// needs them and kept (ncclCommInitAll costs far more than a gather; it used
+// to run inside every call's gather window).  A call checks its set out for
+// its whole gather (`use`): RCCL forbids driving one communicator from two
+// threads at once, so two concurrent sharded calls on the same device set
+// take turns.  zpx_ctx_destroy releases the sets holding its device
+// (shard_release_comms).
+struct CommSet {
+    const CommTable *table = nullptr;
+    std::vector<int> devs;
+    std::vector<NcclComm> comms;
+    std::mutex use;
+};
 std::mutex g_comm_mu;
-std::map<std::pair<const CommTable *, std::vector<int>>, std::vector<NcclComm>> g_comms;
+std::map<std::pair<const CommTable *, std::vector<int>>, std::shared_ptr<CommSet>> g_comms;
 
-NcclResult get_comms(const CommTable &T, const std::vector<int> &devs, std::vector<NcclComm> &out)
+NcclResult get_comms(const CommTable &T, const std::vector<int> &devs, std::shared_ptr<CommSet> &out)
 {
     std::lock_guard<std::mutex> lk(g_comm_mu);
     auto key = std::make_pair(&T, devs);
     auto it = g_comms.find(key);
     if (it == g_comms.end()) {
-        std::vector<NcclComm> c(devs.size(), nullptr);
+        auto cs = std::make_shared<CommSet>();
+        cs->table = &T;
+        cs->devs = devs;
+        cs->comms.assign(devs.size(), nullptr);
         int dev = 0;
         (void)hipGetDevice(&dev);
-        const NcclResult e = T.comm_init_all(c.data(), static_cast<int>(devs.size()), devs.data());
+        const NcclResult e = T.comm_init_all(cs->comms.data(), static_cast<int>(devs.size()), devs.data());
         (void)hipSetDevice(dev);
         if (e) return e;
-        it = g_comms.emplace(key, std::move(c)).first;
+        it = g_comms.emplace(key, std::move(cs)).first;
     }
     out = it->second;
     return kNcclSuccess;
@@ -323,17 +336,24 @@ int sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n, const 
         rank_of[r] = k;
     }
     const double tc = now_s();
-    std::vector<NcclComm> comms;
+    std::shared_ptr<CommSet> cset;
+    std::unique_lock<std::mutex> in_use; // this call's turn on the communicator set
     if (devs.size() > 1 && n > 1) { // (some item lives on a rank other than 0)
         if (!T.ok) {
             root->last_error = "RCCL (librccl.so.1) could not be loaded for the gather";
             return ZPX_E_UNSUPPORTED;
         }
-        if (NcclResult e = get_comms(T, devs, comms)) {
-            root->last_error = comm_error(T, e, "ncclCommInitAll");
-            return ZPX_E_HIP;
+        for (;;) {
+            if (NcclResult e = get_comms(T, devs, cset)) {
+                root->last_error = comm_error(T, e, "ncclCommInitAll");
+                return ZPX_E_HIP;
+            }
+            in_use = std::unique_lock<std::mutex>(cset->use);
+            if (!cset->comms.empty()) break;
+            in_use.unlock(); // released (shard_release_comms) between the lookup and the lock: again
         }
     }
+    const std::vector<NcclComm> comms = cset ? cset->comms : std::vector<NcclComm>();
     const double comm_setup_s = now_s() - tc;
 
     const double t0 = now_s();
@@ -511,6 +531,32 @@ int sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n, const 
 }
 
 } // namespace
+
+void zpx::shard_release_comms(int device)
+{
+    std::vector<std::shared_ptr<CommSet>> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        for (auto it = g_comms.begin(); it != g_comms.end();) {
+            const auto &d = it->second->devs;
+            if (std::find(d.begin(), d.end(), device) != d.end()) {
+                drop.push_back(it->second);
+                it = g_comms.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &cs : drop) {
+        std::lock_guard<std::mutex> lk(cs->use); // a call still gathering on it finishes first
+        for (NcclComm c : cs->comms)
+            if (c) (void)cs->table->comm_destroy(c);
+        cs->comms.clear();
+    }
+    (void)hipSetDevice(cur);
+}
 
 extern "C" int zpx_batch_decode_sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n_items,
                                         const zpx_batch_opts *opts, zpx_batch_stats *stats,

@@ -66,6 +66,7 @@ extern "C" int zpx_ctx_create(int device, zpx_ctx **out)
 extern "C" void zpx_ctx_destroy(zpx_ctx *ctx)
 {
     if (!ctx) return;
+    shard_release_comms(ctx->device);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->scratch_ev) {
@@ -182,7 +183,7 @@ DevJpegFrame zpx::dev_jpeg_frame(const zpx_jpeg_frame &f)
     }
     // quant-pair tables (jpeg_block_kernels.hip, idct_block_pairs); tables are at most 16-bit
     static const int kLo[4] = {1, 5, 2, 0}, kHi[4] = {7, 3, 6, 4};
-    for (int c = 0; c < 3; c++)
+    for (int c = 0; c < 4; c++)
         for (int i = 0; i < 32; i++) {
             const int r = i >> 2, k = i & 3;
             d.qp[c][i] = (static_cast<uint32_t>(f.qt[c][8 * r + kLo[k]]) & 0xffffu) |
@@ -198,6 +199,19 @@ DevJpegFrame zpx::dev_jpeg_frame(const zpx_jpeg_frame &f)
     d.n_comp = f.n_comp;
     d.color = f.color;
     return d;
+}
+
+JpegPlaneGeom zpx::jpeg_plane_geom(const DevJpegFrame &d)
+{
+    JpegPlaneGeom g;
+    g.ncomp = d.n_comp;
+    for (int c = 0; c < 4; c++) {
+        g.h[c] = c < d.n_comp ? d.h[c] : 1;
+        g.v[c] = c < d.n_comp ? d.v[c] : 1;
+    }
+    g.max_mxx = d.mxx;
+    g.max_myy = d.myy;
+    return g;
 }
 
 bool zpx::jpeg_fusable(const zpx_jpeg_frame &f)
@@ -264,12 +278,7 @@ int zpx::jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f
     memcpy(hdesc.ptr, &df, sizeof(df));
     HIPCHK(ctx, desc.reserve(sizeof(df)));
     HIPCHK(ctx, hipMemcpyAsync(desc.ptr, hdesc.ptr, sizeof(df), hipMemcpyHostToDevice, st));
-    int gw = 0, gh = 0;
-    for (int i = 0; i < f.n_comp; i++) {
-        gw = std::max(gw, f.mxx * df.h[i]);
-        gh = std::max(gh, f.myy * df.v[i]);
-    }
-    if (launch_jpeg_planar(desc.as<DevJpegFrame>(), 1, gw, gh, f.coeff_bits, f.narrow != 0, st))
+    if (launch_jpeg_planar(desc.as<DevJpegFrame>(), 1, jpeg_plane_geom(df), f.coeff_bits, f.narrow != 0, st))
         return hip_fail(ctx, hipGetLastError(), "jpeg planar kernel");
     zpx_image planar{};
     planar.kind = c.n_comp == 1 ? ZPX_GRAY : ZPX_YCBCR;
@@ -314,6 +323,7 @@ struct JpegGroup {
     int color = 0, h0 = 1, v0 = 1, hc = 1, vc = 1;
     int max_gw = 0, max_gh = 0, max_mxx = 0, max_myy = 0;
     bool vec_out = true; // every frame: dword-aligned RGBA rows (jpeg_rgba_vec_out)
+    JpegPlaneGeom geom;  // planes output: the group's geometry (one per group)
 };
 struct PngGroup {
     int depth = 0;
@@ -322,6 +332,10 @@ struct PngGroup {
     DevBuf passes, sched, scratch, boundary;
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
     DevBuf staging, merge_jobs; // Adam7 passes 1-5 and pass 6's merge jobs (Adam7Stage)
+    // stream-layout frames of the paired-row kernel: their band slabs, built
+    // on the device before the kernel (png_slab_kernels.hip)
+    DevBuf dslab, slab_jobs;
+    uint32_t nslab_jobs = 0, slab_max_groups = 0;
     uint32_t nsched2 = 0;       // bands of the second launch (Adam7 pass 6), after the first nsched
     size_t scratch_zero_bytes = 0;
 };
@@ -367,7 +381,18 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
                 return ZPX_E_INVALID_ARGUMENT;
             groups[{f.coeff_bits, f.narrow, color, h0, v0, hc, vc}].push_back(i);
         } else {
-            groups[{f.coeff_bits, f.narrow, 0, 0, 0, 0, 0}].push_back(i);
+            // one group per geometry (the planar kernel's task space); the
+            // stores address 8 plane rows through a 31-bit buffer range
+            for (int c = 0; c < f.n_comp; c++)
+                if (f.strides[c] > (size_t(1) << 31) / 8 - 1) return ZPX_E_INVALID_ARGUMENT;
+            const DevJpegFrame d = dev_jpeg_frame(f);
+            int hp = 0, vp = 0;
+            for (int c = 0; c < f.n_comp; c++) {
+                if (d.h[c] < 1 || d.h[c] > 15 || d.v[c] < 1 || d.v[c] > 15) return ZPX_E_INVALID_ARGUMENT;
+                hp |= d.h[c] << (4 * c);
+                vp |= d.v[c] << (4 * c);
+            }
+            groups[{f.coeff_bits, f.narrow, f.n_comp, hp, vp, 0, 0}].push_back(i);
         }
     }
     uint64_t bytes = 0;
@@ -398,7 +423,10 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
             g->vec_out = g->vec_out && jpeg_rgba_vec_out(f);
             g->max_mxx = std::max(g->max_mxx, f.mxx);
             g->max_myy = std::max(g->max_myy, f.myy);
+            g->geom = jpeg_plane_geom(d);
         }
+        g->geom.max_mxx = g->max_mxx;
+        g->geom.max_myy = g->max_myy;
         g->n = static_cast<int>(df.size());
         HIPCHK(ctx, g->frames.alloc(df.size() * sizeof(DevJpegFrame)));
         HIPCHK(ctx, hipMemcpy(g->frames.ptr, df.data(), df.size() * sizeof(DevJpegFrame), hipMemcpyHostToDevice));
@@ -528,7 +556,8 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
     for (int i = 0; i < n_frames; i++) {
         if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
         const bool trns = frames[i].use_transparent != 0;
-        // the paired-row kernel reads band slabs only; stream-layout frames
+        // the paired-row kernel reads band slabs: a stream-layout frame it
+        // takes gets its slab built on the device at each launch; the rest
         // take the one-row-per-lane kernel
         const bool pair_ok = png_use_pair(frames[i].depth, frames[i].interlace, trns, frames[i].width,
                                           frames[i].out_stride);
@@ -537,7 +566,7 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
             ctx->last_error = "png: a slab-layout frame needs the paired-row kernel (zpx_png_stream_slab)";
             return ZPX_E_INVALID_ARGUMENT;
         }
-        const bool pair = frames[i].layout == ZPX_PNG_LAYOUT_SLAB;
+        const bool pair = pair_ok;
         by_depth[{frames[i].depth, pair, pair && trns}].push_back(i);
     }
     uint64_t bytes = 0;
@@ -549,12 +578,45 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
         std::vector<DevPngPass> passes;
         std::vector<uint32_t> rowbytes;
         Adam7Stage a7;
-        for (int idx : kv.second) {
+        // stream-layout frames on the paired-row kernel: one device slab each
+        std::vector<std::vector<uint64_t>> slab_off(kv.second.size());
+        std::vector<size_t> slab_at(kv.second.size(), 0);
+        size_t slab_total = 0;
+        for (size_t k = 0; k < kv.second.size() && g->pair; k++) {
+            const zpx_png_frame &f = frames[kv.second[k]];
+            if (f.layout != ZPX_PNG_LAYOUT_STREAM) continue;
+            slab_at[k] = slab_total;
+            slab_total = (slab_total + png_dev_slab_layout(f, slab_off[k]) + 255) & ~size_t(255);
+        }
+        std::vector<DevSlabBand> sjobs;
+        if (slab_total) HIPCHK(ctx, g->dslab.alloc(slab_total));
+        for (size_t k = 0; k < kv.second.size(); k++) {
+            const int idx = kv.second[k];
+            zpx_png_frame f = frames[idx];
+            if (g->pair && f.layout == ZPX_PNG_LAYOUT_STREAM) {
+                uint8_t *d_slab = g->dslab.as<uint8_t>() + slab_at[k];
+                HIPCHK(ctx, hipMemcpy(d_slab, slab_off[k].data(), slab_off[k].size() * sizeof(uint64_t),
+                                      hipMemcpyHostToDevice));
+                std::vector<DevPngPass> sp;
+                std::vector<uint32_t> srb;
+                uint64_t sbytes = 0;
+                png_frame_passes(f, sp, srb, sbytes); // (the stream's bytes)
+                png_dev_slab_jobs(f, slab_off[k], f.filtered, sbytes + ZPX_PNG_INPUT_PAD, d_slab, sjobs,
+                                  g->slab_max_groups);
+                f.filtered = d_slab;
+                f.layout = ZPX_PNG_LAYOUT_SLAB;
+            }
             const size_t first = passes.size();
-            png_frame_passes(frames[idx], passes, rowbytes, bytes);
+            png_frame_passes(f, passes, rowbytes, bytes);
             const int obpx = png_out_bpp(frames[idx].depth, frames[idx].use_transparent != 0);
             bytes += uint64_t(frames[idx].width) * frames[idx].height * obpx;
             if (g->pair && frames[idx].interlace) png_adam7_stage(frames[idx], obpx, passes, first, a7);
+        }
+        if (!sjobs.empty()) {
+            g->nslab_jobs = static_cast<uint32_t>(sjobs.size());
+            HIPCHK(ctx, g->slab_jobs.alloc(sjobs.size() * sizeof(DevSlabBand)));
+            HIPCHK(ctx, hipMemcpy(g->slab_jobs.ptr, sjobs.data(), sjobs.size() * sizeof(DevSlabBand),
+                                  hipMemcpyHostToDevice));
         }
         if (!a7.jobs.empty()) {
             HIPCHK(ctx, g->staging.alloc(a7.bytes));
@@ -585,7 +647,7 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
     for (auto &g : plan->jpeg) {
         int rc;
         if (plan->kind == 0)
-            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->max_gw, g->max_gh, g->bits, g->narrow, st);
+            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->geom, g->bits, g->narrow, st);
         else
             rc = launch_jpeg_rgba(g->frames.as<DevJpegFrame>(), g->n, g->color, g->h0, g->v0, g->hc, g->vc,
                                   g->max_mxx, g->max_myy, g->bits, g->narrow, g->vec_out, st);
@@ -593,6 +655,10 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
     for (auto &g : plan->png) {
+        // stream-layout frames: their band slabs first
+        if (g->nslab_jobs && launch_png_slab(png_slab_chunk_bytes(g->depth), g->slab_jobs.as<DevSlabBand>(),
+                                             g->nslab_jobs, g->slab_max_groups, st))
+            return hip_fail(ctx, hipGetLastError(), "png slab kernel launch");
         const int rc = g->pair ? launch_png_pair(g->depth, g->trns, g->passes.as<DevPngPass>(),
                                                  g->sched.as<DevPngBand>(), g->nsched, g->scratch.as<uint32_t>(),
                                                  g->boundary.as<uint64_t>(), g->band_bytes, st)
@@ -664,6 +730,7 @@ struct zpx_jpeg_coeffs {
 };
 struct zpx_png_stream {
     PngStream s;
+    std::mutex slab_mu; // zpx_png_stream_slab builds s.slab once, whichever thread asks first
 };
 
 static int zpx_jpeg_entropy_decode_impl(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
@@ -772,6 +839,7 @@ extern "C" int zpx_png_stream_slab(zpx_png_stream *s, const uint8_t **data, size
 {
     if (!s || !data || !len) return ZPX_E_INVALID_ARGUMENT;
     return guarded([&] {
+        std::lock_guard<std::mutex> lk(s->slab_mu);
         if (!s->s.slab_len)
             if (int e = png_stream_build_slab(s->s, png_inflate_threads())) return e;
         *data = static_cast<const uint8_t *>(s->s.slab.ptr);
@@ -780,6 +848,55 @@ extern "C" int zpx_png_stream_slab(zpx_png_stream *s, const uint8_t **data, size
     });
 }
 extern "C" void zpx_png_stream_free(zpx_png_stream *s) { delete s; }
+
+// Test hook: the band slab of stream `s` as the plans build it on the device
+// (png_slab_kernels.hip), copied back to `out` (cap bytes; *len = its size).
+// Bytes the paired-row kernel never reads (groups past a band's last, region
+// tails) are left as 0xa5.
+static int zpx_debug_png_device_slab_impl(zpx_ctx *ctx, const zpx_png_stream *ss, uint8_t *out, size_t cap,
+                                          size_t *len)
+{
+    if (!ctx || !ss || !len) return ZPX_E_INVALID_ARGUMENT;
+    CtxScope scope(ctx);
+    const PngStream &ps = ss->s;
+    if (!png_use_pair(ps.depth, ps.interlace, ps.use_transparent, ps.width, size_t(ps.width) * ps.out_bpp))
+        return ZPX_E_UNSUPPORTED;
+    zpx_png_frame f;
+    memset(&f, 0, sizeof(f));
+    f.width = ps.width;
+    f.height = ps.height;
+    f.depth = ps.depth;
+    f.interlace = ps.interlace;
+    f.use_transparent = ps.use_transparent;
+    f.out_stride = size_t(ps.width) * ps.out_bpp;
+    std::vector<uint64_t> off;
+    const size_t n = png_dev_slab_layout(f, off);
+    *len = n;
+    if (!out || cap < n) return out ? ZPX_E_INVALID_ARGUMENT : ZPX_OK;
+    DevBuf din, dslab, djobs;
+    const size_t in_len = ps.data_len + ZPX_PNG_INPUT_PAD;
+    HIPCHK(ctx, din.alloc(in_len));
+    HIPCHK(ctx, hipMemcpy(din.ptr, ps.data.ptr, in_len, hipMemcpyHostToDevice));
+    HIPCHK(ctx, dslab.alloc(n));
+    HIPCHK(ctx, hipMemset(dslab.ptr, 0xa5, n));
+    HIPCHK(ctx, hipMemcpy(dslab.ptr, off.data(), off.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    std::vector<DevSlabBand> jobs;
+    uint32_t groups = 0;
+    png_dev_slab_jobs(f, off, din.as<uint8_t>(), in_len, dslab.as<uint8_t>(), jobs, groups);
+    HIPCHK(ctx, djobs.alloc(jobs.size() * sizeof(DevSlabBand)));
+    HIPCHK(ctx, hipMemcpy(djobs.ptr, jobs.data(), jobs.size() * sizeof(DevSlabBand), hipMemcpyHostToDevice));
+    if (launch_png_slab(png_slab_chunk_bytes(ps.depth), djobs.as<DevSlabBand>(), static_cast<uint32_t>(jobs.size()),
+                        groups, ctx->stream))
+        return hip_fail(ctx, hipGetLastError(), "png slab kernel");
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(out, dslab.ptr, n, hipMemcpyDeviceToHost));
+    return ZPX_OK;
+}
+
+extern "C" int zpx_debug_png_device_slab(zpx_ctx *ctx, const zpx_png_stream *s, uint8_t *out, size_t cap, size_t *len)
+{
+    return guarded([&] { return zpx_debug_png_device_slab_impl(ctx, s, out, cap, len); });
+}
 
 // ------------------------------------------------------------------ jpeg.decode
 namespace {

@@ -176,10 +176,14 @@ class PngBatch:
 
     def __init__(self, items: list[Stream], slots: list[int] | None = None, device: int = 0,
                  ctx: context.Context | None = None, layout: str = "auto"):
-        """layout: "auto" uploads each image's band slab where the
-        paired-row kernel takes it (Stream.slab, what the decode and batch
-        paths do), else the inflated stream; "stream" always the stream;
-        "mixed" (tests) slabs for even item indices, streams for odd ones."""
+        """layout: "auto" uploads each image's host-built band slab where
+        the paired-row kernel takes it (Stream.slab), else the inflated
+        stream; "stream" always the inflated stream, as parseIdat hands it to
+        readImagePass (png/decoder.zig:516-523) -- for the images the
+        paired-row kernel takes, every launch then builds their slab on the
+        device first (png_slab_kernels.hip; what png.decode and the batch
+        pipeline do); "mixed" (tests) slabs for even item indices, streams
+        for odd ones."""
         torch = _torch()
         self.ctx = ctx or context.default(device)
         self.device = torch.device("cuda", self.ctx.device)
