@@ -575,6 +575,11 @@ int zpx_debug_png_device_slab(zpx_ctx *ctx, const zpx_png_stream *s, uint8_t *ou
  * parallel in this process (tests: the parallel path ran, not its serial
  * fallback).  Host-only. */
 int64_t zpx_debug_jpeg_parallel_scans(void);
+/* Number of progressive frames whose scans the host entropy stage has
+ * decoded concurrently (dependency-ordered, checked against the serial
+ * loop's continuation; a frame that fails the check is decoded serially and
+ * not counted).  Host-only. */
+int64_t zpx_debug_jpeg_parallel_progressive(void);
 /* Test hook for zpx_batch_decode_sharded: 1 installs an in-process fake
  * communicator table in place of RCCL -- ncclSend/ncclRecv pairs matched at
  * ncclGroupEnd and carried out as stream-ordered device copies (the receive

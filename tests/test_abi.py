@@ -597,3 +597,66 @@ def test_parallel_inflate_matches_zlib(threads):
                 pytest.fail("accepted a stream whose first bytes zlib rejects")
             assert len(ref) >= len(raw) and out[:len(raw)].tobytes() == ref[:len(raw)]
     assert accepted >= (16 if threads == 1 else 8)  # dynamic-block streams decode in parallel
+
+
+def _progressive_jpegs():
+    """Progressive JPEGs: the reference's progressive fixtures
+    (decoder.zig:1843-1920 pairs) and Pillow encodes of every subsampling,
+    gray, ragged sizes."""
+    import io
+
+    from PIL import Image
+    from tools import synthetic as S
+
+    out = [(os.path.basename(p), open(p, "rb").read()) for p in JPEGS if "progressive" in os.path.basename(p)]
+    for name, sub, w, h, q in [("420", 2, 333, 177, 80), ("444", 0, 129, 65, 95), ("422", 1, 250, 99, 30),
+                               ("444_big", 0, 640, 480, 75), ("gray", None, 203, 77, 60), ("420_tiny", 2, 9, 7, 90)]:
+        b = io.BytesIO()
+        px = S.content(w * 5 + h, w, h)
+        if sub is None:
+            Image.fromarray(px[..., 0]).save(b, "JPEG", quality=q, progressive=True)
+        else:
+            Image.fromarray(px).save(b, "JPEG", quality=q, subsampling=sub, progressive=True)
+        out.append((name, b.getvalue()))
+    return out
+
+
+def test_host_entropy_progressive_parallel_matches_oracle():
+    """Scan-parallel progressive decoding (jpeg_host.cpp run_deferred_scans:
+    the scans of processSos, decoder.zig:1148-1455 / refine :1459-1549, run
+    concurrently in dependency order, checked against the serial loop's
+    continuation): the oracle's coefficients on every progressive file, the
+    parallel path actually taken there, and on truncated or corrupted
+    streams -- which the check sends back to the serial loop -- the oracle's
+    coefficients or error name."""
+    from zpix_amd.shard import host_cpu_budget
+
+    if int(os.environ.get("ZPX_HUFF_THREADS", min(8, host_cpu_budget()))) < 2:  # (jpeg_huff_threads)
+        pytest.skip("one host thread: the serial loop decodes progressive scans")
+    L = _lib.lib()
+    srcs = _progressive_jpegs()
+    for name, data in srcs:
+        before = L.zpx_debug_jpeg_parallel_progressive()
+        oc = O.jpeg_coefficients(data)
+        pc = J.Coefficients(data)
+        assert L.zpx_debug_jpeg_parallel_progressive() == before + 1, name
+        for c in range(oc.n_comp):
+            assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32)), (name, c)
+    rng = np.random.default_rng(11)
+    for it in range(60):
+        d = bytearray(srcs[it % len(srcs)][1])
+        if it % 3 == 0:
+            d = d[:int(rng.integers(len(d) // 3, len(d)))]  # truncated inside some scan
+        else:
+            for _ in range(rng.integers(1, 3)):
+                d[rng.integers(len(d) // 4, len(d))] = rng.integers(0, 256)
+        data = bytes(d)
+        try:
+            oc = O.jpeg_coefficients(data)
+        except O.OracleError as e:
+            assert _jpeg_err_product(data) == e.name, it
+            continue
+        pc = J.Coefficients(data)
+        for c in range(oc.n_comp):
+            if oc.grids[c] is not None:
+                assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32)), (it, c)

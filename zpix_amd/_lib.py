@@ -155,6 +155,7 @@ EXPORTS = [
     "zpx_png_stream_data", "zpx_png_stream_slab", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
     "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config", "zpx_plan_status",
     "zpx_batch_decode_sharded", "zpx_debug_png_stall", "zpx_debug_jpeg_parallel_scans", "zpx_debug_png_device_slab",
+    "zpx_debug_jpeg_parallel_progressive",
     "zpx_bmp_decode", "zpx_bmp_load", "zpx_bmp_probe_buffer", "zpx_qoi_decode", "zpx_qoi_load",
     "zpx_qoi_probe_buffer", "zpx_qoi_encode", "zpx_qoi_encode_bound", "zpx_qoi_encode_device",
     "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel", "zpx_batch_wait_prefix",
@@ -226,6 +227,7 @@ def lib():
         "zpx_debug_png_stall": (i32, [vp, C.c_uint32, C.POINTER(C.c_double)]),
         "zpx_debug_png_device_slab": (i32, [vp, vp, vp, sz, C.POINTER(sz)]),
         "zpx_debug_jpeg_parallel_scans": (C.c_int64, []),
+        "zpx_debug_jpeg_parallel_progressive": (C.c_int64, []),
         "zpx_bmp_decode": (i32, [vp, vp, C.c_char_p, sz, C.POINTER(zpx_image)]),
         "zpx_bmp_load": (i32, [vp, vp, C.c_char_p, C.POINTER(zpx_image)]),
         "zpx_bmp_probe_buffer": (i32, [C.c_char_p, sz]),

@@ -9,6 +9,10 @@
 
 #include <cstdlib>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <condition_variable>
+#include <memory>
 #include <cstring>
 #include <thread>
 #include <map>
@@ -130,12 +134,56 @@ void HostBuf::release()
 }
 
 // ---------------------------------------------------------------- CoeffGrid
-bool CoeffGrid::init(size_t blocks, bool zero)
+bool CoeffGrid::init(size_t blocks, bool zero, int bits)
 {
     blocks_ = blocks;
-    bits_ = 8;
+    bits_ = bits;
     max_abs_ = 0;
-    return buf_.alloc(blocks * 64 * sizeof(int8_t), zero);
+    return buf_.alloc(blocks * 64 * static_cast<size_t>(bits / 8), zero);
+}
+
+bool CoeffGrid::set(size_t blk, int i, int32_t v)
+{
+    const int32_t a = v < 0 ? (v == INT32_MIN ? INT32_MAX : -v) : v;
+    if (a > max_abs_) {
+        max_abs_ = a;
+        const int need = a > 32767 ? 32 : a > 127 ? 16 : 8;
+        if (need > bits_ && !widen_to(need)) return false;
+    }
+    const size_t k = blk * 64 + static_cast<size_t>(i);
+    if (bits_ == 8) static_cast<int8_t *>(buf_.ptr)[k] = static_cast<int8_t>(v);
+    else if (bits_ == 16) static_cast<int16_t *>(buf_.ptr)[k] = static_cast<int16_t>(v);
+    else static_cast<int32_t *>(buf_.ptr)[k] = v;
+    return true;
+}
+
+bool CoeffGrid::narrow_to8(int threads)
+{
+    if (bits_ != 16 || max_abs_ > 127) return true;
+    HostBuf nb;
+    const size_t n = blocks_ * 64;
+    if (!nb.alloc(n, false)) return false;
+    const int16_t *src = static_cast<const int16_t *>(buf_.ptr);
+    int8_t *dst = static_cast<int8_t *>(nb.ptr);
+    const int nthr = static_cast<int>(std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(std::max(1, threads)),
+                                                                             n / (1u << 20))));
+    auto part = [&](int t) {
+        const size_t a = n * t / nthr, z = n * (t + 1) / nthr;
+        for (size_t i = a; i < z; i++) dst[i] = static_cast<int8_t>(src[i]);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; t++) {
+        try {
+            th.emplace_back(part, t);
+        } catch (...) {
+            part(t);
+        }
+    }
+    part(0);
+    for (auto &t : th) t.join();
+    buf_ = static_cast<HostBuf &&>(nb);
+    bits_ = 8;
+    return true;
 }
 
 void CoeffGrid::load(size_t blk, int32_t *b) const
@@ -515,7 +563,48 @@ class Decoder {
     template <class Sink>
     int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
             Sink &sink);
+    // one block of a progressive scan, touching only the scan's band
+    int prog_block(const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc);
+    // coefficient z (zig-zag order) of block blk of component ci: set also
+    // marks it nonzero in the block's mask (a refinement then visits only
+    // the nonzero coefficients of its band; a coefficient never returns to
+    // zero: refinements only add to its magnitude or set new ones)
+    int prog_set(int ci, size_t blk, int z, int32_t v)
+    {
+        const int i = kUnzig[z];
+        uint64_t *m = &(*nz_[ci])[blk];
+        if (int16_t *g = fixed16_[ci]) { // parallel scan: int16 grid, no widening
+            const int32_t a = v < 0 ? (v == INT32_MIN ? INT32_MAX : -v) : v;
+            if (a > 32767) return kParallelAbort;
+            job_max_[ci] = a > job_max_[ci] ? a : job_max_[ci];
+            g[blk * 64 + static_cast<size_t>(i)] = static_cast<int16_t>(v);
+            // (other bands of the block may be written concurrently)
+            if (v != 0 && !((__atomic_load_n(m, __ATOMIC_RELAXED) >> z) & 1))
+                __atomic_fetch_or(m, uint64_t(1) << z, __ATOMIC_RELAXED);
+            return 0;
+        }
+        if (v != 0) *m |= uint64_t(1) << z;
+        return o_.grid[ci].set(blk, i, v) ? 0 : ZPX_E_OUT_OF_MEMORY;
+    }
+    int32_t prog_get(int ci, size_t blk, int z) const
+    {
+        if (const int16_t *g = fixed16_[ci]) return g[blk * 64 + static_cast<size_t>(kUnzig[z])];
+        return o_.grid[ci].get(blk, kUnzig[z]);
+    }
+    uint64_t prog_mask(int ci, size_t blk) const { return __atomic_load_n(&(*nz_[ci])[blk], __ATOMIC_RELAXED); }
+    // refine :1459-1518 / refineNonZeroes :1522-1549 of an AC band on the
+    // grid itself, through the nonzero masks
+    int prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta);
+    int prog_refine_nonzero(int ci, size_t blk, uint64_t mask, int32_t zig, int32_t ze, int32_t nz, int32_t delta,
+                            int32_t &zout);
+    // the MCU loop of one scan, restart markers included (processSos
+    // :1298-1455), from the scan's first entropy-coded byte
+    int scan_loop(const Scan &sc, bool records);
     int restart_parallel(const Scan &sc, bool &done);
+    friend int run_deferred_scans(std::vector<std::unique_ptr<Decoder>> &jobs, JpegCoeffs &o, int threads);
+    // the run() loop head from byte p: the position after the next marker
+    // byte and that marker (false: the input ends first)
+    bool next_marker(size_t p, size_t &after, uint8_t &marker) const;
     int sof(int32_t n);
     int dqt(int32_t n);
     int dht(int32_t n);
@@ -541,6 +630,19 @@ class Decoder {
     bool interleaved_[4] = {}, noninterleaved_[4] = {};
     int threads_ = 1; // restart-interval-parallel Huffman (baseline scans with DRI)
     bool sparse_ok_ = false; // emit JpegSparse records for a single interleaved baseline scan
+  public:
+    // Progressive scans decoded in parallel (run_deferred_scans): the first
+    // pass walks the markers and, at each SOS, keeps a copy of the decoder --
+    // Huffman tables, restart interval and the scan as they are there --
+    // then skips the scan's entropy-coded bytes to the next marker.
+    std::vector<std::unique_ptr<Decoder>> *deferred_ = nullptr;
+  private:
+    Scan job_scan_;
+    size_t job_start_ = 0, job_skip_ = 0; // the scan's first byte; where the first pass resumed
+    int16_t *fixed16_[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::shared_ptr<std::vector<uint64_t>> nz_[4]; // progressive: per block, its nonzero coefficients (zig-zag bits)
+    int32_t job_max_[4] = {0, 0, 0, 0};
+    static constexpr int kParallelAbort = (1 << 20) + 1; // internal: a value past int16 in a parallel scan
 };
 
 int Decoder::sof(int32_t n)
@@ -825,7 +927,9 @@ int Decoder::sos(int32_t n)
             const size_t nb = size_t(mxx) * size_t(myy) * size_t(o_.comp[ci].h * o_.comp[ci].v);
             bool in_scan = false;
             for (int k = 0; k < ns; k++) in_scan |= scan[k].id == ci;
-            if (!o_.grid[ci].init(nb, !(full_cover && in_scan))) return ZPX_E_OUT_OF_MEMORY;
+            const bool defer = deferred_ != nullptr && o_.progressive;
+            if (!o_.grid[ci].init(nb, defer || !(full_cover && in_scan), defer ? 16 : 8)) return ZPX_E_OUT_OF_MEMORY;
+            if (o_.progressive) nz_[ci] = std::make_shared<std::vector<uint64_t>>(nb, 0);
             o_.has_grid[ci] = true;
         }
     }
@@ -847,6 +951,34 @@ int Decoder::sos(int32_t n)
     sc.myy = myy;
     ba_ = bm_ = 0;
     bn_ = 0;
+    if (deferred_ != nullptr && o_.progressive) {
+        // first pass of the parallel progressive decode: keep this scan's
+        // decoder, skip its entropy-coded bytes (to the first 0xFF that is
+        // not a stuffed byte or a restart marker)
+        std::unique_ptr<Decoder> job(new Decoder(*this));
+        job->deferred_ = nullptr;
+        job->job_scan_ = sc;
+        job->job_start_ = pos_;
+        size_t q = pos_;
+        while (q + 1 < len_ && !(src_[q] == 0xff && src_[q + 1] != 0x00 && (src_[q + 1] < 0xd0 || src_[q + 1] > 0xd7)))
+            q++;
+        if (q + 1 >= len_) q = len_;
+        job->job_skip_ = q;
+        deferred_->push_back(std::move(job));
+        pos_ = q;
+        unread_ = 0;
+        return 0;
+    }
+    ZTRY(scan_loop(sc, records));
+    // baseline reconstructs during the scan with the table current now
+    if (!o_.progressive)
+        for (int k = 0; k < ns; k++) snapshot_quant(scan[k].id);
+    return 0;
+}
+
+int Decoder::scan_loop(const Scan &sc, bool records)
+{
+    const int32_t mxx = sc.mxx, myy = sc.myy;
     bool done = false;
     if (!records) ZTRY(restart_parallel(sc, done));
     if (!done) {
@@ -875,9 +1007,6 @@ int Decoder::sos(int32_t n)
             }
         }
     }
-    // baseline reconstructs during the scan with the table current now
-    if (!o_.progressive)
-        for (int k = 0; k < ns; k++) snapshot_quant(scan[k].id);
     return 0;
 }
 
@@ -893,7 +1022,6 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
     for (int k = 0; k < sc.ns; k++) {
         const int ci = sc.c[k].id;
         const int32_t hi = o_.comp[ci].h, vi = o_.comp[ci].v;
-        CoeffGrid &g = o_.grid[ci];
         const Huff &hdc = huff_[0][sc.c[k].td];
         const Huff &hac = huff_[1][sc.c[k].ta];
         for (int32_t j = 0; j < hi * vi; j++) {
@@ -909,8 +1037,11 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
                     continue;
             }
             const size_t blk = size_t(by) * size_t(mxx * hi) + size_t(bx);
+            if (sc.prog) {
+                ZTRY(prog_block(sc, ci, blk, hdc, hac, dc));
+                continue;
+            }
             int nnz = 0;
-            if (sc.prog) g.load(blk, b);
             if (sc.ah != 0) {
                 ZTRY(refine(b, hac, sc.zs, sc.ze, int32_t(1) << sc.al));
             } else {
@@ -956,15 +1087,174 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
                     }
                 }
             }
-            if (sc.prog) {
-                if (!g.store(blk, b)) return ZPX_E_OUT_OF_MEMORY;
-            } else {
-                ZTRY(sink.put(ci, blk, b, nzpos, nnz));
-                for (int i = 0; i < nnz; i++) b[nzpos[i]] = 0;
-            }
+            ZTRY(sink.put(ci, blk, b, nzpos, nnz));
+            for (int i = 0; i < nnz; i++) b[nzpos[i]] = 0;
         }
     }
     return 0;
+}
+
+// A progressive scan's block (processSos :1340-1431 with refine :1459-1549):
+// the reference loads the whole block, updates the scan's band and stores
+// the whole block back; only the band can change, so only the band is read
+// and only the coefficients that changed are written -- the same grid, and
+// no cost for the blocks an EOB run skips.
+int Decoder::prog_block(const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc)
+{
+    if (sc.ah != 0) {
+        const int32_t delta = int32_t(1) << sc.al;
+        if (sc.zs == 0) { // refine :1461-1470
+            if (sc.ze != 0) return ZPX_E_PANIC;
+            bool set;
+            ZTRY(bit(set));
+            if (set) ZTRY(prog_set(ci, blk, 0, prog_get(ci, blk, 0) | delta));
+            return 0;
+        }
+        return prog_refine_ac(ci, blk, hac, sc.zs, sc.ze, delta);
+    }
+    int32_t zig = sc.zs;
+    if (zig == 0) {
+        zig++;
+        uint8_t t;
+        ZTRY(huffman(hdc, t));
+        if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+        int32_t delta;
+        ZTRY(receive_extend(t, delta));
+        dc[ci] += delta;
+        ZTRY(prog_set(ci, blk, 0, dc[ci] << sc.al));
+    }
+    if (zig <= sc.ze && eob_run_ > 0) {
+        eob_run_--;
+        return 0;
+    }
+    for (; zig <= sc.ze; zig++) {
+        uint8_t value;
+        ZTRY(huffman(hac, value));
+        const uint8_t v0r = value >> 4, v1 = value & 0x0f;
+        if (v1 != 0) {
+            zig += v0r;
+            if (zig > sc.ze) break;
+            int32_t ac;
+            ZTRY(receive_extend(v1, ac));
+            ZTRY(prog_set(ci, blk, zig, ac << sc.al));
+        } else {
+            if (v0r != 0x0f) {
+                eob_run_ = static_cast<uint16_t>(1u << v0r);
+                if (v0r != 0) {
+                    uint32_t x;
+                    ZTRY(bits(v0r, x));
+                    eob_run_ |= static_cast<uint16_t>(x);
+                }
+                eob_run_--;
+                break;
+            }
+            zig += 0x0f;
+        }
+    }
+    return 0;
+}
+
+// refineNonZeroes :1522-1549: from zig, each nonzero coefficient takes a
+// correction bit; the loop stops at the (nz+1)-th zero coefficient (nz = -1:
+// the band's end) and returns its position.  With the block's nonzero mask
+// the stop is found by bit arithmetic and the correction bits, one per
+// nonzero coefficient before it in zig-zag order, are read together (up to
+// 16 at a time: exactly the bits, and so the bytes, the reference's loop
+// reads one at a time).
+int Decoder::prog_refine_nonzero(int ci, size_t blk, uint64_t mask, int32_t zig, int32_t ze, int32_t nz,
+                                 int32_t delta, int32_t &zout)
+{
+    if (zig > ze) {
+        zout = zig;
+        return 0;
+    }
+    const uint64_t band = ((~uint64_t(0)) << zig) & (ze >= 63 ? ~uint64_t(0) : (uint64_t(2) << ze) - 1);
+    int32_t end = ze + 1;
+    if (nz >= 0) {
+        uint64_t zeros = ~mask & band;
+        for (int32_t k = 0; k < nz && zeros; k++) zeros &= zeros - 1;
+        if (zeros) end = __builtin_ctzll(zeros);
+    }
+    uint64_t m = mask & band & (end >= 64 ? ~uint64_t(0) : (uint64_t(1) << end) - 1);
+    while (m) {
+        const int n = std::min(16, __builtin_popcountll(m));
+        uint32_t corr;
+        ZTRY(bits(n, corr));
+        for (int k = n - 1; k >= 0; k--) {
+            const int z = __builtin_ctzll(m);
+            m &= m - 1;
+            if (!((corr >> k) & 1)) continue;
+            const int32_t v = prog_get(ci, blk, z);
+            ZTRY(prog_set(ci, blk, z, v + (v >= 0 ? delta : -delta)));
+        }
+    }
+    zout = end;
+    return 0;
+}
+
+int Decoder::prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta)
+{ // refine :1471-1518
+    int32_t zig = zs;
+    // (a coefficient this scan sets is outside the mask of the zeros the
+    // runs count, and is behind zig before the mask is read again)
+    if (eob_run_ == 0) {
+        for (; zig <= ze; zig++) {
+            int32_t z = 0;
+            uint8_t value;
+            ZTRY(huffman(h, value));
+            const uint8_t v0 = value >> 4, v1 = value & 0x0f;
+            if (v1 == 0) {
+                if (v0 != 0x0f) {
+                    eob_run_ = static_cast<uint16_t>(1u << v0);
+                    if (v0 != 0) {
+                        uint32_t x;
+                        ZTRY(bits(v0, x));
+                        eob_run_ |= static_cast<uint16_t>(x);
+                    }
+                    break;
+                }
+            } else if (v1 == 1) {
+                bool positive;
+                ZTRY(bit(positive));
+                z = positive ? delta : -delta;
+            } else {
+                return ZPX_E_UNEXPECTED_HUFFMAN_CODE;
+            }
+            ZTRY(prog_refine_nonzero(ci, blk, prog_mask(ci, blk), zig, ze, v0, delta, zig));
+            if (zig > ze) return ZPX_E_TOO_MANY_COEFFICIENTS;
+            if (z != 0) ZTRY(prog_set(ci, blk, zig, z));
+        }
+    }
+    if (eob_run_ > 0) {
+        eob_run_--;
+        int32_t ignored;
+        ZTRY(prog_refine_nonzero(ci, blk, prog_mask(ci, blk), zig, ze, -1, delta, ignored));
+    }
+    return 0;
+}
+
+bool Decoder::next_marker(size_t p, size_t &after, uint8_t &marker) const
+{ // run()'s loop head (decodeInner :240-283)
+    for (;;) {
+        if (p + 2 > len_) return false;
+        uint8_t t0 = src_[p], t1 = src_[p + 1];
+        p += 2;
+        while (t0 != 0xff) {
+            if (p >= len_) return false;
+            t0 = t1;
+            t1 = src_[p++];
+        }
+        uint8_t m = t1;
+        if (m == 0) continue;
+        while (m == 0xff) {
+            if (p >= len_) return false;
+            m = src_[p++];
+        }
+        if (m >= 0xd0 && m <= 0xd7) continue; // a stray RST
+        after = p;
+        marker = m;
+        return true;
+    }
 }
 
 std::atomic<int64_t> g_parallel_scans{0}; // zpx_debug_jpeg_parallel_scans
@@ -1171,13 +1461,151 @@ int Decoder::run()
     return 0;
 }
 
+std::atomic<int64_t> g_parallel_prog{0}; // progressive frames decoded scan-parallel (zpx_debug_jpeg_parallel_scans)
+
+// The scans of a progressive frame, decoded concurrently (the reference's
+// processSos runs them one after another, decoder.zig:1148-1455, refine
+// :1459-1549).  Scan j waits for every earlier scan that touches a
+// coefficient it touches (a common component with overlapping spectral
+// bands: refinements follow their band's first scan, DC refinement the DC
+// scan); the rest run at once on `threads` threads -- with the standard
+// scripts the luma bands, the chroma scans and the DC scans overlap.  Each
+// scan runs on the copy of the decoder made at its SOS (its Huffman tables
+// and restart interval), from its first entropy-coded byte, with an empty
+// bit buffer, zero DC predictors and no EOB run, into int16 grids (a value
+// past int16 aborts).  The result is the serial loop's when (checked after):
+// every scan but the last ends with no EOB run pending (the next one started
+// with none), and the marker loop resumed from where each scan's decoding
+// stopped reaches the same next marker as the first pass did.  Anything
+// else -- an error in any scan included -- returns false, and the caller
+// decodes the frame serially from the start, so results and errors are the
+// reference's by construction.
+int run_deferred_scans(std::vector<std::unique_ptr<Decoder>> &jobs, JpegCoeffs &o, int threads)
+{
+    const size_t n = jobs.size();
+    // the components and zig-zag band each scan touches
+    std::vector<std::vector<size_t>> deps(n);
+    for (size_t j = 0; j < n; j++) {
+        const auto &a = jobs[j]->job_scan_;
+        for (size_t i = 0; i < j; i++) {
+            const auto &b = jobs[i]->job_scan_;
+            bool common = false;
+            for (int x = 0; x < a.ns; x++)
+                for (int y = 0; y < b.ns; y++) common |= a.c[x].id == b.c[y].id;
+            if (common && a.zs <= b.ze && b.zs <= a.ze) deps[j].push_back(i);
+        }
+    }
+    for (size_t j = 0; j < n; j++) {
+        Decoder &d = *jobs[j];
+        for (int c = 0; c < o.n_comp; c++) d.fixed16_[c] = o.has_grid[c] ? o.grid[c].data16() : nullptr;
+        for (int k = 0; k < d.job_scan_.ns; k++)
+            if (!d.fixed16_[d.job_scan_.c[k].id]) return false;
+    }
+    std::vector<int> rc(n, 0);
+    std::vector<char> state(n, 0); // 0 waiting, 1 running, 2 done
+    std::mutex mu;
+    std::condition_variable cv;
+    bool failed = false;
+    size_t finished = 0;
+    auto worker = [&] {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            size_t pick = n;
+            for (size_t j = 0; j < n && pick == n && !failed; j++) {
+                if (state[j] != 0) continue;
+                bool ready = true;
+                for (size_t i : deps[j]) ready &= state[i] == 2;
+                if (ready) pick = j;
+            }
+            if (pick == n) {
+                if (failed || finished == n) return;
+                cv.wait(lk);
+                continue;
+            }
+            state[pick] = 1;
+            lk.unlock();
+            Decoder &d = *jobs[pick];
+            d.pos_ = d.job_start_;
+            d.unread_ = 0;
+            d.ba_ = d.bm_ = 0;
+            d.bn_ = 0;
+            d.eob_run_ = 0;
+            int r = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            try {
+                r = d.scan_loop(d.job_scan_, false);
+            } catch (...) {
+                r = ZPX_E_OUT_OF_MEMORY;
+            }
+            if (getenv("ZPX_JPEG_PROG_TRACE"))
+                fprintf(stderr, "scan %zu ns %d c0 %d zs %d ze %d ah %u al %u: %.1f ms\n", pick, d.job_scan_.ns,
+                        d.job_scan_.c[0].id, d.job_scan_.zs, d.job_scan_.ze, d.job_scan_.ah, d.job_scan_.al,
+                        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3);
+            lk.lock();
+            rc[pick] = r;
+            state[pick] = 2;
+            finished++;
+            if (r) failed = true;
+            cv.notify_all();
+        }
+    };
+    const int nthr = std::max(1, std::min<int>(threads, static_cast<int>(n)));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; t++) {
+        try {
+            th.emplace_back(worker);
+        } catch (...) {
+            break;
+        }
+    }
+    worker();
+    for (auto &t : th) t.join();
+    if (failed || finished != n) return false;
+    for (size_t j = 0; j < n; j++) {
+        const Decoder &d = *jobs[j];
+        if (j + 1 < n && d.eob_run_ != 0) return false;
+        // where the serial loop resumes: readFull's settle() first
+        const size_t resume = (d.unread_ > 0 && d.bn_ >= 8) ? d.pos_ - d.unread_ : d.pos_;
+        size_t a0 = 0, a1 = 0;
+        uint8_t m0 = 0, m1 = 0;
+        const bool ok0 = d.next_marker(resume, a0, m0), ok1 = d.next_marker(d.job_skip_, a1, m1);
+        if (!ok0 || !ok1 || a0 != a1 || m0 != m1) return false;
+    }
+    for (int c = 0; c < o.n_comp; c++) {
+        if (!o.has_grid[c]) continue;
+        int32_t m = 0;
+        for (auto &d : jobs) m = std::max(m, d->job_max_[c]);
+        o.grid[c].note_max_abs(m);
+        if (!o.grid[c].narrow_to8(threads)) return false;
+    }
+    g_parallel_prog.fetch_add(1, std::memory_order_relaxed);
+    return true;
+}
+
 } // namespace
 
 int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads, bool sparse)
 {
     try { // no exception crosses the ABI
-        int e;
-        {
+        int e = 0;
+        bool decoded = false;
+        static const bool prog_par = [] {
+            const char *v = getenv("ZPX_JPEG_PROG_PARALLEL");
+            return !(v && v[0] == '0');
+        }();
+        if (threads > 1 && prog_par) {
+            // progressive scans in parallel (run_deferred_scans); a frame
+            // without deferred scans was decoded by this run as usual
+            std::vector<std::unique_ptr<Decoder>> jobs;
+            {
+                Decoder d(buf, len, out, false, threads, sparse);
+                d.deferred_ = &jobs;
+                e = d.run();
+            }
+            decoded = jobs.empty() || (!e && run_deferred_scans(jobs, out, threads));
+            if (!decoded) out = JpegCoeffs{}; // the serial loop from the start
+        }
+        if (!decoded) {
             Decoder d(buf, len, out, false, threads, sparse);
             e = d.run();
         }
@@ -1212,6 +1640,7 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int thr
 }
 
 int64_t jpeg_parallel_scans() { return g_parallel_scans.load(); }
+int64_t jpeg_parallel_progressive() { return g_parallel_prog.load(); }
 
 int jpeg_huff_threads()
 {

@@ -45,7 +45,7 @@ class CoeffGrid {
     // int8 and is widened (copied) the first time a value does not fit.
     // Conforming 8-bit streams never need int32; the bench's q75 frames fit
     // int8, natural photos usually need int16 (iceberg.jpg: max |AC| 157).
-    bool init(size_t blocks, bool zero = true); // zero = false: every block will be stored
+    bool init(size_t blocks, bool zero = true, int bits = 8); // zero = false: every block will be stored
     int bits() const { return bits_; }
     bool wide() const { return bits_ == 32; }
     size_t blocks() const { return blocks_; }
@@ -57,6 +57,21 @@ class CoeffGrid {
     // positions pos[] (all distinct).
     bool store_sparse(size_t blk, const int32_t *b, const uint8_t *pos, int n);
     bool widen_to(int bits);                  // no-op when already that wide
+    // One coefficient (natural index i of block blk), for the progressive
+    // scans, which touch only their band's coefficients: set widens as store.
+    int32_t get(size_t blk, int i) const
+    {
+        const size_t k = blk * 64 + static_cast<size_t>(i);
+        return bits_ == 8 ? static_cast<const int8_t *>(buf_.ptr)[k]
+                          : bits_ == 16 ? static_cast<const int16_t *>(buf_.ptr)[k] : static_cast<const int32_t *>(buf_.ptr)[k];
+    }
+    bool set(size_t blk, int i, int32_t v);
+    // The parallel progressive scans write an int16 grid directly (no
+    // widening); afterwards the grid takes the running max and, when every
+    // value fits, narrows to int8 (`threads` share the copy).
+    int16_t *data16() { return bits_ == 16 ? static_cast<int16_t *>(buf_.ptr) : nullptr; }
+    void note_max_abs(int32_t m) { max_abs_ = m > max_abs_ ? m : max_abs_; }
+    bool narrow_to8(int threads);
     // Concurrent stores into the grid at its current width: disjoint blocks
     // from several threads, no widening; a value too wide for the grid goes
     // to `overflow` (element index, value) and the running max |value| to
@@ -121,6 +136,7 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int thr
 // else min(8, hardware threads)
 int jpeg_huff_threads();
 int64_t jpeg_parallel_scans(); // scans decoded restart-interval-parallel so far
+int64_t jpeg_parallel_progressive(); // progressive frames decoded scan-parallel so far
 
 // jpeg.decodeConfig (decoder.zig:178-218): markers up to SOF (JFIF) or SOS,
 // skipping DQT/DRI/DHT.  model: ZPX_MODEL_GRAY or ZPX_MODEL_YCBCR.

@@ -1368,6 +1368,7 @@ extern "C" int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *se
 }
 
 extern "C" int64_t zpx_debug_jpeg_parallel_scans(void) { return jpeg_parallel_scans(); }
+extern "C" int64_t zpx_debug_jpeg_parallel_progressive(void) { return jpeg_parallel_progressive(); }
 
 // Test hook for the sparse coefficient records (JpegSparse): decodes `buf` in
 // record mode and expands the records on the host with the mapping of
