@@ -825,9 +825,11 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
     PTask k = task_of(task);
     issue(k);
     // the loop head expects the previous task's 8 stores behind the DMA
+    // (dropped: empty range; offsets apart, so hipcc cannot merge them into
+    // fewer, wider stores -- which would let vmcnt(8) pass before the DMA)
     const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, none, 8 * i, 0, kStoreAux);
+    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, none, 4096 * i, 0, kStoreAux);
     constexpr uint32_t kDrop = 0x80000000u;
     for (;;) {
         const int tn = task + tstride;
