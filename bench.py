@@ -75,6 +75,20 @@ def parse():
     return ap.parse_args()
 
 
+def traffic_of(args, line: str):
+    """HBM bytes per launch of a bench line's plan from rocprofv3 --pmc
+    (tools/pmc_summary.py writes profiles/traffic.json: FETCH_SIZE x2 +
+    WRITE_SIZE, summed over the plan's kernels), or None when not measured
+    for this workload."""
+    try:
+        tj = json.load(open(args.traffic_json))
+        if tj.get("images") == args.images and tj.get("size") == args.size and line in tj:
+            return tj[line]["hbm_bytes_per_launch"]
+    except Exception:
+        pass
+    return None
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -276,6 +290,7 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         "kernel_ms_per_launch": round(kern_ms, 3),
         "roofline": {"bound": "hbm", "achieved": round(jb.bytes / (kern_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(jb.bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                     "traffic": traffic_of(args, "progressive_444") if int(co.frame.coeff_bits) == 8 else None,
                      "algorithmic_bytes_per_launch": jb.bytes},
         "host_entropy_mpix_s": round(W * H / t_ent / 1e6, 1),
         "config": {"workload": f"{args.images}x {W}x{H} progressive 4:4:4 JPEG -> RGBA, configs[4]"}}
@@ -296,13 +311,7 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
             raise SystemExit("parity failure: Adam7 RGBA16 PNG != oracle")
     wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, args.warmup, ws)
     pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
-    atraffic = None
-    try:
-        ta = json.load(open(args.traffic_json)).get("adam7_rgba16", {})
-        if ta.get("images") == args.images and ta.get("size") == args.size:
-            atraffic = ta.get("hbm_bytes_per_launch")
-    except Exception:
-        atraffic = None
+    atraffic = traffic_of(args, "adam7_rgba16")
     out["png_adam7_rgba16"] = {
         "value": round(pb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
         "kernel_ms_per_launch": round(kern_ms, 3),
@@ -312,6 +321,28 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
         "host_inflate_mpix_s": round(W * H / t_inf / 1e6, 1),
         "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64, configs[4]"}}
     del pb
+    torch.cuda.empty_cache()
+    # Image.rgbaPixels of that NRGBA64 output (image.zig:103-130, the
+    # premultiply of color.zig:73-89), resident batch, one plan launch
+    import zpix_amd
+
+    img = zpix_amd.from_buffer(pd)
+    rb = device.RgbaBatch([img], slots=[0] * args.images, ctx=ctx)
+    if rank == 0:
+        rb.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        if not np.array_equal(rb.output_tensor(0).cpu().numpy().reshape(-1), O.png_decode(pd).rgba_pixels()):
+            raise SystemExit("parity failure: rgbaPixels of NRGBA64 != oracle")
+    wall, kern_ms = timed_steps(torch, dist, rb.launch, steps, args.warmup, ws)
+    ach = rb.bytes / (kern_ms * 1e-3) / 1e9
+    out["rgba_pixels_nrgba64"] = {
+        "value": round(rb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
+        "kernel_ms_per_launch": round(kern_ms, 3),
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "rgba_batch_kernel<NRGBA64>",
+                     "traffic": traffic_of(args, "rgba_pixels_nrgba64"), "algorithmic_bytes_per_launch": rb.bytes},
+        "config": {"workload": f"{args.images}x {W}x{H} NRGBA64 -> RGBA8 (Image.rgbaPixels), configs[4]'s Adam7 output"}}
+    del rb
     torch.cuda.empty_cache()
     return out
 
@@ -347,12 +378,7 @@ def bench_planar(args, torch, dist, ws, rank, ctx, device, jpeg, datas):
                          "traffic": None, "algorithmic_bytes_per_launch": jb.bytes},
             "config": {"workload": f"{args.images}x {args.size}x{args.size} baseline 4:2:0 JPEG -> Y/Cb/Cr planes "
                                    f"(jpeg.load), int{bits} coefficients"}}
-        try:
-            tp = json.load(open(args.traffic_json)).get(f"planar_int{bits}", {})
-            if tp.get("images") == args.images and tp.get("size") == args.size:
-                out[f"int{bits}"]["roofline"]["traffic"] = tp.get("hbm_bytes_per_launch")
-        except Exception:
-            pass
+        out[f"int{bits}"]["roofline"]["traffic"] = traffic_of(args, f"planar_int{bits}")
         del jb
         torch.cuda.empty_cache()
     return out
@@ -543,18 +569,9 @@ def main():
         value = px_per_step * args.steps / wall / 1e6
         launch_bytes = batch.bytes
         achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
         jkernel = "jpeg_block_kernel"  # the kernel the plan runs on these frames (jpeg_kernels.hip)
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                if tj.get("images") == args.images and tj.get("size") == args.size and tj.get("kernel") == jkernel:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
         coeff_bits = int(coeffs[0].frame.coeff_bits)
-        if traffic is not None and tj.get("coeff_bits", 16) != coeff_bits:
-            traffic = None  # measured on the other coefficient transport
+        traffic = traffic_of(args, "headline") if coeff_bits == 8 else None
         # the same frames through the int16 transport (what a frame with any
         # |coefficient| > 127 takes), for comparison: kernel time only
         int16 = None
@@ -568,14 +585,8 @@ def main():
             a16 = batch.bytes / (k16 * 1e-3) / 1e9
             int16 = {"kernel_ms_per_launch": round(k16, 4), "algorithmic_bytes_per_launch": batch.bytes,
                      "mpix_s_kernel_only": round(batch.pixels * ws / (k16 * 1e-3) / 1e6, 1),
-                     "achieved": round(a16, 1), "frac": round(a16 / PEAK_HBM_GBS, 4), "traffic": None}
-            t16 = os.path.join(os.path.dirname(args.traffic_json), "traffic_int16.json")
-            try:
-                tj16 = json.load(open(t16))
-                if tj16.get("images") == args.images and tj16.get("size") == args.size:
-                    int16["traffic"] = tj16.get("hbm_bytes_per_launch")
-            except Exception:
-                pass
+                     "achieved": round(a16, 1), "frac": round(a16 / PEAK_HBM_GBS, 4),
+                     "traffic": traffic_of(args, "int16")}
         result = {
             "metric": "MPixels/sec decoded (4K baseline JPEG 4:2:0) at 1/8 GPU; % HBM roofline",
             "value": round(value, 1),
@@ -634,14 +645,8 @@ def main():
         steps = max(3, args.steps // 2)
         pv = pb.pixels * ws * steps / wall / 1e6
         ach = pb.bytes / (kern_ms * 1e-3) / 1e9
-        ptraffic = None
         pkernel = "png_pair_kernel<TC8>"
-        try:
-            tp = json.load(open(args.traffic_json)).get("png", {})
-            if tp.get("images") == args.images and tp.get("size") == args.size and tp.get("kernel") == pkernel:
-                ptraffic = tp.get("hbm_bytes_per_launch")
-        except Exception:
-            ptraffic = None
+        ptraffic = traffic_of(args, "png")
         pres = {"metric": "MPixels/sec decoded (4K truecolor-8 PNG, mixed Sub/Up/Avg/Paeth)", "value": round(pv, 1),
                 "unit": "MPixels/sec", "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
                 "config": {"workload": f"{args.images}x {W}x{H} tc8 PNG unfilter -> RGBA, configs[2]"},
@@ -670,6 +675,8 @@ def main():
             "kernel_ms_per_launch": round(skern, 3),
             "roofline": {"bound": "hbm", "achieved": round(sach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(sach / PEAK_HBM_GBS, 4), "kernel": "png_slab_kernel<12> + " + pkernel,
+                         "traffic": (traffic_of(args, "png_slab_build") + ptraffic
+                                     if traffic_of(args, "png_slab_build") and ptraffic else None),
                          "algorithmic_bytes_per_launch": sb.bytes},
             "note": "inflated stream in HBM -> band slab built on the device -> unfilter: both kernels inside the "
                     "timed plan; algorithmic bytes = stream read + RGBA write (the slab's write and re-read are "

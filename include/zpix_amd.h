@@ -420,6 +420,12 @@ void zpx_plan_destroy(zpx_plan *plan);
 /* Image.rgbaPixels on device memory: img->pixels / img->palette are DEVICE
  * pointers; out is a DEVICE buffer of 4*dX*dY bytes. */
 int zpx_dev_rgba_pixels(zpx_ctx *ctx, const zpx_image *img, uint8_t *out, void *stream);
+/* Image.rgbaPixels (image.zig:103-130) of n device-resident images as one
+ * plan: imgs[i].pixels / palette are DEVICE pointers, outs[i] a DEVICE
+ * buffer of 4*dX*dY bytes (RGBA8, stride 4*dX).  zpx_plan_launch enqueues
+ * one kernel per image kind (no host work); zpx_plan_bytes counts the pixels
+ * each kind reads plus the RGBA8 written. */
+int zpx_rgba_plan_create(zpx_ctx *ctx, const zpx_image *imgs, uint8_t *const *outs, int n, zpx_plan **out);
 
 /* ---------------------------------------------------------------------- */
 /* host entropy stage exposed for batching / parity                        */

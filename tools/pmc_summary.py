@@ -1,83 +1,106 @@
-"""Summarise rocprofv3 --pmc CSVs (gpurun_out/pmc/*) per kernel: mean per dispatch."""
-import csv
+"""Summarise rocprofv3 --pmc CSVs (one directory per pass) per kernel
+instance: mean counter value per dispatch; optionally write the HBM
+traffic per launch that bench.py reports as roofline.traffic.
+
+Usage: python3 tools/pmc_summary.py <pass dir root> [traffic.json out] [images] [size]
+
+HBM bytes: FETCH_SIZE x 2 (gfx950 tallies a 128-B streaming read request as
+64 B, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KiB.  A bench line
+whose plan runs several kernels (Adam7: two launches of the paired-row
+kernel; PNG from the stream: the slab build + the paired-row kernel) sums
+them."""
 import collections
+import csv
 import json
 import os
+import re
 import sys
 
-base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for p in sorted(os.listdir(base)):
-    f = os.path.join(base, p, "run_counter_collection.csv")
-    if not os.path.exists(f):
-        continue
-    for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"]
-        short = ("jpeg_rgba" if "jpeg_rgba" in name else "jpeg_block" if "jpeg_block_kernel" in name
-                 else "png_unfilter" if "png_unfilter" in name
-                 else "png_pair" if "png_pair_kernel" in name
-                 else "png_adam7_merge" if "png_adam7_merge" in name else None)
-        import re
-        if short == "png_pair":  # one entry per depth template (tc8 vs the Adam7 RGBA16 line)
-            m = re.search(r"png_pair_kernel<(\d+)(?:, *\w+, *(\w+))?", name)
-            if m and m.group(1) != "6":
-                short = "png_pair_d" + m.group(1)
-            if m and m.group(2) == "true":  # the Adam7 pass-6 merge launch
-                short += "_merge" if short != "png_pair" else "_d6_merge"
-        if short == "jpeg_block":  # the headline instance keeps the plain key
-            m = re.search(r"jpeg_block_kernel<([^>]*)>", name)
-            if m and m.group(1).replace(" ", "") not in ("signedchar,true,2,2,1,1,0", "char,true,2,2,1,1,0"):
-                short = "jpeg_block<" + m.group(1).replace(" ", "") + ">"
-        if not short:
-            continue
-        acc[short][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
-out = {}
-for k, d in acc.items():
-    per = collections.defaultdict(list)
-    for (cn, disp), vals in d.items():
-        per[cn].append(sum(vals))
-    out[k] = {cn: sum(v) / len(v) for cn, v in per.items()}
-print(json.dumps(out, indent=1))
+# kernel-name pattern -> short key (the first match wins)
+KEYS = [
+    (r"jpeg_plane_block_kernel<signed char>", "jpeg_plane_block_i8"),
+    (r"jpeg_plane_block_kernel<short>", "jpeg_plane_block_i16"),
+    (r"jpeg_block_kernel<signed char, true, 2, 2, 1, 1, 0>", "jpeg_block"),  # the headline instance
+    (r"jpeg_block_kernel<short, true, 2, 2, 1, 1, 0>", "jpeg_block_i16"),
+    (r"jpeg_block_kernel<signed char, true, 1, 1, 1, 1, 0>", "jpeg_block_444_i8"),
+    (r"jpeg_block_kernel<short, true, 1, 1, 1, 1, 0>", "jpeg_block_444_i16"),
+    (r"jpeg_block_kernel<([^>]*)>", None),
+    (r"jpeg_rgba_kernel", "jpeg_rgba"),
+    (r"png_slab_kernel<(\d+)>", "png_slab_cb{0}"),
+    (r"png_pair_kernel<(\d+), (\w+), (\w+)>", "png_pair_d{0}{2}"),
+    (r"png_unfilter_kernel", "png_unfilter"),
+    (r"rgba_pixels_kernel", "rgba_pixels"),
+    (r"jpeg_sparse_expand", "jpeg_sparse_expand"),
+]
 
-# roofline.traffic for bench.py: HBM bytes per launch of the fused JPEG kernel,
-# FETCH_SIZE/WRITE_SIZE in KiB; FETCH_SIZE doubled (gfx950 tallies a 128-B
-# streaming read request as 64 B, MI355X_MICROARCH.md "HBM").
-jk = "jpeg_block" if "jpeg_block" in out else "jpeg_rgba"
-if len(sys.argv) > 2 and jk in out:
-    j = out[jk]
-    tr = {"kernel": jk + "_kernel", "images": int(sys.argv[3]) if len(sys.argv) > 3 else 64,
-          "size": int(sys.argv[4]) if len(sys.argv) > 4 else 4096,
-          "fetch_bytes_per_launch": 2 * j["FETCH_SIZE"] * 1024, "write_bytes_per_launch": j["WRITE_SIZE"] * 1024,
-          "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, KiB -> B, mean per dispatch"}
-    tr["hbm_bytes_per_launch"] = tr["fetch_bytes_per_launch"] + tr["write_bytes_per_launch"]
-    try:  # the coefficient transport the passes ran with (bench config)
-        tr["coeff_bits"] = json.load(open(os.path.join(base, "fetch.json")))["config"]["coeff_bits"]
-    except Exception:
-        tr["coeff_bits"] = 16
-    # the paired-row PNG kernel reads the band slab (png_slab.cpp): 1 KiB
-    # contiguous per load instruction, the streaming shape the x2 is
-    # calibrated on (tools/ubench/png_load_pattern mode 2 reads that shape)
-    if "png_pair" in out:
-        p = out["png_pair"]
-        tr["png"] = {"kernel": "png_pair_kernel<TC8>", "images": tr["images"], "size": tr["size"],
-                     "fetch_bytes_per_launch": 2 * p["FETCH_SIZE"] * 1024,
-                     "write_bytes_per_launch": p["WRITE_SIZE"] * 1024,
-                     "note": "FETCH_SIZE x2 (slab loads: 1 KiB contiguous per instruction) + WRITE_SIZE, "
-                             "KiB -> B, mean per dispatch"}
-        tr["png"]["hbm_bytes_per_launch"] = tr["png"]["fetch_bytes_per_launch"] + tr["png"]["write_bytes_per_launch"]
-    if "png_pair_d15" in out and "png_pair_d15_merge" in out:
-        a, b = out["png_pair_d15"], out["png_pair_d15_merge"]
-        tr["adam7_rgba16"] = {
-            "kernel": "png_pair_kernel<TCA16> x2 (passes 1-5 to staging; passes 6-7 merging it)",
-            "images": tr["images"], "size": tr["size"],
-            "fetch_bytes_per_launch": 2 * (a["FETCH_SIZE"] + b["FETCH_SIZE"]) * 1024,
-            "write_bytes_per_launch": (a["WRITE_SIZE"] + b["WRITE_SIZE"]) * 1024,
-            "note": "both launches of one plan launch; FETCH_SIZE x2 (slab loads 1 KiB contiguous per "
-                    "instruction; pass 6's staging reads 64 B contiguous per 8 lanes) + WRITE_SIZE"}
-        t = tr["adam7_rgba16"]
-        t["hbm_bytes_per_launch"] = t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"]
-    if "png_unfilter" in out:
-        p = out["png_unfilter"]
-        tr["png_unfilter"] = {"fetch_bytes_per_launch": 2 * p["FETCH_SIZE"] * 1024,
-                              "write_bytes_per_launch": p["WRITE_SIZE"] * 1024}
-    json.dump(tr, open(sys.argv[2], "w"), indent=1)
+
+def short_name(name):
+    for pat, key in KEYS:
+        m = re.search(pat, name)
+        if m:
+            if key is None:
+                return "jpeg_block<" + m.group(1).replace(" ", "") + ">"
+            g = m.groups()
+            if key.startswith("png_pair"):
+                return "png_pair_d{}{}".format(g[0], "_merge" if g[2] == "true" else "")
+            return key.format(*g)
+    return None
+
+
+def summarise(base):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for p in sorted(os.listdir(base)):
+        f = os.path.join(base, p, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            short = short_name(r["Kernel_Name"])
+            if short:
+                acc[short][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
+    out = {}
+    for k, d in acc.items():
+        per = collections.defaultdict(list)
+        for (cn, _), vals in d.items():
+            per[cn].append(sum(vals))
+        out[k] = {cn: sum(v) / len(v) for cn, v in per.items()}
+        out[k]["dispatches"] = max(len(v) for v in per.values())
+    return out
+
+
+def hbm(out, *keys):
+    if not all(k in out and "FETCH_SIZE" in out[k] and "WRITE_SIZE" in out[k] for k in keys):
+        return None
+    f = sum(2 * out[k]["FETCH_SIZE"] * 1024 for k in keys)
+    w = sum(out[k]["WRITE_SIZE"] * 1024 for k in keys)
+    return {"fetch_bytes_per_launch": f, "write_bytes_per_launch": w, "hbm_bytes_per_launch": f + w,
+            "kernels": list(keys)}
+
+
+# bench.py line -> the kernels one launch of its plan runs
+LINES = {
+    "headline": ("jpeg_block",),
+    "int16": ("jpeg_block_i16",),
+    "progressive_444": ("jpeg_block_444_i8",),
+    "planar_int8": ("jpeg_plane_block_i8",),
+    "planar_int16": ("jpeg_plane_block_i16",),
+    "png": ("png_pair_d6",),
+    "png_slab_build": ("png_slab_cb12",),
+    "adam7_rgba16": ("png_pair_d15", "png_pair_d15_merge"),
+    "rgba_pixels_nrgba64": ("rgba_pixels",),
+}
+
+if __name__ == "__main__":
+    base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    out = summarise(base)
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 2:
+        images = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+        size = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
+        tr = {"images": images, "size": size,
+              "note": "rocprofv3 --pmc, one pass per counter set: FETCH_SIZE x2 (gfx950 correction) + "
+                      "WRITE_SIZE, KiB -> B, mean per dispatch, summed over the kernels of one plan launch"}
+        for line, keys in LINES.items():
+            t = hbm(out, *keys)
+            if t:
+                tr[line] = t
+        json.dump(tr, open(sys.argv[2], "w"), indent=1)

@@ -119,6 +119,95 @@ __global__ __launch_bounds__(256) void rgba_pixels_kernel(DevImage m, uint8_t *_
     }
 }
 
+// The same for a batch of images of one kind (zpx_rgba_plan_create): a
+// workgroup converts 1,024 pixels of one row of one image (grid z), and for
+// the packed kinds each lane reads its 4 pixels as whole 4-32-byte pieces
+// (consecutive lanes on consecutive pieces: whole lines per instruction)
+// instead of byte by byte through the per-pixel switch; a row's last,
+// partial piece and the YCbCr / Paletted kinds take pixel_rgba8.
+template <int KIND>
+__device__ __forceinline__ uint4 rgba4_packed(const uint8_t *row, int x0)
+{
+    if constexpr (KIND == ZPX_NRGBA64 || KIND == ZPX_RGBA64) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(row + 8 * x0);
+        const uint4 b = *reinterpret_cast<const uint4 *>(row + 8 * x0 + 16);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t lo = w[2 * i], hi = w[2 * i + 1]; // bytes r0 r1 g0 g1 | b0 b1 a0 a1 (big endian)
+            if constexpr (KIND == ZPX_RGBA64) {
+                o[i] = pack4(lo & 0xff, (lo >> 16) & 0xff, hi & 0xff, (hi >> 16) & 0xff);
+            } else { // color.zig:73-89: c*a/0xffff, then >>8
+                const uint32_t r = (lo & 0xff) << 8 | ((lo >> 8) & 0xff), g = ((lo >> 16) & 0xff) << 8 | (lo >> 24);
+                const uint32_t bl = (hi & 0xff) << 8 | ((hi >> 8) & 0xff), al = ((hi >> 16) & 0xff) << 8 | (hi >> 24);
+                o[i] = pack4((r * al / 0xffffu) >> 8, (g * al / 0xffffu) >> 8, (bl * al / 0xffffu) >> 8, al >> 8);
+            }
+        }
+        return make_uint4(o[0], o[1], o[2], o[3]);
+    } else if constexpr (KIND == ZPX_RGBA || KIND == ZPX_NRGBA || KIND == ZPX_CMYK) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(row + 4 * x0);
+        if constexpr (KIND == ZPX_RGBA) return a;
+        const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t c0 = w[i] & 0xff, c1 = (w[i] >> 8) & 0xff, c2 = (w[i] >> 16) & 0xff, c3 = w[i] >> 24;
+            if constexpr (KIND == ZPX_NRGBA) {
+                o[i] = nrgba_rgba8(c0, c1, c2, c3);
+            } else { // color.zig:115-121
+                const uint32_t k = 0xffffu - c3 * 0x101u;
+                o[i] = pack4(((0xffffu - c0 * 0x101u) * k / 0xffffu) >> 8, ((0xffffu - c1 * 0x101u) * k / 0xffffu) >> 8,
+                             ((0xffffu - c2 * 0x101u) * k / 0xffffu) >> 8, 255);
+            }
+        }
+        return make_uint4(o[0], o[1], o[2], o[3]);
+    } else if constexpr (KIND == ZPX_GRAY16) {
+        const uint2 a = *reinterpret_cast<const uint2 *>(row + 2 * x0);
+        const uint32_t v[4] = {a.x & 0xff, (a.x >> 16) & 0xff, a.y & 0xff, (a.y >> 16) & 0xff}; // the BE high bytes
+        return make_uint4(v[0] * 0x010101u | 0xff000000u, v[1] * 0x010101u | 0xff000000u,
+                          v[2] * 0x010101u | 0xff000000u, v[3] * 0x010101u | 0xff000000u);
+    } else { // ZPX_GRAY
+        const uint32_t a = *reinterpret_cast<const uint32_t *>(row + x0);
+        return make_uint4((a & 0xff) * 0x010101u | 0xff000000u, ((a >> 8) & 0xff) * 0x010101u | 0xff000000u,
+                          ((a >> 16) & 0xff) * 0x010101u | 0xff000000u, (a >> 24) * 0x010101u | 0xff000000u);
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ void rgba_job_pixels(const DevRgbaJob &j)
+{
+    const DevImage &m = j.m;
+    const int y = blockIdx.y;
+    if (y >= m.height) return;
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (x0 >= m.width) return;
+    uint8_t *o = j.out + (static_cast<size_t>(y) * m.width + x0) * 4;
+    constexpr bool kPacked = KIND != ZPX_YCBCR && KIND != ZPX_PALETTED;
+    if (kPacked && x0 + 4 <= m.width && j.vec) {
+        *reinterpret_cast<uint4 *>(o) = rgba4_packed<KIND>(m.pixels + static_cast<size_t>(y) * m.stride, x0);
+        return;
+    }
+    uint32_t p[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) p[i] = x0 + i < m.width ? pixel_rgba8(m, x0 + i, y) : 0;
+    if (x0 + 4 <= m.width && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+        *reinterpret_cast<uint4 *>(o) = make_uint4(p[0], p[1], p[2], p[3]);
+    } else {
+        for (int i = 0; i < 4 && x0 + i < m.width; i++) reinterpret_cast<uint32_t *>(o)[i] = p[i];
+    }
+}
+template <int KIND>
+__global__ __launch_bounds__(256) void rgba_batch_kernel(const DevRgbaJob *__restrict__ jobs)
+{
+    rgba_job_pixels<KIND>(jobs[blockIdx.z]);
+}
+template <int KIND>
+__global__ __launch_bounds__(256) void rgba_one_kernel(DevRgbaJob j)
+{
+    rgba_job_pixels<KIND>(j);
+}
+
 // convertToRGB: R = Y, G = Cb, B = Cr with c_scale horizontal and cOffset
 // vertical indexing, A = 255.
 __global__ __launch_bounds__(256) void jpeg_rgb_kernel(DevImage m, int c_scale, uint8_t *__restrict__ out)
@@ -164,11 +253,43 @@ __global__ __launch_bounds__(256) void jpeg_cmyk_kernel(DevImage m, const uint8_
 
 } // namespace
 
+DevRgbaJob rgba_job(const DevImage &m, uint8_t *out)
+{
+    DevRgbaJob j{};
+    j.m = m;
+    j.out = out;
+    j.vec = (reinterpret_cast<uintptr_t>(m.pixels) & 15) == 0 && (m.stride & 15) == 0 &&
+            (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (m.width & 3) == 0;
+    return j;
+}
+
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s)
 {
     if (m.width <= 0 || m.height <= 0) return 0;
     dim3 grid((m.width + 1023) / 1024, m.height);
-    hipLaunchKernelGGL(rgba_pixels_kernel, grid, dim3(256), 0, s, m, out);
+    const DevRgbaJob j = rgba_job(m, out);
+    switch (m.kind) {
+#define ZPX_CASE(K) case K: hipLaunchKernelGGL(rgba_one_kernel<K>, grid, dim3(256), 0, s, j); break;
+        ZPX_CASE(ZPX_GRAY) ZPX_CASE(ZPX_GRAY16) ZPX_CASE(ZPX_YCBCR) ZPX_CASE(ZPX_RGBA) ZPX_CASE(ZPX_RGBA64)
+        ZPX_CASE(ZPX_NRGBA) ZPX_CASE(ZPX_NRGBA64) ZPX_CASE(ZPX_CMYK) ZPX_CASE(ZPX_PALETTED)
+#undef ZPX_CASE
+    default: hipLaunchKernelGGL(rgba_pixels_kernel, grid, dim3(256), 0, s, m, out); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_rgba_batch(int kind, const DevRgbaJob *jobs, int n, int max_w, int max_h, hipStream_t s)
+{
+    if (n <= 0 || max_w <= 0 || max_h <= 0) return 0;
+    if (n > 65535 || max_h > 65535) return -2;
+    const dim3 grid((max_w + 1023) / 1024, max_h, n);
+    switch (kind) {
+#define ZPX_CASE(K) case K: hipLaunchKernelGGL(rgba_batch_kernel<K>, grid, dim3(256), 0, s, jobs); break;
+        ZPX_CASE(ZPX_GRAY) ZPX_CASE(ZPX_GRAY16) ZPX_CASE(ZPX_YCBCR) ZPX_CASE(ZPX_RGBA) ZPX_CASE(ZPX_RGBA64)
+        ZPX_CASE(ZPX_NRGBA) ZPX_CASE(ZPX_NRGBA64) ZPX_CASE(ZPX_CMYK) ZPX_CASE(ZPX_PALETTED)
+#undef ZPX_CASE
+    default: return -2;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -102,4 +102,12 @@ struct DevImage {
     int32_t kind, subsample, width, height, palette_len, pad;
 };
 
+// One image of a batched Image.rgbaPixels (zpx_rgba_plan_create).
+struct DevRgbaJob {
+    DevImage m;
+    uint8_t *out;  // RGBA8, stride 4 * width
+    int32_t vec;   // rows and out 16-byte aligned: whole 4-pixel pieces load and store as vectors
+    int32_t pad;
+};
+
 } // namespace zpx

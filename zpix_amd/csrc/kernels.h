@@ -68,6 +68,10 @@ int launch_png_pair_merge(int depth, bool trns, const DevPngPass *passes, const 
 int launch_png_slab(int cb, const DevSlabBand *jobs, uint32_t njobs, uint32_t max_groups, hipStream_t s);
 
 int launch_rgba_pixels(const DevImage &m, uint8_t *out, hipStream_t s);
+// the batched form's job for one image (vec: the aligned vector path applies)
+DevRgbaJob rgba_job(const DevImage &m, uint8_t *out);
+// Image.rgbaPixels of n images of one kind (grid z = image; rows up to max_h)
+int launch_rgba_batch(int kind, const DevRgbaJob *jobs, int n, int max_w, int max_h, hipStream_t s);
 int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s);
 int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,
                      uint8_t *out, hipStream_t s);

@@ -4,7 +4,9 @@
 // (src/png/decoder.zig:516-523).  So the host hands over the stream as
 // inflate produced it and keeps no transposition work.
 //
-// A workgroup takes 16 rows of one band and 16 groups (128 chunks) of them:
+// A workgroup takes 16 rows of one band and walks their groups, 16 groups
+// (128 chunks) a window, the next window's loads in flight during the
+// current one's stores:
 //   1. the band's 128 filter bytes -> the skew of every row (the kernel's
 //      rule: row r minus the last row <= r that restarts the chain: a None /
 //      Sub row, a row past the pass, or the band's first) and the band's
@@ -31,7 +33,7 @@ namespace {
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kRows = 16;   // rows per workgroup
-constexpr int kGroups = 16; // groups (8 chunks each) per workgroup
+constexpr int kGroups = 16; // groups (8 chunks each) per window
 constexpr int kOOR = 0x7ffffff0;
 
 template <int CB>
@@ -39,19 +41,22 @@ __global__ __launch_bounds__(256) void png_slab_kernel(const DevSlabBand *__rest
 {
     constexpr int NQ = CB / 2;                  // 16-byte pieces per row and group (8 CB / 16)
     constexpr int WIN = kGroups * 8 * CB;       // window bytes per row
-    constexpr int NDW = WIN / 4 + 1;            // dwords loaded per row (+1: the window's misalignment)
-    __shared__ uint32_t tile[kRows * NDW];
+    constexpr int NC = WIN / 16 + 1;            // 16-byte chunks loaded per row (+1: the window's misalignment)
+    constexpr int RS = NC * 4 + 1;              // LDS dwords per row (odd: row starts spread over the banks)
+    constexpr int NLD = (kRows * NC + 255) / 256; // chunk loads per thread per window
+    constexpr int NPIECE = kGroups * 2 * NQ * 8;  // output pieces per window
+    static_assert(NPIECE % 256 == 0, "whole output rounds");
+    __shared__ uint32_t tile[kRows * RS];
     __shared__ uint8_t ft[128];
     __shared__ int32_t skew[128];
     __shared__ int32_t max_skew;
     const int tid = threadIdx.x;
     const int band = static_cast<int>(blockIdx.x) >> 3, R0 = (static_cast<int>(blockIdx.x) & 7) * kRows;
-    const int range = static_cast<int>(blockIdx.y);
     typedef const __attribute__((address_space(4))) DevSlabBand *CJob;
     const auto &j = *(reinterpret_cast<CJob>(reinterpret_cast<uintptr_t>(jobs)) + band);
     const uint32_t rows = j.rows, rb = j.rb, rstride = rb + 1;
     const uintptr_t r0a = reinterpret_cast<uintptr_t>(j.rows0);
-    const uint32_t delta = static_cast<uint32_t>(r0a & 3u);
+    const uint32_t delta = static_cast<uint32_t>(r0a & 15u);
     const auto src = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(r0a - delta), 0,
                                                        static_cast<int>(j.avail + delta), 0x00020000);
     // 1. filter bytes and skews (png_slab.cpp band_skews; png_pair_kernel)
@@ -69,59 +74,80 @@ __global__ __launch_bounds__(256) void png_slab_kernel(const DevSlabBand *__rest
     }
     __syncthreads();
     const int ngroups = (static_cast<int>(j.nchunks) + max_skew + 7) / 8;
-    const int g0 = range * kGroups;
-    if (g0 >= ngroups) return; // (uniform: past the band's groups)
-    if (range == 0 && R0 == 0 && tid < 32)
+    if (R0 == 0 && tid < 32)
         reinterpret_cast<uint32_t *>(j.region)[tid] = reinterpret_cast<const uint32_t *>(ft)[tid];
-    // 2. the rows' windows into LDS: consecutive threads on consecutive
-    // dwords of one row
-    for (int idx = tid; idx < kRows * NDW; idx += 256) {
-        const int rl = idx / NDW, d = idx - rl * NDW;
-        const int r = R0 + rl;
-        const int x0 = (8 * g0 - skew[r]) * CB; // the window's first byte in the row (>= -skew * CB)
-        // (>= 1: a row holds at least CB - 1 bytes, png_pair_supported, so
-        // r (rb + 1) + 1 >= skew * CB)
-        const uint32_t a = static_cast<uint32_t>(r) * rstride + 1u + static_cast<uint32_t>(x0) + delta;
-        const int o = static_cast<uint32_t>(r) < rows ? static_cast<int>((a & ~3u) + 4u * static_cast<uint32_t>(d)) : kOOR;
-        tile[idx] = __builtin_amdgcn_raw_buffer_load_b32(src, o, 0, 0);
-    }
-    __syncthreads();
-    // 3. the pieces, eight lanes per 128-byte line of the slab
-    constexpr int NPIECE = kGroups * 2 * NQ * 8;
+    // a row's window of groups g0 .. g0 + 15 starts at its chunk 8 g0 - skew:
+    // byte a of the band (from the descriptor base), loaded from a & ~15
+    auto win_start = [&](int r, int g0) {
+        return static_cast<uint32_t>(r) * rstride + 1u + static_cast<uint32_t>((8 * g0 - skew[r]) * CB) + delta;
+    };
+    // 2. the windows' 16-byte chunks, consecutive threads on consecutive
+    // chunks of one row, into registers one window ahead
+    v4u ld[NLD];
+    auto load_window = [&](int g0) {
+#pragma unroll
+        for (int k = 0; k < NLD; k++) {
+            const int idx = tid + 256 * k;
+            const int rl = idx / NC, c = idx - rl * NC;
+            const int r = R0 + rl;
+            const bool in = idx < kRows * NC && static_cast<uint32_t>(r) < rows && 8 * g0 < ngroups * 8;
+            const int o = in ? static_cast<int>((win_start(r, g0) & ~15u) + 16u * static_cast<uint32_t>(c)) : kOOR;
+            ld[k] = __builtin_amdgcn_raw_buffer_load_b128(src, o, 0, 0);
+        }
+    };
     uint8_t *const groups = j.region + 128;
-#pragma unroll 2
-    for (int idx = tid; idx < NPIECE; idx += 256) {
-        const int l = idx & 7, rest = idx >> 3;
-        const int q = rest % NQ, gh = rest / NQ, h = gh & 1, gl = gh >> 1;
-        const int g = g0 + gl;
-        if (g >= ngroups) continue;
-        const int rl = 2 * l + h, r = R0 + rl;
-        v4u v = v4u{0, 0, 0, 0};
-        if (static_cast<uint32_t>(r) < rows) {
-            const int sk = skew[r];
-            const uint32_t a = static_cast<uint32_t>(r) * rstride + 1u + static_cast<uint32_t>((8 * g0 - sk) * CB) + delta;
-            const uint32_t local = (a & 3u) + static_cast<uint32_t>(8 * gl * CB + 16 * q);
-            const uint32_t *t = tile + rl * NDW + (local >> 2);
-            const uint32_t sh = local & 3u;
-            const uint32_t w0 = t[0], w1 = t[1], w2 = t[2], w3 = t[3], w4 = t[4];
-            v = v4u{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
-            const int p = (8 * g - sk) * CB + 16 * q; // the piece's first byte in the row
-            if (p < 0 || p + 16 > static_cast<int>(rb)) { // a row edge: zeros outside [0, rb)
+    load_window(0);
+    for (int g0 = 0; g0 < ngroups; g0 += kGroups) {
+        __syncthreads(); // the previous window's pieces are out of the tile
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    uint32_t m = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; b++) {
-                        const int x = p + 4 * e + b;
-                        m |= (x >= 0 && x < static_cast<int>(rb)) ? 0xffu << (8 * b) : 0u;
-                    }
-                    v[e] &= m;
-                }
+        for (int k = 0; k < NLD; k++) {
+            const int idx = tid + 256 * k;
+            if (idx < kRows * NC) {
+                const int rl = idx / NC, c = idx - rl * NC;
+                uint32_t *t = tile + rl * RS + 4 * c;
+                t[0] = ld[k][0];
+                t[1] = ld[k][1];
+                t[2] = ld[k][2];
+                t[3] = ld[k][3];
             }
         }
-        const int lane = (R0 >> 1) + l;
-        *reinterpret_cast<v4u *>(groups + (static_cast<size_t>(2 * g + h) * NQ + q) * 1024 + lane * 16) = v;
+        __syncthreads();
+        if (g0 + kGroups < ngroups) load_window(g0 + kGroups); // (in flight during the pieces below)
+        // 3. the pieces, eight lanes per 128-byte line of the slab
+#pragma unroll
+        for (int k = 0; k < NPIECE / 256; k++) {
+            const int idx = tid + 256 * k;
+            const int l = idx & 7, rest = idx >> 3;
+            const int q = rest % NQ, gh = rest / NQ, h = gh & 1, gl = gh >> 1;
+            const int g = g0 + gl;
+            const int rl = 2 * l + h, r = R0 + rl;
+            v4u v = v4u{0, 0, 0, 0};
+            if (static_cast<uint32_t>(r) < rows) {
+                const uint32_t local = (win_start(r, g0) & 15u) + static_cast<uint32_t>(8 * gl * CB + 16 * q);
+                const uint32_t *t = tile + rl * RS + (local >> 2);
+                const uint32_t sh = local & 3u;
+                const uint32_t w0 = t[0], w1 = t[1], w2 = t[2], w3 = t[3], w4 = t[4];
+                v = v4u{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                        __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+                const int p = (8 * g - skew[r]) * CB + 16 * q; // the piece's first byte in the row
+                if (p < 0 || p + 16 > static_cast<int>(rb)) { // a row edge: zeros outside [0, rb)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        uint32_t m = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            const int x = p + 4 * e + b;
+                            m |= (x >= 0 && x < static_cast<int>(rb)) ? 0xffu << (8 * b) : 0u;
+                        }
+                        v[e] &= m;
+                    }
+                }
+            }
+            if (g < ngroups) {
+                const int lane = (R0 >> 1) + l;
+                *reinterpret_cast<v4u *>(groups + (static_cast<size_t>(2 * g + h) * NQ + q) * 1024 + lane * 16) = v;
+            }
+        }
     }
 }
 
@@ -130,7 +156,8 @@ __global__ __launch_bounds__(256) void png_slab_kernel(const DevSlabBand *__rest
 int launch_png_slab(int cb, const DevSlabBand *jobs, uint32_t njobs, uint32_t max_groups, hipStream_t s)
 {
     if (njobs == 0) return 0;
-    const dim3 grid(njobs * 8, (max_groups + kGroups - 1) / kGroups);
+    (void)max_groups; // (each workgroup walks its band's groups)
+    const dim3 grid(njobs * 8);
     if (cb == 12) hipLaunchKernelGGL(png_slab_kernel<12>, grid, dim3(256), 0, s, jobs);
     else if (cb == 16) hipLaunchKernelGGL(png_slab_kernel<16>, grid, dim3(256), 0, s, jobs);
     else return -2;

@@ -340,9 +340,15 @@ struct PngGroup {
     size_t scratch_zero_bytes = 0;
 };
 
+struct RgbaGroup {
+    int kind = 0, n = 0, max_w = 0, max_h = 0;
+    DevBuf jobs; // DevRgbaJob per image
+};
+
 struct zpx_plan {
     zpx_ctx *ctx = nullptr;
-    int kind = 0; // 0 jpeg planes, 1 jpeg rgba, 2 png
+    int kind = 0; // 0 jpeg planes, 1 jpeg rgba, 2 png, 3 rgbaPixels
+    std::vector<std::unique_ptr<RgbaGroup>> rgba;
     std::vector<std::unique_ptr<JpegGroup>> jpeg;
     std::vector<std::unique_ptr<PngGroup>> png;
     HostBuf status_host; // pinned: per PNG group {status, sticky status}
@@ -638,12 +644,72 @@ extern "C" int zpx_png_plan_create(zpx_ctx *ctx, const zpx_png_frame *frames, in
     return guarded([&] { return zpx_png_plan_create_impl(ctx, frames, n_frames, out); });
 }
 
+// Image.rgbaPixels (image.zig:103-130) over a batch of device-resident
+// images: one launch per image kind.
+static int zpx_rgba_plan_create_impl(zpx_ctx *ctx, const zpx_image *imgs, uint8_t *const *outs, int n,
+                                     zpx_plan **out)
+{
+    if (!ctx || !imgs || !outs || n <= 0 || !out) return ZPX_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    CtxScope s(ctx);
+    std::unique_ptr<zpx_plan> plan(new zpx_plan);
+    plan->ctx = ctx;
+    plan->kind = 3;
+    std::map<int, std::vector<DevRgbaJob>> by_kind;
+    uint64_t bytes = 0;
+    for (int i = 0; i < n; i++) {
+        const zpx_image &im = imgs[i];
+        if (im.min_x != 0 || im.min_y != 0) return ZPX_E_UNSUPPORTED;
+        if (im.kind < ZPX_GRAY || im.kind > ZPX_PALETTED || !outs[i] || !im.pixels) return ZPX_E_INVALID_ARGUMENT;
+        const uint64_t w = uint64_t(im.max_x), h = uint64_t(im.max_y);
+        if (w > 65535u * 1024u || h > 65535) return ZPX_E_UNSUPPORTED;
+        by_kind[im.kind].push_back(rgba_job(dev_image_of(&im, im.pixels, im.palette), outs[i]));
+        // algorithmic bytes: the pixels the kind reads, then RGBA8
+        static const int kBpp[9] = {1, 2, 0, 4, 8, 4, 8, 4, 1}; // zpx_kind order
+        uint64_t in = w * h * uint64_t(kBpp[im.kind]);
+        if (im.kind == ZPX_YCBCR) {
+            const uint64_t cw = (im.subsample == ZPX_RATIO444 || im.subsample == ZPX_RATIO440) ? w
+                                : (im.subsample == ZPX_RATIO411 || im.subsample == ZPX_RATIO410) ? (w + 3) / 4 : (w + 1) / 2;
+            const uint64_t ch = (im.subsample == ZPX_RATIO420 || im.subsample == ZPX_RATIO440 ||
+                                 im.subsample == ZPX_RATIO410) ? (h + 1) / 2 : h;
+            in = w * h + 2 * cw * ch;
+        }
+        bytes += in + w * h * 4;
+    }
+    for (auto &kv : by_kind) {
+        if (kv.second.size() > 65535) return ZPX_E_UNSUPPORTED;
+        std::unique_ptr<RgbaGroup> g(new RgbaGroup);
+        g->kind = kv.first;
+        g->n = static_cast<int>(kv.second.size());
+        for (const DevRgbaJob &j : kv.second) {
+            g->max_w = std::max(g->max_w, j.m.width);
+            g->max_h = std::max(g->max_h, j.m.height);
+        }
+        HIPCHK(ctx, g->jobs.alloc(kv.second.size() * sizeof(DevRgbaJob)));
+        HIPCHK(ctx, hipMemcpy(g->jobs.ptr, kv.second.data(), kv.second.size() * sizeof(DevRgbaJob),
+                              hipMemcpyHostToDevice));
+        plan->rgba.push_back(std::move(g));
+    }
+    plan->bytes = bytes;
+    *out = plan.release();
+    return ZPX_OK;
+}
+
+extern "C" int zpx_rgba_plan_create(zpx_ctx *ctx, const zpx_image *imgs, uint8_t *const *outs, int n,
+                                    zpx_plan **out)
+{
+    return guarded([&] { return zpx_rgba_plan_create_impl(ctx, imgs, outs, n, out); });
+}
+
 extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
 {
     if (!plan) return ZPX_E_INVALID_ARGUMENT;
     zpx_ctx *ctx = plan->ctx;
     CtxScope s(ctx);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    for (auto &g : plan->rgba)
+        if (launch_rgba_batch(g->kind, g->jobs.as<DevRgbaJob>(), g->n, g->max_w, g->max_h, st))
+            return hip_fail(ctx, hipGetLastError(), "rgba batch kernel launch");
     for (auto &g : plan->jpeg) {
         int rc;
         if (plan->kind == 0)
@@ -715,7 +781,7 @@ extern "C" int zpx_plan_status(zpx_plan *plan, void *stream)
 extern "C" uint64_t zpx_plan_bytes(const zpx_plan *plan) { return plan ? plan->bytes : 0; }
 extern "C" int zpx_plan_kernel_count(const zpx_plan *plan)
 {
-    return plan ? static_cast<int>(plan->jpeg.size() + plan->png.size()) : 0;
+    return plan ? static_cast<int>(plan->jpeg.size() + plan->png.size() + plan->rgba.size()) : 0;
 }
 extern "C" void zpx_plan_destroy(zpx_plan *plan)
 {

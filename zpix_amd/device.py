@@ -236,3 +236,62 @@ class PngBatch:
         f = self.frames[slot]
         o = self.out_offsets[slot]
         return self.out_arena[o:o + f.out_stride * f.height]
+
+
+class RgbaBatch:
+    """Image.rgbaPixels (image.zig:103-130) of a batch of images resident in
+    HBM, as one plan (zpx_rgba_plan_create): `items` are host `Image`s,
+    uploaded once; `slots[i]` picks the item of device slot i; launch()
+    converts every slot to RGBA8 (stride 4 * width) in HBM."""
+
+    def __init__(self, items, slots: list[int] | None = None, device: int = 0,
+                 ctx: context.Context | None = None):
+        torch = _torch()
+        self.ctx = ctx or context.default(device)
+        self.device = torch.device("cuda", self.ctx.device)
+        self.items = items
+        self.slots = list(range(len(items))) if slots is None else list(slots)
+        in_sizes = [_align(np.asarray(items[i].pixels).size) + _align(256 * C.sizeof(_lib.zpx_color))
+                    for i in self.slots]
+        out_sizes = [_align(items[i].width * items[i].height * 4) for i in self.slots]
+        self.in_arena = torch.empty(max(sum(in_sizes), 1), dtype=torch.uint8, device=self.device)
+        self.out_arena = torch.zeros(max(sum(out_sizes), 1), dtype=torch.uint8, device=self.device)
+        imgs = (_lib.zpx_image * len(self.slots))()
+        outs = (C.c_void_p * len(self.slots))()
+        oi = oo = 0
+        self.out_offsets = []
+        for s, i in enumerate(self.slots):
+            img = items[i]
+            raw = img._to_c()  # (its palette pointer lives until the next _to_c of this item)
+            px = np.ascontiguousarray(img.pixels, np.uint8)
+            self.in_arena[oi:oi + px.size].copy_(torch.from_numpy(px))
+            imgs[s] = raw
+            imgs[s].pixels = C.cast(C.c_void_p(self.in_arena.data_ptr() + oi), C.POINTER(C.c_uint8))
+            if img.kind == "Paletted" and raw.palette:
+                pal = np.ctypeslib.as_array(C.cast(raw.palette, C.POINTER(C.c_uint8)),
+                                            shape=(256 * C.sizeof(_lib.zpx_color),)).copy()
+                po = oi + _align(px.size)
+                self.in_arena[po:po + pal.size].copy_(torch.from_numpy(pal))
+                imgs[s].palette = C.cast(C.c_void_p(self.in_arena.data_ptr() + po), C.POINTER(_lib.zpx_color))
+            outs[s] = self.out_arena.data_ptr() + oo
+            self.out_offsets.append(oo)
+            oi += in_sizes[s]
+            oo += out_sizes[s]
+        torch.cuda.synchronize(self.device)
+        h = C.c_void_p()
+        _lib.check(_lib.lib().zpx_rgba_plan_create(self.ctx.handle, imgs, outs, len(self.slots), C.byref(h)),
+                   self.ctx.handle)
+        self.plan = _Plan(h, self.ctx)
+        self.pixels = sum(items[i].width * items[i].height for i in self.slots)
+
+    @property
+    def bytes(self) -> int:
+        return self.plan.bytes
+
+    def launch(self, stream: int | None = None) -> None:
+        self.plan.launch(stream)
+
+    def output_tensor(self, slot: int):
+        img = self.items[self.slots[slot]]
+        o = self.out_offsets[slot]
+        return self.out_arena[o:o + img.width * img.height * 4].view(img.height, img.width, 4)
