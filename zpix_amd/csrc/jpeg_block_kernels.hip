@@ -8,6 +8,7 @@
 // width -- and the strip kernel (jpeg_kernels.hip) the rest.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <type_traits>
@@ -751,7 +752,17 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 // at a task's start the only operations issued after its DMA are the
 // previous task's 8 stores.
 // ---------------------------------------------------------------------------
-constexpr int kPlaneWavesPerEu = 4; // <= 128 VGPRs: 16 waves per CU
+#ifndef ZPX_PLANE_WPE
+#define ZPX_PLANE_WPE 4
+#endif
+#ifndef ZPX_PLANE_DMA_NT
+#define ZPX_PLANE_DMA_NT 1
+#endif
+#ifndef ZPX_PLANE_ST
+#define ZPX_PLANE_ST 2
+#endif
+constexpr int kPlaneWavesPerEu = ZPX_PLANE_WPE; // <= 128 VGPRs: 16 waves per CU
+constexpr int kPlaneStoreAux = ZPX_PLANE_ST;
 
 template <typename CoefT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kPlaneWavesPerEu)))
@@ -811,7 +822,7 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
         for (int i = 0; i < I::P; i++) {
             const int bx = min(k.bx0 + I::B * i + lane % I::B, last);
             const int q = (lane / I::B + I::P - (I::P == 8 ? i : 0)) % I::P;
-            glds16<true>(row + static_cast<uint32_t>(bx * BYTES + 16 * q), cimg + 1024 * i);
+            glds16<ZPX_PLANE_DMA_NT != 0>(row + static_cast<uint32_t>(bx * BYTES + 16 * q), cimg + 1024 * i);
         }
     };
     int task;
@@ -829,7 +840,7 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
     // fewer, wider stores -- which would let vmcnt(8) pass before the DMA)
     const auto none = __builtin_amdgcn_make_buffer_rsrc(const_cast<DevJpegFrame *>(frames), 0, 0, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, none, 4096 * i, 0, kStoreAux);
+    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, none, 4096 * i, 0, kPlaneStoreAux);
     constexpr uint32_t kDrop = 0x80000000u;
     for (;;) {
         const int tn = task + tstride;
@@ -860,7 +871,7 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const u32x2 v{pack4(s + 8 * r) ^ kBias4, pack4(s + 8 * r + 4) ^ kBias4};
-            __builtin_amdgcn_raw_buffer_store_b64(v, prsrc, live ? o0 + r * k.stride : kDrop, 0, kStoreAux);
+            __builtin_amdgcn_raw_buffer_store_b64(v, prsrc, live ? o0 + r * k.stride : kDrop, 0, kPlaneStoreAux);
         }
         if (!more) break;
         task = tn;
@@ -950,7 +961,14 @@ int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const Jp
     auto kernel = coeff_bits == 8 ? jpeg_plane_block_kernel<int8_t> : jpeg_plane_block_kernel<int16_t>;
     static const int resident8 = resident_waves(jpeg_plane_block_kernel<int8_t>);
     static const int resident16 = resident_waves(jpeg_plane_block_kernel<int16_t>);
-    const int resident = coeff_bits == 8 ? resident8 : resident16;
+    // waves per CU: as many as fit for int8 (20: 8 / 12 / 16 ran 0.855 /
+    // 0.823 / 0.810 ms against 0.800 per 64 frames), 8 for int16 (0.952 /
+    // 0.972 / 0.988 ms at 8 / 12 / 16 against 0.990 at all 16 that fit;
+    // gpurun_out/plab2)
+#ifndef ZPX_PLANE_WPCU16
+#define ZPX_PLANE_WPCU16 8
+#endif
+    const int resident = coeff_bits == 8 ? resident8 : std::min(resident16, device_cu_count() * ZPX_PLANE_WPCU16);
     const int grid = total < resident ? static_cast<int>(total) : resident;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, geo);
     return hipGetLastError() == hipSuccess ? 0 : -1;
