@@ -572,26 +572,29 @@ class Decoder {
     int prog_set(int ci, size_t blk, int z, int32_t v)
     {
         const int i = kUnzig[z];
-        uint64_t *m = &(*nz_[ci])[blk];
         if (int16_t *g = fixed16_[ci]) { // parallel scan: int16 grid, no widening
             const int32_t a = v < 0 ? (v == INT32_MIN ? INT32_MAX : -v) : v;
             if (a > 32767) return kParallelAbort;
             job_max_[ci] = a > job_max_[ci] ? a : job_max_[ci];
+            if (z == 0) { // DC apart from the block (the DC scans run beside the AC scans)
+                dc16_[ci][blk] = static_cast<int16_t>(v);
+                return 0;
+            }
             g[blk * 64 + static_cast<size_t>(i)] = static_cast<int16_t>(v);
-            // (other bands of the block may be written concurrently)
-            if (v != 0 && !((__atomic_load_n(m, __ATOMIC_RELAXED) >> z) & 1))
-                __atomic_fetch_or(m, uint64_t(1) << z, __ATOMIC_RELAXED);
+            // (no two AC scans of one component run at once: run_deferred_scans)
+            if (v != 0) (*nz_[ci])[blk] |= uint64_t(1) << z;
             return 0;
         }
-        if (v != 0) *m |= uint64_t(1) << z;
+        if (v != 0 && z != 0) (*nz_[ci])[blk] |= uint64_t(1) << z;
         return o_.grid[ci].set(blk, i, v) ? 0 : ZPX_E_OUT_OF_MEMORY;
     }
     int32_t prog_get(int ci, size_t blk, int z) const
     {
-        if (const int16_t *g = fixed16_[ci]) return g[blk * 64 + static_cast<size_t>(kUnzig[z])];
+        if (const int16_t *g = fixed16_[ci])
+            return z == 0 ? dc16_[ci][blk] : g[blk * 64 + static_cast<size_t>(kUnzig[z])];
         return o_.grid[ci].get(blk, kUnzig[z]);
     }
-    uint64_t prog_mask(int ci, size_t blk) const { return __atomic_load_n(&(*nz_[ci])[blk], __ATOMIC_RELAXED); }
+    uint64_t prog_mask(int ci, size_t blk) const { return (*nz_[ci])[blk]; }
     // refine :1459-1518 / refineNonZeroes :1522-1549 of an AC band on the
     // grid itself, through the nonzero masks
     int prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta);
@@ -640,6 +643,7 @@ class Decoder {
     Scan job_scan_;
     size_t job_start_ = 0, job_skip_ = 0; // the scan's first byte; where the first pass resumed
     int16_t *fixed16_[4] = {nullptr, nullptr, nullptr, nullptr};
+    int16_t *dc16_[4] = {nullptr, nullptr, nullptr, nullptr}; // parallel scans: the DC coefficients, per block
     std::shared_ptr<std::vector<uint64_t>> nz_[4]; // progressive: per block, its nonzero coefficients (zig-zag bits)
     int32_t job_max_[4] = {0, 0, 0, 0};
     static constexpr int kParallelAbort = (1 << 20) + 1; // internal: a value past int16 in a parallel scan
@@ -1492,12 +1496,20 @@ int run_deferred_scans(std::vector<std::unique_ptr<Decoder>> &jobs, JpegCoeffs &
             bool common = false;
             for (int x = 0; x < a.ns; x++)
                 for (int y = 0; y < b.ns; y++) common |= a.c[x].id == b.c[y].id;
-            if (common && a.zs <= b.ze && b.zs <= a.ze) deps[j].push_back(i);
+            // overlapping bands; and any two AC scans of one component, which
+            // share its blocks' nonzero masks
+            if (common && ((a.zs <= b.ze && b.zs <= a.ze) || (a.zs > 0 && b.zs > 0))) deps[j].push_back(i);
         }
     }
+    std::vector<int16_t> dc[4]; // the DC coefficients, apart from the blocks until the scans are done
+    for (int c = 0; c < o.n_comp; c++)
+        if (o.has_grid[c]) dc[c].assign(o.grid[c].blocks(), 0);
     for (size_t j = 0; j < n; j++) {
         Decoder &d = *jobs[j];
-        for (int c = 0; c < o.n_comp; c++) d.fixed16_[c] = o.has_grid[c] ? o.grid[c].data16() : nullptr;
+        for (int c = 0; c < o.n_comp; c++) {
+            d.fixed16_[c] = o.has_grid[c] ? o.grid[c].data16() : nullptr;
+            d.dc16_[c] = o.has_grid[c] ? dc[c].data() : nullptr;
+        }
         for (int k = 0; k < d.job_scan_.ns; k++)
             if (!d.fixed16_[d.job_scan_.c[k].id]) return false;
     }
@@ -1575,6 +1587,9 @@ int run_deferred_scans(std::vector<std::unique_ptr<Decoder>> &jobs, JpegCoeffs &
         if (!o.has_grid[c]) continue;
         int32_t m = 0;
         for (auto &d : jobs) m = std::max(m, d->job_max_[c]);
+        int16_t *g = o.grid[c].data16();
+        const size_t nb = o.grid[c].blocks();
+        for (size_t b = 0; b < nb; b++) g[b * 64] = dc[c][b];
         o.grid[c].note_max_abs(m);
         if (!o.grid[c].narrow_to8(threads)) return false;
     }
