@@ -918,6 +918,15 @@ int block_geom(int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStrea
     case 0x2111: return launch_block_t<CoefT, 2, 1, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:2:2
     case 0x1211: return launch_block_t<CoefT, 1, 2, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:4:0
     case 0x1111: return launch_block_t<CoefT, 1, 1, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:4:4
+#ifndef ZPX_JPEGB_COMMON_ONLY
+    case 0x4111: return launch_block_t<CoefT, 4, 1, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:1:1
+    case 0x4211: return launch_block_t<CoefT, 4, 2, 1, 1, COLOR>(d, n, mxx, myy, s); // 4:1:0
+    case 0x2212: return launch_block_t<CoefT, 2, 2, 1, 2, COLOR>(d, n, mxx, myy, s); // 2x2 luma, 1x2 chroma
+    case 0x2221: return launch_block_t<CoefT, 2, 2, 2, 1, COLOR>(d, n, mxx, myy, s);
+    case 0x2222: return launch_block_t<CoefT, 2, 2, 2, 2, COLOR>(d, n, mxx, myy, s); // 4:4:4 in 2x2 MCUs
+    case 0x2121: return launch_block_t<CoefT, 2, 1, 2, 1, COLOR>(d, n, mxx, myy, s);
+    case 0x1212: return launch_block_t<CoefT, 1, 2, 1, 2, COLOR>(d, n, mxx, myy, s);
+#endif
     }
     return -2;
 }

@@ -337,7 +337,20 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
     constexpr int kSlots = 2 * FL;          // ring slots per row
     constexpr int RPR = 64 / FL;            // rows per flush round (FL lanes each)
     constexpr int NR = 128 / RPR;           // flush rounds
-    constexpr int RS = kSlots * 4 + 4;      // ring dwords per row: 2 FL output chunks of 16 bytes + 16 bytes of bank skew
+#ifndef ZPX_PNG_RING_SWZ
+#define ZPX_PNG_RING_SWZ 1
+#endif
+    // ring dwords per row: 2 FL output chunks of 16 bytes (+ 16 bytes of
+    // bank skew without the swizzle).  With ZPX_PNG_RING_SWZ rows start on
+    // bank 0 and the rows 2j, 2j+1 of odd lanes j keep chunk k in slot
+    // (k mod 16) xor 8: a flush read (ds_read_b128, 16-lane groups over 4
+    // rows x 4 chunks, banks mod 64) then meets 4 disjoint 16-dword bank
+    // sets, and the step's ring writes (ds_write_b128, 8-lane groups, banks
+    // mod 32) spread with the rows' skews instead of colliding along a chain
+    constexpr int RS = ZPX_PNG_RING_SWZ ? kSlots * 4 : kSlots * 4 + 4;
+    auto rslot = [](int k, int row) {
+        return ((k & (kSlots - 1)) ^ (ZPX_PNG_RING_SWZ ? 8 * ((row >> 1) & 1) : 0)) * 4;
+    };
     constexpr int WG = kG * CW;             // boundary granules of one window (kG chunks)
     static_assert(WG % 2 == 0 && WG / 2 <= 64, "window loads are granule pairs, one per lane");
     __shared__ __attribute__((aligned(16))) uint32_t ring[128 * RS + 4]; // + a trash slot
@@ -497,8 +510,8 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             if (xf1) {
                 fso[x0] = p0 ? static_cast<uint32_t>(r0) * static_cast<uint32_t>(orow_bytes) + fl0 * (FL * 16) : kOOR;
                 fso[x1] = p1 ? static_cast<uint32_t>(r1) * static_cast<uint32_t>(orow_bytes) + fl1 * (FL * 16) : kOOR;
-                fsr[x0] = 4 * ring0 + ((fl0 * FL) & (kSlots - 1)) * 16;
-                fsr[x1] = 4 * ring1 + ((fl1 * FL) & (kSlots - 1)) * 16;
+                fsr[x0] = 4 * (ring0 + rslot(fl0 * FL, r0));
+                fsr[x1] = 4 * (ring1 + rslot(fl1 * FL, r1));
             } else {
                 fst[x0] = p0 ? static_cast<uint32_t>(fl0) : 0xffffu;
                 fst[x1] = p1 ? static_cast<uint32_t>(fl1) : 0xffffu;
@@ -541,7 +554,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 const int r = RPR * i + lane / FL;
                 const bool post = blk[i] != 0xffffu;
                 const int k = static_cast<int>(post ? blk[i] : 0u) * FL + lane % FL;
-                const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + (k & (kSlots - 1)) * 4]);
+                const v4u v = *reinterpret_cast<const v4u *>(&ring[r * RS + rslot(k, r)]);
                 store(post, r * static_cast<int>(orow_bytes), k, v);
             };
             if (!merge) { // Adam7 passes 1-4 into Q: pixels xf (2 or 4) apart
@@ -677,9 +690,9 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 // (a chunk k < 0 lands in the slot of chunk k + 16, which
                 // overwrites it before any flush reads it; past the row's end
                 // the trash slot keeps its unflushed last chunks)
-                *reinterpret_cast<v4u *>(&ring[k0 < nchunks ? ring0 + (k0 & (kSlots - 1)) * 4 : kTrash]) =
+                *reinterpret_cast<v4u *>(&ring[k0 < nchunks ? ring0 + rslot(k0, 2 * lane) : kTrash]) =
                     expand_chunk<DEPTH, TRNS>(ps, plo);
-                *reinterpret_cast<v4u *>(&ring[k1 < nchunks ? ring1 + (k1 & (kSlots - 1)) * 4 : kTrash]) =
+                *reinterpret_cast<v4u *>(&ring[k1 < nchunks ? ring1 + rslot(k1, 2 * lane + 1) : kTrash]) =
                     expand_chunk<DEPTH, TRNS>(ps, phi);
                 const bool act1 = ok1 && k1 >= 0 && k1 < nchunks;
                 // ---- publish the band's last row (row 127: lane 63's high
@@ -732,7 +745,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                         const int k = k0 + j;
                         if (k >= nchunks) break;
                         const int n = k < nfull ? C : static_cast<int>(ps.width) - k * C;
-                        const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
+                        const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + rslot(k, 2 * lane + h)]);
                         for (int u = 0; u < n; u++) {
                             gu8 *d = orow + static_cast<size_t>(2 * (k * C + u)) * T::OBPX;
                             a7_store<T::OBPX>(d, te[j][u]);
@@ -748,7 +761,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 }
             } else {
                 for (int k = fl * FL; k < nchunks; k++) {
-                    const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + (k & (kSlots - 1)) * 4]);
+                    const v4u v = *reinterpret_cast<const v4u *>(&ring[rbase + rslot(k, 2 * lane + h)]);
                     if (k < nfull && ps.xf == 1) put_chunk<DEPTH>(orow, k, v);
                     else put_partial<DEPTH>(ps, orow, k, v, k < nfull ? C : static_cast<int>(ps.width) - k * C);
                 }
