@@ -384,6 +384,81 @@ def bench_planar(args, torch, dist, ws, rank, ctx, device, jpeg, datas):
     return out
 
 
+class _Regeom:
+    """A host-decoded frame's coefficient grids under another MCU geometry
+    (the same bytes: for 4:1:1 at 4096^2 the luma grid keeps its 512 x 512
+    blocks and the 65,536 chroma blocks of each 4:2:0 grid become 128 x 512)."""
+
+    def __init__(self, co, h, v, mxx, myy):
+        import ctypes as C
+
+        from zpix_amd import _lib
+
+        self.frame = _lib.zpx_jpeg_frame()
+        C.pointer(self.frame)[0] = co.frame
+        for c in range(3):
+            self.frame.h[c], self.frame.v[c] = h[c], v[c]
+        self.frame.mxx, self.frame.myy = mxx, myy
+        self.coeff_bytes = list(co.coeff_bytes)
+        for c in range(3):
+            assert self.coeff_bytes[c] == mxx * h[c] * myy * v[c] * 64 * int(co.frame.coeff_bits) // 8
+        self._co = co  # (the grids' host memory)
+
+
+def bench_odd_geometry(args, torch, dist, ws, rank, ctx, device, jpeg, datas):
+    """4:1:1 frames (h0 = 4: the MCU is 4 luma blocks wide), the geometry
+    the strip kernel took until round 4, now on the block kernel: the
+    headline frame's grids re-read as 4:1:1 (_Regeom), `images` slots, slot
+    0 checked against the oracle's reconstructBlock (decoder.zig:1553-1634)
+    + Image.rgbaPixels (image.zig:103-130, cOffset for Ratio411)."""
+    import ctypes as C
+
+    import numpy as np
+    import oracle_py as O
+
+    W = H = args.size
+    co = jpeg.Coefficients(datas[0])
+    fr = _Regeom(co, [4, 1, 1], [1, 1, 1], W // 32, H // 8)
+    jb = device.JpegBatch([fr], slots=[0] * args.images, output="rgba", ctx=ctx)
+    if rank == 0:
+        jb.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        f = fr.frame
+        dt = {8: np.int8, 16: np.int16}[int(f.coeff_bits)]
+        grids = [np.ctypeslib.as_array(C.cast(f.coeffs[c], C.POINTER(C.c_uint8)), shape=(fr.coeff_bytes[c],))
+                 .view(dt).astype(np.int32).reshape(-1, 64) for c in range(3)]
+        unzig = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
+                 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45,
+                 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]
+        qz = [np.array([f.qt[c][unzig[z]] for z in range(64)], np.int32) for c in range(3)]
+        strides = [f.mxx * 4 * 8, f.mxx * 8, f.mxx * 8]
+        planes = [np.zeros(strides[c] * f.myy * 8, np.uint8) for c in range(3)]
+        O.reconstruct_grids(3, W, H, [4, 1, 1], [1, 1, 1], f.mxx, f.myy, grids, qz, False, planes, strides)
+        buf = np.concatenate(planes)
+        img = O.ZoImage(kind=2, min_x=0, min_y=0, max_x=W, max_y=H, y_off=0, cb_off=planes[0].size,
+                        cr_off=planes[0].size + planes[1].size, y_stride=strides[0], c_stride=strides[1], subsample=4)
+        img.pixels = buf.ctypes.data_as(C.POINTER(C.c_uint8))
+        img.pixels_len = buf.size
+        want = np.zeros(W * H * 4, np.uint8)
+        O.lib().zo_rgba_pixels(C.byref(img), want.ctypes.data)
+        if not np.array_equal(jb.output_tensor(0).reshape(-1).cpu().numpy(), want):
+            raise SystemExit("parity failure: 4:1:1 frame on the block kernel != oracle")
+    steps = max(3, args.steps // 2)
+    wall, kern_ms = timed_steps(torch, dist, jb.launch, steps, args.warmup, ws)
+    ach = jb.bytes / (kern_ms * 1e-3) / 1e9
+    out = {"value": round(jb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
+           "kernel_ms_per_launch": round(kern_ms, 3),
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "jpeg_block_kernel<4,1,1,1>",
+                        "algorithmic_bytes_per_launch": jb.bytes},
+           "coeff_bits": int(fr.frame.coeff_bits),
+           "config": {"workload": f"{args.images}x {W}x{H} 4:1:1 JPEG -> RGBA (the headline frames' grids as "
+                                  "4:1:1 MCUs), block kernel"}}
+    del jb
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg):
     """4094x4096 4:2:0 frames (width % 4 != 0: rows only dword aligned, each
     row's last 4-pixel piece partial), `images` slots of one frame, slot 0
@@ -696,6 +771,7 @@ def main():
         result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)
     if not args.no_strip and not args.png_only:
         result["odd_width"] = bench_strip(args, torch, dist, ws, rank, ctx, S, device, jpeg)
+        result["odd_width"]["ratio411"] = bench_odd_geometry(args, torch, dist, ws, rank, ctx, device, jpeg, datas)
     if not args.no_e2e and not args.png_only:
         result["end_to_end"] = bench_e2e(args, torch, dist, ws, rank, ctx, S, threads)
     # ------------------------------------------------------------ CPU baseline (rank 0, N=1)
