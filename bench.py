@@ -650,7 +650,7 @@ def main():
         # the same frames through the int16 transport (what a frame with any
         # |coefficient| > 127 takes), for comparison: kernel time only
         int16 = None
-        if coeff_bits < 16 and not os.environ.get("ZPX_BENCH_NO_INT16"):
+        if coeff_bits < 16 and os.environ.get("ZPX_BENCH_NO_INT16", "0") != "1":
             del batch
             torch.cuda.empty_cache()
             for co in coeffs:

@@ -29,7 +29,8 @@ KEYS = [
     (r"png_slab_kernel<(\d+)>", "png_slab_cb{0}"),
     (r"png_pair_kernel<(\d+), (\w+), (\w+)>", "png_pair_d{0}{2}"),
     (r"png_unfilter_kernel", "png_unfilter"),
-    (r"rgba_pixels_kernel", "rgba_pixels"),
+    (r"rgba_batch_kernel<6>", "rgba_pixels"),  # (NRGBA64, the bench's rgbaPixels line)
+    (r"rgba_pixels_kernel", "rgba_pixels_generic"),
     (r"jpeg_sparse_expand", "jpeg_sparse_expand"),
 ]
 
