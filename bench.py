@@ -59,6 +59,7 @@ def parse():
                     help="skip configs[4]: progressive 4:4:4 JPEG + Adam7 RGBA16 PNG (worst-case control flow)")
     ap.add_argument("--no-planar", action="store_true",
                     help="skip the planar line (jpeg.load: the headline frames into Y/Cb/Cr planes)")
+    ap.add_argument("--no-pieces", action="store_true", help="skip the pieces-transport lines")
     ap.add_argument("--no-strip", action="store_true",
                     help="skip the odd-width line (4094-wide 4:2:0 frames: block kernel, and the strip-kernel fallback forced)")
     ap.add_argument("--gather-chunks", type=int, default=8,
@@ -379,6 +380,54 @@ def bench_planar(args, torch, dist, ws, rank, ctx, device, jpeg, datas):
             "config": {"workload": f"{args.images}x {args.size}x{args.size} baseline 4:2:0 JPEG -> Y/Cb/Cr planes "
                                    f"(jpeg.load), int{bits} coefficients"}}
         out[f"int{bits}"]["roofline"]["traffic"] = traffic_of(args, f"planar_int{bits}")
+        del jb
+        torch.cuda.empty_cache()
+    return out
+
+
+def bench_pieces(args, torch, dist, ws, rank, ctx, device, jpeg, datas):
+    """The headline's frames in the batch pipeline's compact transport
+    (ZPX_COEFFS_PIECES: each block's coefficients in zig-zag order up to its
+    last nonzero one, in 16-byte pieces, plus a uint32 index word a block;
+    SURVEY §8(f)1), read straight into the block kernels' coefficient image --
+    no dense grid is written or read back.  RGBA (the fused kernel) and
+    jpeg.load's planes (the planar kernel); slot 0 of each checked against the
+    oracle before timing.  Algorithmic bytes: the pieces + index words read,
+    the output written."""
+    import oracle_py as O
+
+    out = {}
+    cos = [jpeg.Coefficients(d, pieces=True) for d in datas]
+    if not all(c.is_pieces for c in cos):
+        return {"skipped": "frames not decoded into pieces"}
+    bits = int(cos[0].frame.coeff_bits)
+    slots = [i % len(cos) for i in range(args.images)]
+    dense_int8 = sum(c.frame.mxx * c.frame.myy * 6 * 64 for c in (cos[i] for i in slots))
+    for output, line in (("rgba", "rgba"), ("planes", "planes")):
+        jb = device.JpegBatch(cos, slots=slots, output=output, ctx=ctx)
+        if rank == 0:
+            jb.launch(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            ref = O.jpeg_decode(datas[0])
+            want = torch.from_numpy(ref.rgba_pixels() if output == "rgba" else ref.pixels)
+            if not torch.equal(jb.output_tensor(0).reshape(-1).cpu(), want.reshape(-1)):
+                raise SystemExit(f"parity failure: pieces {output} != oracle")
+        wall, kern_ms = timed_steps(torch, dist, jb.launch, args.steps, args.warmup, ws)
+        ach = jb.bytes / (kern_ms * 1e-3) / 1e9
+        kernel = "jpeg_block_kernel<pieces>" if output == "rgba" else "jpeg_plane_block_kernel<pieces>"
+        pieces_bytes = sum(int(cos[i].frame.pieces_bytes) for i in slots)
+        out[line] = {
+            "value": round(jb.pixels * ws * args.steps / wall / 1e6, 1), "unit": "MPixels/sec",
+            "kernel_ms_per_launch": round(kern_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": kernel,
+                         "traffic": traffic_of(args, f"pieces_{line}"), "algorithmic_bytes_per_launch": jb.bytes},
+            "coefficient_bytes_per_launch": {"pieces": pieces_bytes,
+                                             "index": sum(sum(cos[i].coeff_bytes) for i in slots),
+                                             "dense_int8_grids": dense_int8},
+            "config": {"workload": f"{args.images}x {args.size}x{args.size} baseline 4:2:0 JPEG from pieces -> "
+                                   + ("RGBA" if output == "rgba" else "Y/Cb/Cr planes (jpeg.load)")
+                                   + f", int{bits} pieces"}}
         del jb
         torch.cuda.empty_cache()
     return out
@@ -766,6 +815,9 @@ def main():
     # ------------------------------------------------------------ planar (jpeg.load)
     if not args.no_planar and not args.png_only:
         result["planar"] = bench_planar(args, torch, dist, ws, rank, ctx, device, jpeg, datas)
+    # ------------------------------------------------------------ the compact (pieces) transport
+    if not args.no_pieces and not args.png_only:
+        result["pieces"] = bench_pieces(args, torch, dist, ws, rank, ctx, device, jpeg, datas)
     # ------------------------------------------------------------ configs[4] and end to end
     if not args.no_config5 and not args.png_only:
         result["config5"] = bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png)

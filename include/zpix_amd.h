@@ -331,6 +331,16 @@ enum zpx_jpeg_color {
     ZPX_JPEG_COLOR_GRAY = 2,  /* 1 component: .gray (color.zig:122-126) */
 };
 
+/* How a frame's coefficients are laid out in memory. */
+enum zpx_coeff_layout {
+    ZPX_COEFFS_GRID = 0,   /* coeffs[c]: (mxx*h) x (myy*v) blocks x 64 natural-order coefficients */
+    ZPX_COEFFS_PIECES = 1, /* coeffs[c]: a uint32 per block in grid order, first_piece << 4 | pieces;
+                              the block's coefficients are `pieces` 16-byte pieces from `first_piece` of
+                              zpx_jpeg_frame.pieces, in zig-zag order up to its last nonzero one (the rest
+                              of the last piece zero), int8 (16 a piece) or int16 (8 a piece) per
+                              coeff_bits; pieces 0: an all-zero block.  Piece 0 must be zeros. */
+};
+
 /* One JPEG frame after host entropy decoding: coefficient grids
  * (processSos accumulate form, decoder.zig:1340-1345) + frame geometry. */
 typedef struct zpx_jpeg_frame {
@@ -348,6 +358,9 @@ typedef struct zpx_jpeg_frame {
     size_t strides[4];
     uint8_t *rgba;           /* DEVICE, ZPX_JPEG_RGBA */
     size_t rgba_stride;
+    int32_t layout;          /* zpx_coeff_layout of coeffs[] */
+    const void *pieces;      /* DEVICE, ZPX_COEFFS_PIECES: the frame's 16-byte pieces */
+    size_t pieces_bytes;     /* ZPX_COEFFS_PIECES: bytes at `pieces` */
 } zpx_jpeg_frame;
 
 /* Uploads the frame descriptors once; zpx_plan_launch then only enqueues
@@ -434,7 +447,14 @@ typedef struct zpx_jpeg_coeffs zpx_jpeg_coeffs;
 /* Runs the host half of jpeg.decode (markers, DHT/DQT/SOF/SOS, Huffman,
  * progressive refinement) and keeps the coefficient grids in pinned memory. */
 int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out);
-/* Fills a frame descriptor (host pointers for coeffs) from decoded coefficients. */
+/* The same, but a baseline frame whose single scan interleaves all three
+ * components is kept as ZPX_COEFFS_PIECES (the batch pipeline's transport:
+ * about 40 % of the dense int8 grid for a q75 photo, and the block kernels
+ * read it directly); other frames still decode into grids. */
+int zpx_jpeg_entropy_decode_pieces(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out);
+/* Fills a frame descriptor (host pointers for coeffs, and for pieces with
+ * layout ZPX_COEFFS_PIECES; coeff_bytes_per_comp then counts the index
+ * arrays) from decoded coefficients. */
 int zpx_jpeg_coeffs_frame(const zpx_jpeg_coeffs *c, zpx_jpeg_frame *frame,
                           size_t *coeff_bytes_per_comp /* [4] */);
 void zpx_jpeg_coeffs_free(zpx_jpeg_coeffs *c);
@@ -600,16 +620,16 @@ int zpx_debug_shard_fake_comm(int on);
  *   "jpeg_strip"  1: the fused JPEG plans use the strip kernel for every
  *                 frame (default 0: the block-per-lane kernel where it applies);
  *   "jpeg_sparse" 0: the batch pipeline uploads dense coefficient grids
- *                 (default 1: sparse records);
+ *                 (default 1: ZPX_COEFFS_PIECES);
  *   "png_pair"    0: PNG frames use the one-row-per-lane kernel (default 1);
  *   "qoi_segment" pixels per lane segment of the QOI encoder (16..4096;
  *                 default 0 = 128). */
 int zpx_debug_option(const char *name, int value);
-/* Test hook: decodes a baseline 3-component interleaved JPEG into the sparse
- * coefficient records the batch pipeline uploads and expands
- * them on the host into int32 grids (component after component, blocks x 64,
- * natural order).  Returns the record count, 0 if the frame took grids, or
- * -(status). */
+/* Test hook: decodes a baseline 3-component interleaved JPEG into the
+ * ZPX_COEFFS_PIECES form the batch pipeline uploads and
+ * expands it on the host into int32 grids (component after component,
+ * blocks x 64, natural order), checking the layout's invariants.  Returns
+ * the block count, 0 if the frame took grids, or -(status). */
 int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, int32_t *grids, size_t grid_elems);
 /* Test hook: the speculative multi-threaded inflate of one zlib stream (the
  * PNG host stage for large single images).  1 when it decoded

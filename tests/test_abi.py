@@ -523,15 +523,17 @@ def _sparse_grids(data: bytes):
     return n, out
 
 
+@pytest.mark.parametrize("quality", [75, 98])
 @pytest.mark.parametrize("sub", [0, 1, 2])
-def test_jpeg_sparse_records_match_oracle_grids(sub):
-    """The batch pipeline's sparse coefficient upload: the
-    records a baseline interleaved scan emits, expanded with the device
-    kernel's record -> block mapping, equal the oracle's coefficient grids."""
+def test_jpeg_pieces_match_oracle_grids(sub, quality):
+    """The batch pipeline's compact coefficient upload (ZPX_COEFFS_PIECES,
+    SURVEY §8(f)1): the zig-zag pieces a baseline interleaved scan emits,
+    expanded with the device kernels' index -> block mapping, equal the
+    oracle's coefficient grids (q98: int16 pieces)."""
     from tools import synthetic as S
 
     for seed, (w, h) in enumerate([(8, 8), (37, 21), (129, 67), (256, 200)]):
-        data = S.jpeg_subsampled(seed, w, h, sub)
+        data = S.jpeg_subsampled(seed, w, h, sub, quality)
         n, flat = _sparse_grids(data)
         assert n > 0, (sub, w, h)
         c = O.jpeg_coefficients(data)
@@ -540,9 +542,49 @@ def test_jpeg_sparse_records_match_oracle_grids(sub):
             g = np.asarray(g, np.int32).reshape(-1)
             assert np.array_equal(flat[off:off + g.size], g), (sub, w, h, i)
             off += g.size
+        assert n * 64 == off
 
 
-def test_jpeg_sparse_records_fall_back_to_grids():
+def _flat_then_busy(seed: int, w: int, h: int, quality: int) -> bytes:
+    """A frame whose first rows are flat and whose last rows are noise: the
+    pieces start int8 and widen to int16 part way through the scan."""
+    import io
+
+    from PIL import Image
+
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w, 3), 128, np.uint8)
+    img[h // 2:] = rng.integers(0, 256, (h - h // 2, w, 3), dtype=np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "JPEG", quality=quality, subsampling=2)
+    return b.getvalue()
+
+
+def test_jpeg_pieces_widen_midway():
+    """Pieces written as int8 are widened to int16 when a later block needs
+    it (JpegPieces::widen): same grids as the oracle, int16 width, and the
+    layout's invariants (piece 0 zeros, every block's pieces inside the
+    data) hold."""
+    from zpix_amd import jpeg as J
+
+    data = _flat_then_busy(5, 96, 160, 100)
+    n, flat = _sparse_grids(data)
+    c = O.jpeg_coefficients(data)
+    want = np.concatenate([np.asarray(g, np.int32).reshape(-1) for g in c.grids])
+    assert n * 64 == want.size and np.array_equal(flat[:want.size], want)
+    co = J.Coefficients(data, pieces=True)
+    assert co.is_pieces and co.frame.coeff_bits == 16
+    raw = co.pieces_bytes()
+    assert not raw[:16].any()
+    for comp in range(3):
+        ix = co.index(comp).astype(np.int64)
+        n_p, first = ix & 15, ix >> 4
+        assert ((n_p == 0) == (first == 0)).all()
+        assert (first + n_p <= len(raw) // 16).all() and (n_p <= 8).all()
+        assert np.array_equal(co.grid(comp).astype(np.int32).reshape(-1), np.asarray(c.grids[comp], np.int32).reshape(-1))
+
+
+def test_jpeg_pieces_fall_back_to_grids():
     """Progressive, gray, non-interleaved and DRI-parallel frames take grids."""
     from tools import synthetic as S
 

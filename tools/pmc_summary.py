@@ -18,12 +18,16 @@ import sys
 
 # kernel-name pattern -> short key (the first match wins)
 KEYS = [
-    (r"jpeg_plane_block_kernel<signed char>", "jpeg_plane_block_i8"),
-    (r"jpeg_plane_block_kernel<short>", "jpeg_plane_block_i16"),
-    (r"jpeg_block_kernel<signed char, true, 2, 2, 1, 1, 0>", "jpeg_block"),  # the headline instance
-    (r"jpeg_block_kernel<short, true, 2, 2, 1, 1, 0>", "jpeg_block_i16"),
-    (r"jpeg_block_kernel<signed char, true, 1, 1, 1, 1, 0>", "jpeg_block_444_i8"),
-    (r"jpeg_block_kernel<short, true, 1, 1, 1, 1, 0>", "jpeg_block_444_i16"),
+    # (the block kernels' last template argument: ZPX_COEFFS_PIECES instances)
+    (r"jpeg_plane_block_kernel<signed char, false>", "jpeg_plane_block_i8"),
+    (r"jpeg_plane_block_kernel<short, false>", "jpeg_plane_block_i16"),
+    (r"jpeg_plane_block_kernel<signed char, true>", "jpeg_plane_block_i8_pieces"),
+    (r"jpeg_plane_block_kernel<short, true>", "jpeg_plane_block_i16_pieces"),
+    (r"jpeg_block_kernel<signed char, true, 2, 2, 1, 1, 0, true>", "jpeg_block_pieces"),
+    (r"jpeg_block_kernel<signed char, true, 2, 2, 1, 1, 0, false>", "jpeg_block"),  # the headline instance
+    (r"jpeg_block_kernel<short, true, 2, 2, 1, 1, 0, false>", "jpeg_block_i16"),
+    (r"jpeg_block_kernel<signed char, true, 1, 1, 1, 1, 0, false>", "jpeg_block_444_i8"),
+    (r"jpeg_block_kernel<short, true, 1, 1, 1, 1, 0, false>", "jpeg_block_444_i16"),
     (r"jpeg_block_kernel<([^>]*)>", None),
     (r"jpeg_rgba_kernel", "jpeg_rgba"),
     (r"png_slab_kernel<(\d+)>", "png_slab_cb{0}"),
@@ -88,6 +92,8 @@ LINES = {
     "png_slab_build": ("png_slab_cb12",),
     "adam7_rgba16": ("png_pair_d15", "png_pair_d15_merge"),
     "rgba_pixels_nrgba64": ("rgba_pixels",),
+    "pieces_rgba": ("jpeg_block_pieces",),
+    "pieces_planes": ("jpeg_plane_block_i8_pieces",),
 }
 
 if __name__ == "__main__":

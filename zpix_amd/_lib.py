@@ -76,6 +76,9 @@ class zpx_jpeg_frame(C.Structure):
         ("strides", C.c_size_t * 4),
         ("rgba", C.c_void_p),
         ("rgba_stride", C.c_size_t),
+        ("layout", C.c_int32),
+        ("pieces", C.c_void_p),
+        ("pieces_bytes", C.c_size_t),
     ]
 
 
@@ -150,7 +153,7 @@ EXPORTS = [
     "zpx_jpeg_decode", "zpx_jpeg_load", "zpx_jpeg_probe_buffer", "zpx_jpeg_decode_rgba",
     "zpx_png_decode", "zpx_png_load", "zpx_png_probe_buffer", "zpx_from_buffer", "zpx_from_file_path",
     "zpx_jpeg_plan_create", "zpx_png_plan_create", "zpx_plan_launch", "zpx_plan_bytes",
-    "zpx_plan_kernel_count", "zpx_plan_destroy", "zpx_dev_rgba_pixels", "zpx_rgba_plan_create", "zpx_jpeg_entropy_decode",
+    "zpx_plan_kernel_count", "zpx_plan_destroy", "zpx_dev_rgba_pixels", "zpx_rgba_plan_create", "zpx_jpeg_entropy_decode", "zpx_jpeg_entropy_decode_pieces",
     "zpx_jpeg_coeffs_frame", "zpx_jpeg_coeffs_free", "zpx_jpeg_coeffs_widen", "zpx_png_inflate", "zpx_png_stream_frame",
     "zpx_png_stream_data", "zpx_png_stream_slab", "zpx_png_stream_free", "zpx_batch_decode_rgba", "zpx_batch_start",
     "zpx_batch_wait", "zpx_jpeg_decode_config", "zpx_png_decode_config", "zpx_plan_status",
@@ -203,6 +206,7 @@ def lib():
         "zpx_dev_rgba_pixels": (i32, [vp, C.POINTER(zpx_image), vp, vp]),
         "zpx_rgba_plan_create": (i32, [vp, C.POINTER(zpx_image), C.POINTER(vp), i32, C.POINTER(vp)]),
         "zpx_jpeg_entropy_decode": (i32, [C.c_char_p, sz, C.POINTER(vp)]),
+        "zpx_jpeg_entropy_decode_pieces": (i32, [C.c_char_p, sz, C.POINTER(vp)]),
         "zpx_jpeg_coeffs_frame": (i32, [vp, C.POINTER(zpx_jpeg_frame), C.POINTER(sz)]),
         "zpx_jpeg_coeffs_free": (None, [vp]),
         "zpx_jpeg_coeffs_widen": (i32, [vp, i32]),

@@ -82,12 +82,14 @@ struct Slot {
     bool busy = false;
     bool check_png = false;
     bool failed = false; // the image failed after its slot was bound (status already set)
-    DevJpegSparse sparse_args; // the slot's sparse expand launch (issue_jpeg)
+    DevPiecesExpand expand[4]; // a pieces frame the block kernels do not take: its expand jobs (issue_jpeg)
+    int nexpand = 0;
+    uint32_t expand_max = 0;
 };
 
 bool host_reserve(HostBuf &b, size_t n) { return b.bytes >= n || b.alloc(n, false); }
 
-// test switch "jpeg_sparse" = 0: dense coefficient grids instead of records
+// test switch "jpeg_sparse" = 0: dense coefficient grids instead of pieces
 bool jpeg_sparse_upload() { return opt(Opt::JpegSparse) != 0; }
 
 class Pipeline {
@@ -109,7 +111,7 @@ class Pipeline {
     int setup();
     int issue(Slot &s, bool &sync_done);
     int issue_jpeg(Slot &s, bool &sync_done);
-    int upload_sparse(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f);
+    int upload_pieces(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f, bool direct);
     int issue_png(Slot &s);
     int finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32_t W, uint32_t H, hipStream_t producer);
     void retire(Slot &s);
@@ -271,60 +273,57 @@ int Pipeline::finish_copy(Slot &s, const uint8_t *src, size_t src_stride, uint32
     return ZPX_OK;
 }
 
-// The records of a sparse frame (JpegSparse): H2D of counts, group offsets
-// and record bytes on the copy stream, device grids sized for the width the
-// values need; the expand kernel is launched on the compute stream once the
-// copy has landed (issue_jpeg).  f's coefficient pointers, width and narrow
-// flag are those of the expanded grids.
-int Pipeline::upload_sparse(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f)
+// A pieces frame (JpegPieces): H2D of its index arrays and pieces on the
+// copy stream.  direct: the block kernels read them (f keeps the pieces
+// layout with device pointers); otherwise the slot's expand jobs turn them
+// into dense grids on the compute stream first (issue_jpeg) and f points at
+// those.
+int Pipeline::upload_pieces(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f, bool direct)
 {
-    const JpegSparse &sp = jc.sparse;
-    int32_t m = 0;
-    int64_t mq = 0;
-    for (int k = 0; k < sp.ns; k++) {
-        const int c = sp.scan_comp[k];
-        m = std::max(m, sp.max_abs[c]);
-        mq = std::max<int64_t>(mq, int64_t(sp.max_abs[c]) * jc.max_q[c]);
+    const JpegPieces &p = jc.pieces;
+    size_t ib = 0;
+    for (int c = 0; c < jc.n_comp; c++) ib += align_up(p.blocks[c] * sizeof(uint32_t));
+    HIPCHK(ctx_, s.din.reserve(ib + p.data_bytes()));
+    uint8_t *base = s.din.as<uint8_t>();
+    const uint32_t *dix[4] = {};
+    size_t off = 0;
+    for (int c = 0; c < jc.n_comp; c++) {
+        const size_t n = p.blocks[c] * sizeof(uint32_t);
+        HIPCHK(ctx_, hipMemcpyAsync(base + off, p.index_of(c), n, hipMemcpyHostToDevice, h2d_));
+        dix[c] = reinterpret_cast<const uint32_t *>(base + off);
+        off += align_up(n);
     }
-    const int bits = m > 127 ? 16 : 8;
-    f.coeff_bits = bits;
-    f.narrow = mq <= 16384 ? 1 : 0;
-    const size_t nc = align_up(sp.nrec), ng = align_up(sp.groups_bytes());
-    HIPCHK(ctx_, s.din.reserve(nc + ng + sp.bytes + 16));
-    uint8_t *dc = s.din.as<uint8_t>(), *dg = dc + nc, *dd = dg + ng;
-    HIPCHK(ctx_, hipMemcpyAsync(dc, sp.counts.ptr, sp.nrec, hipMemcpyHostToDevice, h2d_));
-    HIPCHK(ctx_, hipMemcpyAsync(dg, sp.groups.ptr, sp.groups_bytes(), hipMemcpyHostToDevice, h2d_));
-    if (sp.bytes) HIPCHK(ctx_, hipMemcpyAsync(dd, sp.data.ptr, sp.bytes, hipMemcpyHostToDevice, h2d_));
-    h2d_bytes_ += double(sp.nrec + sp.groups_bytes() + sp.bytes);
+    uint8_t *dp = base + off;
+    HIPCHK(ctx_, hipMemcpyAsync(dp, p.data.ptr, p.data_bytes(), hipMemcpyHostToDevice, h2d_));
+    h2d_bytes_ += double(off + p.data_bytes());
+    s.nexpand = 0;
+    s.expand_max = 0;
+    if (direct) {
+        for (int c = 0; c < jc.n_comp; c++) f.coeffs[c] = dix[c];
+        f.pieces = dp;
+        return ZPX_OK;
+    }
     size_t gbytes[4] = {}, total = 0;
     for (int c = 0; c < jc.n_comp; c++) {
-        gbytes[c] = size_t(jc.mxx) * jc.myy * jc.comp[c].h * jc.comp[c].v * 64 * (bits / 8);
+        gbytes[c] = p.blocks[c] * 64 * (f.coeff_bits / 8);
         total += align_up(gbytes[c]);
     }
     HIPCHK(ctx_, s.dgrid.reserve(total));
-    DevJpegSparse &a = s.sparse_args;
-    a = DevJpegSparse{};
-    a.counts = dc;
-    a.groups = reinterpret_cast<const uint32_t *>(dg);
-    a.data = dd;
-    a.nrec = sp.nrec;
-    a.mxx = jc.mxx;
-    a.ns = sp.ns;
-    size_t off = 0;
-    uint8_t *grid[4] = {};
+    off = 0;
     for (int c = 0; c < jc.n_comp; c++) {
-        grid[c] = s.dgrid.as<uint8_t>() + off;
+        DevPiecesExpand &j = s.expand[s.nexpand++];
+        j = DevPiecesExpand{};
+        j.index = dix[c];
+        j.pieces = dp;
+        j.grid = s.dgrid.as<uint8_t>() + off;
+        j.blocks = static_cast<uint32_t>(p.blocks[c]);
+        s.expand_max = std::max(s.expand_max, j.blocks);
+        f.coeffs[c] = j.grid;
         off += align_up(gbytes[c]);
-        f.coeffs[c] = grid[c];
     }
-    for (int k = 0; k < sp.ns; k++) {
-        const int c = sp.scan_comp[k];
-        a.h[k] = jc.comp[c].h;
-        a.v[k] = jc.comp[c].v;
-        a.gw[k] = jc.mxx * jc.comp[c].h;
-        a.grid[k] = grid[c];
-        a.bpm += a.h[k] * a.v[k];
-    }
+    f.layout = ZPX_COEFFS_GRID;
+    f.pieces = nullptr;
+    f.pieces_bytes = 0;
     return ZPX_OK;
 }
 
@@ -345,8 +344,15 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
         return ZPX_OK;
     }
     // fused dequant + IDCT + upsample + colour straight into the destination
-    if (d.jc.sparse.valid) {
-        if (int e = upload_sparse(s, d.jc, f)) return e;
+    if (d.jc.pieces.valid) {
+        // the block kernels read the pieces (the RGBA rows they store are
+        // dword aligned: a device destination's own stride, or the slot's
+        // staging at 4W)
+        const bool aligned = on_host_ || ((stride & 3) == 0 && (reinterpret_cast<uintptr_t>(it.dst) & 3) == 0);
+        const bool direct = fused && f.narrow && (f.coeff_bits == 8 || f.coeff_bits == 16) &&
+                            opt(Opt::JpegStrip) == 0 && aligned &&
+                            jpeg_block_pieces_supported(f.color, f.h[0], f.v[0], f.h[1], f.v[1]);
+        if (int e = upload_pieces(s, d.jc, f, direct)) return e;
     } else {
         size_t total = 0;
         for (int c = 0; c < 4; c++) total += f.coeffs[c] ? align_up(cb[c]) : 0;
@@ -363,8 +369,19 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
     }
     HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
     HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
-    if (d.jc.sparse.valid && launch_jpeg_sparse_expand(s.sparse_args, f.coeff_bits, ctx_->stream))
-        return hip_fail(ctx_, hipGetLastError(), "batch: jpeg sparse expand");
+    if (d.jc.pieces.valid && s.nexpand) {
+        // the jobs go up behind the frame descriptor's place in the staging
+        // (the descriptor copy below must not overwrite them in flight)
+        const size_t jo = align_up(sizeof(DevJpegFrame));
+        HIPCHK(ctx_, s.ddesc.reserve(jo + sizeof(s.expand)));
+        if (!host_reserve(s.hdesc, jo + sizeof(s.expand))) return ZPX_E_OUT_OF_MEMORY;
+        memcpy(static_cast<uint8_t *>(s.hdesc.ptr) + jo, s.expand, sizeof(s.expand));
+        HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.as<uint8_t>() + jo, static_cast<uint8_t *>(s.hdesc.ptr) + jo,
+                                    sizeof(s.expand), hipMemcpyHostToDevice, ctx_->stream));
+        if (launch_jpeg_pieces_expand(reinterpret_cast<const DevPiecesExpand *>(s.ddesc.as<uint8_t>() + jo), s.nexpand,
+                                      s.expand_max, f.coeff_bits, ctx_->stream))
+            return hip_fail(ctx_, hipGetLastError(), "batch: jpeg pieces expand");
+    }
     if (!fused) {
         // planes + colour pass from the coefficients this worker already
         // decoded (no second entropy decode, no host sync): CMYK, Adobe RGB

@@ -19,6 +19,18 @@ struct DevJpegFrame {
     int32_t qt[4][64];       // natural order
     uint32_t qp[4][32];      // quant-pair tables of the block kernels' row pass, per component
                              // (per row r: (q1,q7), (q5,q3), (q2,q6), (q0,q4) as u16 pairs)
+    const uint8_t *pieces;   // ZPX_COEFFS_PIECES: the 16-byte pieces; coeffs[c] are then the
+                             // per-block index arrays (first piece << 4 | pieces), else null
+};
+
+// One component of a ZPX_COEFFS_PIECES frame expanded into its dense grid
+// (jpeg_pieces_expand_kernel).
+struct DevPiecesExpand {
+    const uint32_t *index;
+    const uint8_t *pieces;
+    void *grid;
+    uint32_t blocks;
+    uint32_t pad;
 };
 
 // The planar block kernel's task space for one plan group (frames of one

@@ -184,6 +184,38 @@ __device__ __forceinline__ u32x4 row_coef_pairs(const u32x4 *raw, int r)
     }
 }
 
+// The same pairs from a ZPX_COEFFS_PIECES block: its coefficients in zig-zag
+// order (the image's pieces hold 16 int8 / 8 int16 values).  Each pair is one
+// v_perm of the two dwords holding its coefficients -- for int8, a value at
+// an even byte comes from its dword shifted up a byte, so that the perm's
+// sign selectors (which read bytes 1 and 3 of either source) reach it -- the
+// same count as the natural order's perms and shifts.
+template <typename CoefT>
+__device__ __forceinline__ u32x4 row_coef_pairs_zz(const u32x4 *raw, int r)
+{
+    constexpr int kLo[4] = {1, 5, 2, 0}, kHi[4] = {7, 3, 6, 4}; // the qpair order
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int za = kZigOf[8 * r + kLo[k]], zb = kZigOf[8 * r + kHi[k]];
+        if constexpr (sizeof(CoefT) == 1) {
+            const int da = za >> 2, ba = za & 3, db = zb >> 2, bb = zb & 3;
+            const uint32_t wa = raw[da >> 2][da & 3], wb = raw[db >> 2][db & 3];
+            const uint32_t sa = (ba & 1) ? wa : wa << 8, sb = (bb & 1) ? wb : wb << 8;
+            const uint32_t pa = static_cast<uint32_t>(ba | 1), pb = static_cast<uint32_t>(bb | 1);
+            const uint32_t sel = pa | (pa == 1 ? 8u : 9u) << 8 | (4u + pb) << 16 | (pb == 1 ? 10u : 11u) << 24;
+            o[k] = __builtin_amdgcn_perm(sb, sa, sel);
+        } else {
+            const int da = za >> 1, ha = za & 1, db = zb >> 1, hb = zb & 1;
+            const uint32_t wa = raw[da >> 2][da & 3], wb = raw[db >> 2][db & 3];
+            const uint32_t sel = static_cast<uint32_t>(2 * ha) | static_cast<uint32_t>(2 * ha + 1) << 8 |
+                                 static_cast<uint32_t>(4 + 2 * hb) << 16 | static_cast<uint32_t>(5 + 2 * hb) << 24;
+            o[k] = __builtin_amdgcn_perm(wb, wa, sel);
+        }
+    }
+    return o;
+}
+
 // Lane j's block from the LDS image into registers (all LDS reads of the
 // image issue here, so the caller's lgkmcnt(0) lets the next DMA refill it).
 template <typename CoefT>
@@ -196,12 +228,12 @@ __device__ __forceinline__ void load_raw(const uint8_t *img, int j, u32x4 raw[Co
 
 // Dequant + row pass (idct.zig:79-145) + column pass with clamp, as
 // idct_block, from the raw block and the component's quant-pair table.
-template <typename CoefT, typename QRow>
+template <typename CoefT, bool ZZ = false, typename QRow>
 __device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT>::P], QRow &&qrow, int32_t s[64])
 {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const u32x4 p = qrow(r, row_coef_pairs<CoefT>(raw, r));
+        const u32x4 p = qrow(r, ZZ ? row_coef_pairs_zz<CoefT>(raw, r) : row_coef_pairs<CoefT>(raw, r));
         const uint32_t p17 = p[0], p53 = p[1], p26 = p[2], p04 = p[3];
         int32_t x4 = dot2<W1, W7>(p17), x5 = dot2<W7, -W1>(p17);
         int32_t x6 = dot2<W5, W3>(p53), x7 = dot2<W3, -W5>(p53);
@@ -349,7 +381,7 @@ __device__ __forceinline__ void static_for(F &&f)
     static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR>
+template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR, bool ZZ = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 2 ? kWavesPerEu16 : kWavesPerEu8)))
 void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int tasks_per_frame, int total_tasks)
 {
@@ -396,7 +428,8 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
     // read inside the loop compile to vector loads whose vmcnt waits would
     // also wait for the stores in flight)
     struct TaskSrc {
-        const CoefT *g[3];
+        const CoefT *g[3]; // (ZZ: the components' piece index arrays)
+        const uint8_t *pz; // ZZ: the frame's pieces
         uint64_t qp; // address of DevJpegFrame::qp[0] of the task's frame (uniform: scalar loads)
         uint8_t *rgba;
         int gwy, gwc, myy, width, height;
@@ -434,6 +467,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         s.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
         s.stride = u32(static_cast<uint32_t>(fr.rgba_stride));
         s.qp = reinterpret_cast<uint64_t>(ptr(reinterpret_cast<const void *>(reinterpret_cast<uintptr_t>(&fr.qp[0][0]))));
+        s.pz = ZZ ? static_cast<const uint8_t *>(ptr(fr.pieces)) : nullptr;
         return s;
     };
     auto coords = [&](int t, int &f, int &my, int &mx0) __attribute__((always_inline)) {
@@ -503,6 +537,32 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             glds16<kDmaNt>(row + static_cast<uint32_t>(bx * BYTES + 16 * q), img + 1024 * k);
         }
     };
+    // ZPX_COEFFS_PIECES (ZZ): the index word of the lane's own block of pass
+    // P (its pass_block; 0 -- all zeros -- for a block that does not
+    // exist), one vector load, made one task ahead
+    auto load_ix = [&](const TaskSrc &t, int my_, int mx0_, auto P) __attribute__((always_inline)) -> uint32_t {
+        const PassBlock b = pass_block(P, lane);
+        const int hh = b.comp == 0 ? H0 : HC, vv = b.comp == 0 ? V0 : VC;
+        const int gw = b.comp == 0 ? t.gwy : t.gwc;
+        const uint32_t *ix = reinterpret_cast<const uint32_t *>(b.comp == 0 ? t.g[0] : (b.comp == 1 ? t.g[1] : t.g[2]));
+        if (!(b.ok && ix != nullptr && my_ < t.myy)) return 0u;
+        const int bx = min(mx0_ * hh + b.cx, gw - 1);
+        return ix[static_cast<size_t>(my_ * vv + b.cy) * static_cast<uint32_t>(gw) + static_cast<uint32_t>(bx)];
+    };
+    // ... and the pass's pieces -> cimg in the CoefImage layout: DMA
+    // instruction k's lane fetches piece q of block j = B k + lane % B (whose
+    // index word lane j holds: ds_bpermute); a piece past the block's count
+    // is piece 0, zeros
+    auto issue_pass_zz = [&](const TaskSrc &t, uint32_t ixv, uint8_t *img) __attribute__((always_inline)) {
+        using I = CoefImage<CoefT>;
+#pragma unroll
+        for (int k = 0; k < I::P; k++) {
+            const uint32_t e = static_cast<uint32_t>(__shfl(static_cast<int>(ixv), I::B * k + lane % I::B));
+            const uint32_t q = static_cast<uint32_t>((lane / I::B + I::P - (I::P == 8 ? k : 0)) % I::P);
+            const uint32_t piece = q < (e & 15u) ? (e >> 4) + q : 0u;
+            glds16<kDmaNt>(t.pz + static_cast<size_t>(piece) * 16, img + 1024 * k);
+        }
+    };
     // vmcnt bookkeeping (the DMA is inline asm, so the kernel counts it):
     // S(p) stores per pass; the image of pass p was issued one pass earlier,
     // and at pass p's start the operations issued after it are that pass's
@@ -518,7 +578,17 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         for (int i = 0; i < 32; i++)
             if (i < n) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0, 0, 0, 0}, none, 16 * i, 0, kStoreAux);
     };
-    issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
+    // ZZ: index words of the current task's passes (ixc) and, loaded at its
+    // first pass before that pass's DMA, of the next task's (ixn)
+    static_assert(!ZZ || NP >= 2, "the next task's index words load during its predecessor");
+    uint32_t ixc[ZZ ? NP : 1], ixn[ZZ ? NP : 1];
+    if constexpr (ZZ) {
+        static_for<NP>([&](auto Q) __attribute__((always_inline)) { ixc[decltype(Q)::value] = load_ix(ts, my, mx0, Q); });
+        issue_pass_zz(ts, ixc[0], cimg);
+    } else {
+        issue_pass(ts, my, mx0, std::integral_constant<int, 0>{}, cimg);
+    }
+    (void)ixn;
     pad_stores(S(NP - 1));
     uint32_t cbr[kInLane ? 16 : 1], crr[kInLane ? 16 : 1]; // in-lane chroma samples (bytes)
     (void)cbr;
@@ -564,10 +634,20 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             // pass p + 1's coefficients load while this pass computes
             constexpr int pn = p + 1;
-            if constexpr (pn < NP)
+            if constexpr (ZZ) {
+                if constexpr (p == 0)
+                    static_for<NP>([&](auto Q) __attribute__((always_inline)) {
+                        ixn[decltype(Q)::value] = load_ix(tsn, myn, mxn, Q);
+                    });
+                if constexpr (pn < NP)
+                    issue_pass_zz(ts, ixc[pn], cimg);
+                else
+                    issue_pass_zz(tsn, ixn[0], cimg);
+            } else if constexpr (pn < NP) {
                 issue_pass(ts, my, mx0, std::integral_constant<int, pn>{}, cimg);
-            else
+            } else {
                 issue_pass(tsn, myn, mxn, std::integral_constant<int, pn - NP>{}, cimg);
+            }
             static_assert(NARROW, "the pair IDCT needs |coef * q| <= 16384");
             {
                 // the pass's component(s): one for luma / in-lane passes, and
@@ -578,7 +658,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 typedef const __attribute__((address_space(4))) u32x4 *cq;
                 const uint64_t q0 = ts.qp + 128 * c0, q2 = ts.qp + 256;
                 // dequantized pairs of row r: coefficient pairs c x the row's quant pairs
-                idct_block_pairs<CoefT>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
+                idct_block_pairs<CoefT, ZZ>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
                     const u32x4 a = *reinterpret_cast<cq>(q0 + 16 * r);
                     if constexpr (kind(p) == 1 && kCb > 0 && kCb < 64) {
                         const u32x4 b = *reinterpret_cast<cq>(q2 + 16 * r);
@@ -724,6 +804,9 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         });
         if (!more) break;
         if constexpr (CP > 0) wave_lds_order(); // the tile's reads precede the next task's writes
+        if constexpr (ZZ)
+#pragma unroll
+            for (int q = 0; q < NP; q++) ixc[q] = ixn[q];
         task = tn;
         f = fn;
         my = myn;
@@ -764,7 +847,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 constexpr int kPlaneWavesPerEu = ZPX_PLANE_WPE; // <= 128 VGPRs: 16 waves per CU
 constexpr int kPlaneStoreAux = ZPX_PLANE_ST;
 
-template <typename CoefT>
+template <typename CoefT, bool ZZ = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kPlaneWavesPerEu)))
 void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskGeom geo)
 {
@@ -781,7 +864,8 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
     // a task's uniform view (scalar loads of the descriptor through the
     // constant address space, as in jpeg_block_kernel)
     struct PTask {
-        uint64_t grid, plane, qp;
+        uint64_t grid, plane, qp; // (ZZ: grid = the component's piece index array)
+        uint64_t pz;              // ZZ: the frame's pieces
         uint32_t stride;
         int gw, by, bx0, rule, hh, vv, width, height;
         bool ok;
@@ -806,6 +890,7 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
         k.height = static_cast<int>(u32(static_cast<uint32_t>(fr.height)));
         k.hh = geo.hh[c];
         k.vv = geo.vv[c];
+        k.pz = ZZ ? uptr(fr.pieces) : 0;
         // (a ragged batch's task past a smaller frame's grid, or a component
         // never scanned / without a plane, writes nothing)
         k.ok = k.by < gh && k.bx0 < k.gw && k.grid != 0 && k.plane != 0 && k.rule != ZPX_BLOCKS_NONE;
@@ -825,6 +910,25 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
             glds16<ZPX_PLANE_DMA_NT != 0>(row + static_cast<uint32_t>(bx * BYTES + 16 * q), cimg + 1024 * i);
         }
     };
+    // ZZ (ZPX_COEFFS_PIECES): the index word of the lane's block (0 past the
+    // grid: zeros), and the task's pieces -> cimg as `issue` does: DMA
+    // instruction i's lane fetches piece q of block j = B i + lane % B, whose
+    // index word lane j holds (ds_bpermute); past the block's count, piece 0
+    auto load_ix = [&](const PTask &k) __attribute__((always_inline)) -> uint32_t {
+        if (!k.ok) return 0u;
+        const uint32_t *ix = reinterpret_cast<const uint32_t *>(k.grid);
+        return ix[static_cast<size_t>(k.by) * static_cast<uint32_t>(k.gw) + static_cast<uint32_t>(min(k.bx0 + lane, k.gw - 1))];
+    };
+    auto issue_zz = [&](const PTask &k, uint32_t ixv) __attribute__((always_inline)) {
+        const uint8_t *pz = reinterpret_cast<const uint8_t *>(k.pz);
+#pragma unroll
+        for (int i = 0; i < I::P; i++) {
+            const uint32_t e = static_cast<uint32_t>(__shfl(static_cast<int>(ixv), I::B * i + lane % I::B));
+            const uint32_t q = static_cast<uint32_t>((lane / I::B + I::P - (I::P == 8 ? i : 0)) % I::P);
+            const uint32_t piece = q < (e & 15u) ? (e >> 4) + q : 0u;
+            glds16<ZPX_PLANE_DMA_NT != 0>(pz + static_cast<size_t>(piece) * 16, cimg + 1024 * i);
+        }
+    };
     int task;
     {
         const int nw = static_cast<int>(gridDim.x), w = static_cast<int>(blockIdx.x);
@@ -834,7 +938,18 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
     if (task >= geo.total) return;
     const int tstride = static_cast<int>(gridDim.x);
     PTask k = task_of(task);
-    issue(k);
+    // ZZ: the next task and its index word, loaded one task ahead of its DMA
+    PTask kz = k;
+    uint32_t ixz = 0;
+    if constexpr (ZZ) {
+        issue_zz(k, load_ix(k));
+        if (task + tstride < geo.total) {
+            kz = task_of(task + tstride);
+            ixz = load_ix(kz);
+        }
+    } else {
+        issue(k);
+    }
     // the loop head expects the previous task's 8 stores behind the DMA
     // (dropped: empty range; offsets apart, so hipcc cannot merge them into
     // fewer, wider stores -- which would let vmcnt(8) pass before the DMA)
@@ -850,13 +965,23 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
         load_raw<CoefT>(cimg, lane, raw);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         PTask kn = k;
-        if (more) {
+        if constexpr (ZZ) {
+            // (the index load after the DMA: the next vmcnt(8) waits for both)
+            if (more) {
+                kn = kz;
+                issue_zz(kn, ixz);
+                if (tn + tstride < geo.total) {
+                    kz = task_of(tn + tstride);
+                    ixz = load_ix(kz);
+                }
+            }
+        } else if (more) {
             kn = task_of(tn);
             issue(kn);
         }
         int32_t s[64];
         typedef const __attribute__((address_space(4))) u32x4 *cq;
-        idct_block_pairs<CoefT>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
+        idct_block_pairs<CoefT, ZZ>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
             const u32x4 a = *reinterpret_cast<cq>(k.qp + 16 * r);
             return u32x4{pk_mul16(c[0], a[0]), pk_mul16(c[1], a[1]), pk_mul16(c[2], a[2]), pk_mul16(c[3], a[3])};
         }, s);
@@ -896,14 +1021,14 @@ int resident_waves(K kernel)
     return device_cu_count() * per_cu;
 }
 
-template <typename CoefT, int H0, int V0, int HC, int VC, int COLOR>
+template <typename CoefT, int H0, int V0, int HC, int VC, int COLOR, bool ZZ = false>
 int launch_block_t(const DevJpegFrame *d_frames, int n_frames, int max_mxx, int max_myy, hipStream_t stream)
 {
     constexpr int T = 64 / H0;
     const int tasks_x = (max_mxx + T - 1) / T;
     const int per_frame = tasks_x * max_myy;
     const int total = per_frame * n_frames;
-    auto kernel = jpeg_block_kernel<CoefT, true, H0, V0, HC, VC, COLOR>;
+    auto kernel = jpeg_block_kernel<CoefT, true, H0, V0, HC, VC, COLOR, ZZ>;
     static const int resident = resident_waves(kernel); // (one per instance: this function is)
     const int grid = total < resident ? total : resident;
     if (grid > 0) hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, tasks_x, per_frame, total);
@@ -931,6 +1056,21 @@ int block_geom(int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStrea
     return -2;
 }
 
+// the ZPX_COEFFS_PIECES instances (the batch pipeline's transport: baseline
+// frames whose one scan interleaves Y, Cb, Cr)
+template <typename CoefT>
+int block_pieces(int color, int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStream_t s)
+{
+    if (color != ZPX_JPEG_COLOR_YCBCR) return -2;
+    switch (key) {
+    case 0x2211: return launch_block_t<CoefT, 2, 2, 1, 1, ZPX_JPEG_COLOR_YCBCR, true>(d, n, mxx, myy, s);
+    case 0x2111: return launch_block_t<CoefT, 2, 1, 1, 1, ZPX_JPEG_COLOR_YCBCR, true>(d, n, mxx, myy, s);
+    case 0x1211: return launch_block_t<CoefT, 1, 2, 1, 1, ZPX_JPEG_COLOR_YCBCR, true>(d, n, mxx, myy, s);
+    case 0x1111: return launch_block_t<CoefT, 1, 1, 1, 1, ZPX_JPEG_COLOR_YCBCR, true>(d, n, mxx, myy, s);
+    }
+    return -2;
+}
+
 template <typename CoefT>
 int block_color(int color, int key, const DevJpegFrame *d, int n, int mxx, int myy, hipStream_t s)
 {
@@ -943,8 +1083,14 @@ int block_color(int color, int key, const DevJpegFrame *d, int n, int mxx, int m
 }
 } // namespace
 
+bool jpeg_block_pieces_supported(int color, int h0, int v0, int hc, int vc)
+{
+    const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
+    return color == ZPX_JPEG_COLOR_YCBCR && (key == 0x2211 || key == 0x2111 || key == 0x1211 || key == 0x1111);
+}
+
 int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &g, int coeff_bits,
-                            bool narrow, hipStream_t stream)
+                            bool narrow, bool pieces, hipStream_t stream)
 {
     if (!narrow || (coeff_bits != 8 && coeff_bits != 16)) return -2;
     if (g.ncomp < 1 || g.ncomp > 4) return -2;
@@ -967,9 +1113,12 @@ int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const Jp
     if (total >= (int64_t(1) << 31)) return -2;
     geo.per_frame = static_cast<int32_t>(per);
     geo.total = static_cast<int32_t>(total);
-    auto kernel = coeff_bits == 8 ? jpeg_plane_block_kernel<int8_t> : jpeg_plane_block_kernel<int16_t>;
+    auto kernel = pieces ? (coeff_bits == 8 ? jpeg_plane_block_kernel<int8_t, true> : jpeg_plane_block_kernel<int16_t, true>)
+                         : (coeff_bits == 8 ? jpeg_plane_block_kernel<int8_t> : jpeg_plane_block_kernel<int16_t>);
     static const int resident8 = resident_waves(jpeg_plane_block_kernel<int8_t>);
     static const int resident16 = resident_waves(jpeg_plane_block_kernel<int16_t>);
+    static const int resident8z = resident_waves(jpeg_plane_block_kernel<int8_t, true>);
+    static const int resident16z = resident_waves(jpeg_plane_block_kernel<int16_t, true>);
     // waves per CU: as many as fit for int8 (20: 8 / 12 / 16 ran 0.855 /
     // 0.823 / 0.810 ms against 0.800 per 64 frames), 8 for int16 (0.952 /
     // 0.972 / 0.988 ms at 8 / 12 / 16 against 0.990 at all 16 that fit;
@@ -977,19 +1126,25 @@ int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const Jp
 #ifndef ZPX_PLANE_WPCU16
 #define ZPX_PLANE_WPCU16 8
 #endif
-    const int resident = coeff_bits == 8 ? resident8 : std::min(resident16, device_cu_count() * ZPX_PLANE_WPCU16);
+    const int resident = coeff_bits == 8 ? (pieces ? resident8z : resident8)
+                                         : std::min(pieces ? resident16z : resident16, device_cu_count() * ZPX_PLANE_WPCU16);
     const int grid = total < resident ? static_cast<int>(total) : resident;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, geo);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
-                      int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream)
+                      int max_mxx, int max_myy, int coeff_bits, bool narrow, bool pieces, hipStream_t stream)
 {
     if (!narrow || (coeff_bits != 8 && coeff_bits != 16)) return -2;
     const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;
-    const int rc = coeff_bits == 8 ? block_color<int8_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
-                                   : block_color<int16_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
+    int rc;
+    if (pieces)
+        rc = coeff_bits == 8 ? block_pieces<int8_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
+                             : block_pieces<int16_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
+    else
+        rc = coeff_bits == 8 ? block_color<int8_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream)
+                             : block_color<int16_t>(color, key, d_frames, n_frames, max_mxx, max_myy, stream);
     if (rc) return rc;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

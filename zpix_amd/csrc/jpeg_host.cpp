@@ -299,6 +299,36 @@ bool CoeffGrid::apply_overflow(int32_t max_abs, const std::vector<std::pair<size
     return true;
 }
 
+bool JpegPieces::widen()
+{
+    if (bits == 16) return true;
+    HostBuf nd;
+    if (!nd.alloc(cap * 16, false)) return false;
+    uint8_t *o = static_cast<uint8_t *>(nd.ptr);
+    const int8_t *src = static_cast<const int8_t *>(data.ptr);
+    memset(o, 0, 16);
+    size_t n = 1;
+    uint32_t *ix = static_cast<uint32_t *>(index.ptr);
+    size_t total = 0;
+    for (int c = 0; c < 4; c++) total = std::max(total, first[c] + blocks[c]);
+    for (size_t k = 0; k < total; k++) {
+        if (ix[k] == 0) continue;
+        const int8_t *v = src + size_t(ix[k] >> 4) * 16;
+        int eob = static_cast<int>(ix[k] & 15) * 16;
+        while (eob > 0 && v[eob - 1] == 0) eob--;
+        const size_t np = static_cast<size_t>((eob + 7) / 8);
+        if (n + np > cap) return false;
+        int16_t *d = reinterpret_cast<int16_t *>(o + n * 16);
+        for (size_t z = 0; z < np * 8; z++) d[z] = static_cast<int16_t>(z < size_t(eob) ? v[z] : 0);
+        ix[k] = np ? static_cast<uint32_t>(n << 4 | np) : 0u;
+        n += np;
+    }
+    data = static_cast<HostBuf &&>(nd);
+    npieces = n;
+    bits = 16;
+    return true;
+}
+
 // ---------------------------------------------------------------- decoder
 namespace {
 
@@ -309,6 +339,15 @@ constexpr uint8_t kUnzig[64] = {
     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
 };
+// natural -> zig-zag index
+struct ZigOf {
+    uint8_t z[64];
+    constexpr ZigOf() : z()
+    {
+        for (int i = 0; i < 64; i++) z[kUnzig[i]] = static_cast<uint8_t>(i);
+    }
+};
+constexpr ZigOf kZigOf{};
 
 struct Huff { // HuffTable.zig
     int32_t num_codes = 0;
@@ -317,7 +356,7 @@ struct Huff { // HuffTable.zig
     int32_t min_codes[16] = {}, max_codes[16] = {}, vals_indices[16] = {};
 };
 
-// internal status: the frame does not fit the sparse records (jpeg_entropy_decode
+// internal status: the frame does not fit the pieces (jpeg_entropy_decode
 // then decodes it again into grids); never returned to a caller
 constexpr int kSparseAbort = 1 << 20;
 
@@ -528,26 +567,44 @@ class Decoder {
             return o.grid[ci].store_sparse(blk, b, pos, n) ? 0 : ZPX_E_OUT_OF_MEMORY;
         }
     };
-    // appends a block's record to o.sparse (see JpegSparse)
-    struct RecordSink {
-        JpegSparse &sp;
-        int put(int ci, size_t, int32_t *b, const uint8_t *pos, int n)
+    // appends a block's pieces to o.pieces (see JpegPieces)
+    struct PieceSink {
+        JpegPieces &p;
+        int put(int ci, size_t blk, int32_t *b, const uint8_t *pos, int n)
         {
-            if (sp.bytes + 3 * size_t(n) > sp.cap) return kSparseAbort;
-            uint8_t *d = static_cast<uint8_t *>(sp.data.ptr) + sp.bytes;
-            static_cast<uint8_t *>(sp.counts.ptr)[sp.nrec++] = static_cast<uint8_t>(n);
-            int32_t m = sp.max_abs[ci];
+            // pos[] is in decode (zig-zag) order: the end of block follows
+            // the last nonzero entry (the DC entry is listed even when zero)
+            int32_t m = p.max_abs[ci];
+            int eob = 0;
             for (int i = 0; i < n; i++) {
                 const int32_t v = b[pos[i]];
                 const int32_t a = v < 0 ? -v : v;
                 if (a > 32767 || v == INT32_MIN) return kSparseAbort;
                 m = a > m ? a : m;
-                d[i] = pos[i];
-                d[n + 2 * i] = static_cast<uint8_t>(v);
-                d[n + 2 * i + 1] = static_cast<uint8_t>(v >> 8);
+                if (v != 0) eob = kZigOf.z[pos[i]] + 1;
             }
-            sp.max_abs[ci] = m;
-            sp.bytes += 3 * size_t(n);
+            p.max_abs[ci] = m;
+            if (p.bits == 8 && m > 127 && !p.widen()) return kSparseAbort;
+            uint32_t &ix = p.index_of(ci)[blk];
+            if (eob == 0) {
+                ix = 0;
+                return 0;
+            }
+            const int per = p.bits == 8 ? 16 : 8; // coefficients a piece
+            const size_t np = static_cast<size_t>((eob + per - 1) / per);
+            if (p.npieces + np > p.cap) return kSparseAbort;
+            uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + p.npieces * 16;
+            memset(d, 0, np * 16);
+            if (p.bits == 8) {
+                for (int i = 0; i < n; i++) reinterpret_cast<int8_t *>(d)[kZigOf.z[pos[i]]] = static_cast<int8_t>(b[pos[i]]);
+            } else {
+                for (int i = 0; i < n; i++) {
+                    const int16_t v = static_cast<int16_t>(b[pos[i]]);
+                    memcpy(d + 2 * kZigOf.z[pos[i]], &v, 2);
+                }
+            }
+            ix = static_cast<uint32_t>(p.npieces << 4 | np);
+            p.npieces += np;
             return 0;
         }
     };
@@ -602,7 +659,7 @@ class Decoder {
                             int32_t &zout);
     // the MCU loop of one scan, restart markers included (processSos
     // :1298-1455), from the scan's first entropy-coded byte
-    int scan_loop(const Scan &sc, bool records);
+    int scan_loop(const Scan &sc, bool pieces);
     int restart_parallel(const Scan &sc, bool &done);
     friend int run_deferred_scans(std::vector<std::unique_ptr<Decoder>> &jobs, JpegCoeffs &o, int threads);
     // the run() loop head from byte p: the position after the next marker
@@ -632,7 +689,7 @@ class Decoder {
     bool config_only_ = false;
     bool interleaved_[4] = {}, noninterleaved_[4] = {};
     int threads_ = 1; // restart-interval-parallel Huffman (baseline scans with DRI)
-    bool sparse_ok_ = false; // emit JpegSparse records for a single interleaved baseline scan
+    bool sparse_ok_ = false; // emit JpegPieces for a single interleaved baseline scan
   public:
     // Progressive scans decoded in parallel (run_deferred_scans): the first
     // pass walks the markers and, at each SOS, keeps a copy of the decoder --
@@ -898,34 +955,38 @@ int Decoder::sos(int32_t n)
     const int32_t myy = (static_cast<int32_t>(o_.height) + 8 * v0 - 1) / (8 * v0);
     o_.mxx = mxx;
     o_.myy = myy;
-    if (o_.sparse.valid) return kSparseAbort; // a second scan after a record scan: redo with grids
-    bool records = sparse_ok_ && !seen_sos_ && !o_.progressive && ns == 3 && o_.n_comp == 3 &&
+    if (o_.pieces.valid) return kSparseAbort; // a second scan after a pieces scan: redo with grids
+    bool pieces = sparse_ok_ && !seen_sos_ && !o_.progressive && ns == 3 && o_.n_comp == 3 &&
                    !(threads_ > 1 && restart_interval_ > 0);
     seen_sos_ = true;
-    int32_t bpm = 0;
-    for (int k = 0; k < ns; k++) bpm += o_.comp[scan[k].id].h * o_.comp[scan[k].id].v;
-    const size_t nrec = size_t(mxx) * size_t(myy) * size_t(bpm);
-    // every coefficient costs at least two bits of entropy-coded data, plus
-    // one DC entry per block; never more than dense int16
-    const size_t bound = std::min(3 * (4 * len_ + nrec), nrec * (64 * 3));
-    // the device reads every 64th record's byte offset as a uint32: a frame
-    // whose records could pass 4 GiB takes grids
-    if (bound > size_t(UINT32_MAX)) records = false;
-    if (records) {
-        JpegSparse &sp = o_.sparse;
-        if (!sp.counts.alloc(nrec, false) || !sp.data.alloc(bound, false)) return ZPX_E_OUT_OF_MEMORY;
-        sp.cap = bound;
-        sp.nrec = sp.bytes = 0;
-        sp.ns = ns;
-        for (int k = 0; k < ns; k++) sp.scan_comp[k] = scan[k].id;
-        sp.valid = true;
+    size_t nblocks = 0;
+    for (int c = 0; c < o_.n_comp; c++) nblocks += size_t(mxx) * size_t(myy) * size_t(o_.comp[c].h * o_.comp[c].v);
+    // int16 worst case: 8 pieces a block, plus the zero piece; the index
+    // holds a piece number in 28 bits
+    const size_t cap = 1 + 8 * nblocks;
+    if (cap >= (size_t(1) << 28)) pieces = false;
+    if (pieces) {
+        JpegPieces &pc = o_.pieces;
+        if (!pc.index.alloc(nblocks * sizeof(uint32_t), true) || !pc.data.alloc(cap * 16, false))
+            return ZPX_E_OUT_OF_MEMORY;
+        size_t first = 0;
+        for (int c = 0; c < o_.n_comp; c++) {
+            pc.first[c] = first;
+            pc.blocks[c] = size_t(mxx) * size_t(myy) * size_t(o_.comp[c].h * o_.comp[c].v);
+            first += pc.blocks[c];
+        }
+        memset(pc.data.ptr, 0, 16); // piece 0
+        pc.cap = cap;
+        pc.npieces = 1;
+        pc.bits = 8;
+        pc.valid = true;
     }
     // Grids: like progressive_coefficients, allocated for scan[i].id over
     // i < n_comp (:1269-1282; slots past ns read component 0).  A baseline
     // scan interleaving several components writes every block of every MCU,
     // so its grids need no clearing.
     const bool full_cover = !o_.progressive && ns > 1;
-    for (int i = 0; i < o_.n_comp && !records; i++) {
+    for (int i = 0; i < o_.n_comp && !pieces; i++) {
         const int ci = scan[i].id;
         if (!o_.has_grid[ci]) {
             const size_t nb = size_t(mxx) * size_t(myy) * size_t(o_.comp[ci].h * o_.comp[ci].v);
@@ -973,18 +1034,18 @@ int Decoder::sos(int32_t n)
         unread_ = 0;
         return 0;
     }
-    ZTRY(scan_loop(sc, records));
+    ZTRY(scan_loop(sc, pieces));
     // baseline reconstructs during the scan with the table current now
     if (!o_.progressive)
         for (int k = 0; k < ns; k++) snapshot_quant(scan[k].id);
     return 0;
 }
 
-int Decoder::scan_loop(const Scan &sc, bool records)
+int Decoder::scan_loop(const Scan &sc, bool pieces)
 {
     const int32_t mxx = sc.mxx, myy = sc.myy;
     bool done = false;
-    if (!records) ZTRY(restart_parallel(sc, done));
+    if (!pieces) ZTRY(restart_parallel(sc, done));
     if (!done) {
         int32_t mcu_i = 0, block_count = 0;
         uint8_t expected_rst = 0xd0;
@@ -993,10 +1054,10 @@ int Decoder::scan_loop(const Scan &sc, bool records)
         uint8_t nzpos[64];
         memset(b, 0, sizeof(b));
         SerialSink serial{o_};
-        RecordSink rec{o_.sparse};
+        PieceSink rec{o_.pieces};
         for (int32_t my = 0; my < myy; my++) {
             for (int32_t mx = 0; mx < mxx; mx++) {
-                ZTRY(records ? mcu(sc, my, mx, block_count, dc, b, nzpos, rec)
+                ZTRY(pieces ? mcu(sc, my, mx, block_count, dc, b, nzpos, rec)
                              : mcu(sc, my, mx, block_count, dc, b, nzpos, serial));
                 mcu_i++;
                 if (restart_interval_ > 0 && mcu_i % restart_interval_ == 0 && mcu_i < mxx * myy) {
@@ -1599,7 +1660,7 @@ int run_deferred_scans(std::vector<std::unique_ptr<Decoder>> &jobs, JpegCoeffs &
 
 } // namespace
 
-int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads, bool sparse)
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads, bool pieces)
 {
     try { // no exception crosses the ABI
         int e = 0;
@@ -1613,7 +1674,7 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int thr
             // without deferred scans was decoded by this run as usual
             std::vector<std::unique_ptr<Decoder>> jobs;
             {
-                Decoder d(buf, len, out, false, threads, sparse);
+                Decoder d(buf, len, out, false, threads, pieces);
                 d.deferred_ = &jobs;
                 e = d.run();
             }
@@ -1621,27 +1682,16 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int thr
             if (!decoded) out = JpegCoeffs{}; // the serial loop from the start
         }
         if (!decoded) {
-            Decoder d(buf, len, out, false, threads, sparse);
+            Decoder d(buf, len, out, false, threads, pieces);
             e = d.run();
         }
-        if (e == kSparseAbort) { // records could not hold this frame: grids from the start
+        if (e == kSparseAbort) { // pieces could not hold this frame: grids from the start
             out = JpegCoeffs{};
             Decoder d(buf, len, out, false, threads, false);
             e = d.run();
         }
         if (e) return e;
-        if (out.sparse.valid) { // byte offset of every 64th record
-            JpegSparse &sp = out.sparse;
-            if (!sp.groups.alloc(sp.groups_bytes(), false)) return ZPX_E_OUT_OF_MEMORY;
-            const uint8_t *cnt = static_cast<const uint8_t *>(sp.counts.ptr);
-            uint32_t *g = static_cast<uint32_t *>(sp.groups.ptr);
-            size_t off = 0;
-            for (size_t r = 0; r < sp.nrec; r++) {
-                if (r % 64 == 0) g[r / 64] = static_cast<uint32_t>(off);
-                off += 3 * size_t(cnt[r]);
-            }
-            return ZPX_OK;
-        }
+        if (out.pieces.valid) return ZPX_OK;
         // one width per frame (the kernels take one coefficient type per frame)
         int bits = 8;
         for (int i = 0; i < 4; i++)

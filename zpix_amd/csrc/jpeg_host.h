@@ -89,19 +89,31 @@ class CoeffGrid {
     int32_t max_abs_ = 0;
 };
 
-// Sparse coefficient records: the batch pipeline's H2D form of a baseline
-// interleaved scan.  One record per block in decode (MCU)
-// order -- n natural-order positions (u8), then n values (i16 little endian)
-// -- and a u8 count per record; `groups` holds the byte offset of every 64th
-// record.  Expanded into dense grids on the device (launch_jpeg_sparse_expand).
-struct JpegSparse {
+// Compact coefficient blocks ("pieces"): the batch pipeline's H2D form of a
+// baseline frame whose one scan interleaves every component.
+// A block keeps its coefficients in zig-zag order up to its last nonzero one
+// (the end of block of processSos, src/jpeg/decoder.zig:1300-1345) as whole
+// 16-byte pieces of int8 (16 coefficients a piece) or int16 (8) values, the
+// rest of the last piece zero; piece 0 is all zeros.  Per component a u32 per
+// block, in grid order, indexes them:
+//   index = first piece << 4 | pieces   (pieces 0: the block is all zeros)
+// The block kernels read the pieces straight into their LDS coefficient
+// image -- a piece past a block's count reads piece 0 -- so no dense grid is
+// ever written or read back (jpeg_block_kernels.hip); the other kernels take
+// grids expanded from them on the device (launch_jpeg_pieces_expand).
+// The width starts at int8 and is widened (every piece so far copied) the
+// first time a value does not fit.
+struct JpegPieces {
     bool valid = false;
-    HostBuf counts, data, groups;
-    size_t nrec = 0, bytes = 0, cap = 0;
+    int bits = 8;                 // 8 or 16: the values of every piece
+    HostBuf data;                 // npieces x 16 bytes
+    HostBuf index;                // u32 per block: component c's blocks from first[c]
+    size_t first[4] = {0, 0, 0, 0}, blocks[4] = {0, 0, 0, 0};
+    size_t npieces = 0, cap = 0;  // pieces written / allocated
     int32_t max_abs[4] = {0, 0, 0, 0};
-    int ns = 0;
-    int scan_comp[4] = {0, 0, 0, 0}; // component of each scan slot (record order within an MCU)
-    size_t groups_bytes() const { return ((nrec + 63) / 64) * sizeof(uint32_t); }
+    size_t data_bytes() const { return npieces * 16; }
+    uint32_t *index_of(int c) const { return static_cast<uint32_t *>(index.ptr) + first[c]; }
+    bool widen(); // int8 -> int16 pieces
 };
 
 struct JpegCoeffs {
@@ -118,7 +130,7 @@ struct JpegCoeffs {
     // quant table each component is reconstructed with, natural order
     int32_t qt_natural[4][64] = {};
     int32_t max_q[4] = {0, 0, 0, 0};
-    JpegSparse sparse; // valid: the scan's coefficients are records, not grids
+    JpegPieces pieces; // valid: the scan's coefficients are compact pieces, not grids
 };
 
 // Decode `buf` into coefficient grids.  Returns ZPX_E_* (ZPX_E_OK on success),
@@ -128,10 +140,10 @@ struct JpegCoeffs {
 // threads > 1: baseline scans with a restart interval decode their restart
 // segments in parallel (identical result; anything irregular falls back to
 // the serial loop).
-// sparse: a baseline frame whose one scan interleaves every component (and is
-// not split by restart intervals over threads) is decoded into out.sparse
-// records instead of grids; anything else decodes into grids as usual.
-int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads = 1, bool sparse = false);
+// pieces: a baseline frame whose one scan interleaves every component (and is
+// not split by restart intervals over threads) is decoded into out.pieces
+// instead of grids; anything else decodes into grids as usual.
+int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int threads = 1, bool pieces = false);
 // default thread count of the single-image entry points: ZPX_HUFF_THREADS,
 // else min(8, hardware threads)
 int jpeg_huff_threads();

@@ -505,12 +505,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5))) v
 // launchers
 // ---------------------------------------------------------------------------
 int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &geom, int coeff_bits,
-                       bool narrow, hipStream_t stream)
+                       bool narrow, bool pieces, hipStream_t stream)
 {
     // the block-per-lane kernel (jpeg_block_kernels.hip) takes the narrow
     // int8 / int16 frames; the test switch "jpeg_strip" forces this one
+    if (pieces) return launch_jpeg_plane_block(d_frames, n_frames, geom, coeff_bits, narrow, true, stream);
     if (opt(Opt::JpegStrip) == 0) {
-        const int rc = launch_jpeg_plane_block(d_frames, n_frames, geom, coeff_bits, narrow, stream);
+        const int rc = launch_jpeg_plane_block(d_frames, n_frames, geom, coeff_bits, narrow, false, stream);
         if (rc != -2) return rc;
     }
     int max_gw = 0, max_gh = 0;
@@ -619,14 +620,19 @@ bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc)
 }
 
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc,
-                     int vc, int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, hipStream_t stream)
+                     int vc, int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, bool pieces,
+                     hipStream_t stream)
 {
     // the block-per-lane kernel (jpeg_block_kernels.hip) takes the common
     // frames; the test switch "jpeg_strip" forces the strip kernel
+    if (pieces)
+        return vec_out ? launch_jpeg_block(d_frames, n_frames, color, h0, v0, hc, vc, max_mxx, max_myy, coeff_bits,
+                                           narrow, true, stream)
+                       : -2;
     const bool strip_only = opt(Opt::JpegStrip) != 0;
     if (vec_out && !strip_only) {
         const int rc = launch_jpeg_block(d_frames, n_frames, color, h0, v0, hc, vc, max_mxx, max_myy, coeff_bits,
-                                         narrow, stream);
+                                         narrow, false, stream);
         if (rc != -2) return rc;
     }
     const int key = (h0 << 12) | (v0 << 8) | (hc << 4) | vc;

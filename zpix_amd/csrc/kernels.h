@@ -19,20 +19,29 @@ struct JpegPlaneGeom {
     int h[4] = {1, 1, 1, 1}, v[4] = {1, 1, 1, 1};
     int max_mxx = 0, max_myy = 0;
 };
+// pieces: the frames are ZPX_COEFFS_PIECES (only the block kernels read
+// them: -2 when they do not take the frames -- expand them first)
 int launch_jpeg_planar(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &geom, int coeff_bits,
-                       bool narrow, hipStream_t stream);
+                       bool narrow, bool pieces, hipStream_t stream);
 bool jpeg_rgba_supported(int color, int h0, int v0, int hc, int vc);
 // vec_out: every frame's RGBA rows are dword aligned (jpeg_rgba_vec_out:
 // the block-per-lane kernel's store layout)
 int launch_jpeg_rgba(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
-                     int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, hipStream_t stream);
+                     int max_mxx, int max_myy, int coeff_bits, bool narrow, bool vec_out, bool pieces,
+                     hipStream_t stream);
 
 // jpeg_block_kernels.hip: -2 when the frame kind is not one it takes
 int launch_jpeg_block(const DevJpegFrame *d_frames, int n_frames, int color, int h0, int v0, int hc, int vc,
-                      int max_mxx, int max_myy, int coeff_bits, bool narrow, hipStream_t stream);
+                      int max_mxx, int max_myy, int coeff_bits, bool narrow, bool pieces, hipStream_t stream);
+// the fused kernel's ZPX_COEFFS_PIECES instances: YCbCr 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4
+bool jpeg_block_pieces_supported(int color, int h0, int v0, int hc, int vc);
 // the planar block kernel (narrow int8 / int16 frames); -2 for the rest
 int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const JpegPlaneGeom &geom, int coeff_bits,
-                            bool narrow, hipStream_t stream);
+                            bool narrow, bool pieces, hipStream_t stream);
+// ZPX_COEFFS_PIECES -> dense natural-order grids (njobs components, up to
+// max_blocks blocks each)
+int launch_jpeg_pieces_expand(const DevPiecesExpand *jobs, int njobs, uint32_t max_blocks, int coeff_bits,
+                              hipStream_t stream);
 
 // png_kernels.hip
 // CUs of the current device (read once: the node's GPUs are alike; a
@@ -75,18 +84,6 @@ int launch_rgba_batch(int kind, const DevRgbaJob *jobs, int n, int max_w, int ma
 int launch_jpeg_rgb(const DevImage &m, int c_scale, uint8_t *out, hipStream_t s);
 int launch_jpeg_cmyk(const DevImage &m, const uint8_t *k_plane, uint64_t k_stride, uint32_t sub_mask,
                      uint8_t *out, hipStream_t s);
-
-// jpeg_sparse_kernels.hip: JpegSparse records -> dense coefficient grids
-struct DevJpegSparse {
-    const uint8_t *counts = nullptr;   // device: u8 per record
-    const uint32_t *groups = nullptr;  // device: byte offset of every 64th record
-    const uint8_t *data = nullptr;     // device: record bytes
-    uint64_t nrec = 0;
-    int32_t mxx = 0, ns = 0, bpm = 0;  // MCU columns, scan slots, blocks per MCU
-    int32_t h[4] = {}, v[4] = {}, gw[4] = {}; // per scan slot: sampling, grid blocks per row
-    void *grid[4] = {};                // per scan slot: the component's dense grid
-};
-int launch_jpeg_sparse_expand(const DevJpegSparse &a, int coeff_bits, hipStream_t s);
 
 // bmp_kernels.hip: the pixel loop of bmp.decode over the file's row data
 // (bpp 1/2/4/8 -> palette indices, 24 -> RGBA, 32 -> NRGBA)

@@ -198,6 +198,7 @@ DevJpegFrame zpx::dev_jpeg_frame(const zpx_jpeg_frame &f)
     d.myy = f.myy;
     d.n_comp = f.n_comp;
     d.color = f.color;
+    d.pieces = f.layout == ZPX_COEFFS_PIECES ? static_cast<const uint8_t *>(f.pieces) : nullptr;
     return d;
 }
 
@@ -229,7 +230,7 @@ int zpx::launch_jpeg_rgba_frame(const zpx_jpeg_frame &f, const DevJpegFrame *d_f
     const int h0 = f.n_comp == 1 ? 1 : f.h[0], v0 = f.n_comp == 1 ? 1 : f.v[0];
     const int hc = f.n_comp == 3 ? f.h[1] : 1, vc = f.n_comp == 3 ? f.v[1] : 1;
     return launch_jpeg_rgba(d_frame, 1, color, h0, v0, hc, vc, f.mxx, f.myy, f.coeff_bits, f.narrow != 0,
-                            jpeg_rgba_vec_out(f), st);
+                            jpeg_rgba_vec_out(f), f.layout == ZPX_COEFFS_PIECES, st);
 }
 
 bool zpx::jpeg_rgba_vec_out(const zpx_jpeg_frame &f)
@@ -278,7 +279,7 @@ int zpx::jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f
     memcpy(hdesc.ptr, &df, sizeof(df));
     HIPCHK(ctx, desc.reserve(sizeof(df)));
     HIPCHK(ctx, hipMemcpyAsync(desc.ptr, hdesc.ptr, sizeof(df), hipMemcpyHostToDevice, st));
-    if (launch_jpeg_planar(desc.as<DevJpegFrame>(), 1, jpeg_plane_geom(df), f.coeff_bits, f.narrow != 0, st))
+    if (launch_jpeg_planar(desc.as<DevJpegFrame>(), 1, jpeg_plane_geom(df), f.coeff_bits, f.narrow != 0, false, st))
         return hip_fail(ctx, hipGetLastError(), "jpeg planar kernel");
     zpx_image planar{};
     planar.kind = c.n_comp == 1 ? ZPX_GRAY : ZPX_YCBCR;
@@ -324,6 +325,13 @@ struct JpegGroup {
     int max_gw = 0, max_gh = 0, max_mxx = 0, max_myy = 0;
     bool vec_out = true; // every frame: dword-aligned RGBA rows (jpeg_rgba_vec_out)
     JpegPlaneGeom geom;  // planes output: the group's geometry (one per group)
+    // ZPX_COEFFS_PIECES frames: read by the block kernels directly (pieces),
+    // or expanded into the group's own dense grids at every launch first
+    // (expand_jobs; `frames` then points at the grids)
+    bool pieces = false;
+    DevBuf grids, expand_jobs;
+    int nexpand = 0;
+    uint32_t expand_max_blocks = 0;
 };
 struct PngGroup {
     int depth = 0;
@@ -355,6 +363,15 @@ struct zpx_plan {
     uint64_t bytes = 0;
 };
 
+// A group of ZPX_COEFFS_PIECES frames that the block kernels read directly
+// (the others are expanded into dense grids first)
+static bool jpeg_pieces_direct(int output, const JpegGroup &g)
+{
+    if (!g.narrow || (g.bits != 8 && g.bits != 16) || opt(Opt::JpegStrip) != 0) return false;
+    if (output == ZPX_JPEG_PLANES) return true;
+    return g.vec_out && jpeg_block_pieces_supported(g.color, g.h0, g.v0, g.hc, g.vc);
+}
+
 static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames, int n_frames, int output,
                                     zpx_plan **out)
 {
@@ -366,11 +383,15 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
     plan->ctx = ctx;
     plan->kind = output == ZPX_JPEG_PLANES ? 0 : 1;
     // group frames by kernel variant
-    std::map<std::tuple<int, int, int, int, int, int, int>, std::vector<int>> groups;
+    std::map<std::tuple<int, int, int, int, int, int, int, int>, std::vector<int>> groups;
     for (int i = 0; i < n_frames; i++) {
         const zpx_jpeg_frame &f = frames[i];
         if (f.n_comp != 1 && f.n_comp != 3 && f.n_comp != 4) return ZPX_E_INVALID_ARGUMENT;
         if (f.coeff_bits != 8 && f.coeff_bits != 16 && f.coeff_bits != 32) return ZPX_E_INVALID_ARGUMENT;
+        const int layout = f.layout;
+        if (layout != ZPX_COEFFS_GRID && layout != ZPX_COEFFS_PIECES) return ZPX_E_INVALID_ARGUMENT;
+        if (layout == ZPX_COEFFS_PIECES && (f.coeff_bits == 32 || !f.pieces || f.pieces_bytes < 16))
+            return ZPX_E_INVALID_ARGUMENT;
         int color = 0, hc = 1, vc = 1;
         if (output == ZPX_JPEG_RGBA) {
             color = f.n_comp == 1 ? ZPX_JPEG_COLOR_GRAY : f.color;
@@ -385,7 +406,7 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
             // through a buffer descriptor with a 31-bit range
             if (f.rgba_stride < size_t(f.width) * 4 || f.rgba_stride > (size_t(1) << 31) / 32)
                 return ZPX_E_INVALID_ARGUMENT;
-            groups[{f.coeff_bits, f.narrow, color, h0, v0, hc, vc}].push_back(i);
+            groups[{f.coeff_bits, f.narrow, color, h0, v0, hc, vc, layout}].push_back(i);
         } else {
             // one group per geometry (the planar kernel's task space); the
             // stores address 8 plane rows through a 31-bit buffer range
@@ -398,7 +419,7 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
                 hp |= d.h[c] << (4 * c);
                 vp |= d.v[c] << (4 * c);
             }
-            groups[{f.coeff_bits, f.narrow, f.n_comp, hp, vp, 0, 0}].push_back(i);
+            groups[{f.coeff_bits, f.narrow, f.n_comp, hp, vp, 0, 0, layout}].push_back(i);
         }
     }
     uint64_t bytes = 0;
@@ -411,6 +432,7 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
         g->v0 = std::get<4>(kv.first);
         g->hc = std::get<5>(kv.first);
         g->vc = std::get<6>(kv.first);
+        g->pieces = std::get<7>(kv.first) == ZPX_COEFFS_PIECES;
         std::vector<DevJpegFrame> df;
         for (int idx : kv.second) {
             const zpx_jpeg_frame &f = frames[idx];
@@ -421,9 +443,11 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
                 const int gw = f.mxx * d.h[c], gh = f.myy * d.v[c];
                 g->max_gw = std::max(g->max_gw, gw);
                 g->max_gh = std::max(g->max_gh, gh);
-                if (f.coeffs[c]) bytes += uint64_t(gw) * gh * 64 * esz;
+                // pieces: the index (4 B a block); the pieces themselves below
+                if (f.coeffs[c]) bytes += uint64_t(gw) * gh * (g->pieces ? 4 : 64 * esz);
                 if (output == ZPX_JPEG_PLANES) bytes += uint64_t(gw) * gh * 64;
             }
+            if (g->pieces) bytes += f.pieces_bytes;
             bytes += uint64_t(f.n_comp) * 64 * 4; // quant tables
             if (output == ZPX_JPEG_RGBA) bytes += uint64_t(f.width) * f.height * 4;
             g->vec_out = g->vec_out && jpeg_rgba_vec_out(f);
@@ -434,6 +458,39 @@ static int zpx_jpeg_plan_create_impl(zpx_ctx *ctx, const zpx_jpeg_frame *frames,
         g->geom.max_mxx = g->max_mxx;
         g->geom.max_myy = g->max_myy;
         g->n = static_cast<int>(df.size());
+        if (g->pieces && !jpeg_pieces_direct(output, *g)) {
+            // the kernel that takes these frames reads dense grids: expand the
+            // pieces into the group's own grids at every launch
+            std::vector<DevPiecesExpand> jobs;
+            size_t total = 0;
+            const size_t esz = g->bits / 8;
+            for (const DevJpegFrame &d : df)
+                for (int c = 0; c < d.n_comp; c++)
+                    if (d.coeffs[c]) total += (size_t(d.mxx) * d.h[c] * d.myy * d.v[c] * 64 * esz + 255) & ~size_t(255);
+            HIPCHK(ctx, g->grids.alloc(std::max<size_t>(total, 256)));
+            size_t off = 0;
+            for (DevJpegFrame &d : df) {
+                for (int c = 0; c < d.n_comp; c++) {
+                    if (!d.coeffs[c]) continue;
+                    const size_t blocks = size_t(d.mxx) * d.h[c] * d.myy * d.v[c];
+                    DevPiecesExpand j;
+                    j.index = static_cast<const uint32_t *>(d.coeffs[c]);
+                    j.pieces = d.pieces;
+                    j.grid = g->grids.as<uint8_t>() + off;
+                    j.blocks = static_cast<uint32_t>(blocks);
+                    jobs.push_back(j);
+                    g->expand_max_blocks = std::max(g->expand_max_blocks, j.blocks);
+                    d.coeffs[c] = j.grid;
+                    off += (blocks * 64 * esz + 255) & ~size_t(255);
+                }
+                d.pieces = nullptr;
+            }
+            g->nexpand = static_cast<int>(jobs.size());
+            HIPCHK(ctx, g->expand_jobs.alloc(std::max<size_t>(jobs.size(), 1) * sizeof(DevPiecesExpand)));
+            HIPCHK(ctx, hipMemcpy(g->expand_jobs.ptr, jobs.data(), jobs.size() * sizeof(DevPiecesExpand),
+                                  hipMemcpyHostToDevice));
+            g->pieces = false;
+        }
         HIPCHK(ctx, g->frames.alloc(df.size() * sizeof(DevJpegFrame)));
         HIPCHK(ctx, hipMemcpy(g->frames.ptr, df.data(), df.size() * sizeof(DevJpegFrame), hipMemcpyHostToDevice));
         plan->jpeg.push_back(std::move(g));
@@ -712,11 +769,14 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
             return hip_fail(ctx, hipGetLastError(), "rgba batch kernel launch");
     for (auto &g : plan->jpeg) {
         int rc;
+        if (g->nexpand && launch_jpeg_pieces_expand(g->expand_jobs.as<DevPiecesExpand>(), g->nexpand,
+                                                    g->expand_max_blocks, g->bits, st))
+            return hip_fail(ctx, hipGetLastError(), "jpeg pieces expand launch");
         if (plan->kind == 0)
-            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->geom, g->bits, g->narrow, st);
+            rc = launch_jpeg_planar(g->frames.as<DevJpegFrame>(), g->n, g->geom, g->bits, g->narrow, g->pieces, st);
         else
             rc = launch_jpeg_rgba(g->frames.as<DevJpegFrame>(), g->n, g->color, g->h0, g->v0, g->hc, g->vc,
-                                  g->max_mxx, g->max_myy, g->bits, g->narrow, g->vec_out, st);
+                                  g->max_mxx, g->max_myy, g->bits, g->narrow, g->vec_out, g->pieces, st);
         if (rc == -2) return ZPX_E_UNSUPPORTED;
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
@@ -781,7 +841,11 @@ extern "C" int zpx_plan_status(zpx_plan *plan, void *stream)
 extern "C" uint64_t zpx_plan_bytes(const zpx_plan *plan) { return plan ? plan->bytes : 0; }
 extern "C" int zpx_plan_kernel_count(const zpx_plan *plan)
 {
-    return plan ? static_cast<int>(plan->jpeg.size() + plan->png.size() + plan->rgba.size()) : 0;
+    if (!plan) return 0;
+    int n = static_cast<int>(plan->rgba.size());
+    for (auto &g : plan->jpeg) n += 1 + (g->nexpand ? 1 : 0);
+    for (auto &g : plan->png) n += 1 + (g->nslab_jobs ? 1 : 0) + (g->nsched2 ? 1 : 0);
+    return n;
 }
 extern "C" void zpx_plan_destroy(zpx_plan *plan)
 {
@@ -799,19 +863,24 @@ struct zpx_png_stream {
     std::mutex slab_mu; // zpx_png_stream_slab builds s.slab once, whichever thread asks first
 };
 
-static int zpx_jpeg_entropy_decode_impl(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
+static int zpx_jpeg_entropy_decode_impl(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out, bool pieces)
 {
     if (!out || (!buf && len)) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
     std::unique_ptr<zpx_jpeg_coeffs> c(new zpx_jpeg_coeffs);
-    if (int e = jpeg_entropy_decode(buf, len, c->c, jpeg_huff_threads())) return e;
+    if (int e = jpeg_entropy_decode(buf, len, c->c, jpeg_huff_threads(), pieces)) return e;
     *out = c.release();
     return ZPX_OK;
 }
 
 extern "C" int zpx_jpeg_entropy_decode(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
 {
-    return guarded([&] { return zpx_jpeg_entropy_decode_impl(buf, len, out); });
+    return guarded([&] { return zpx_jpeg_entropy_decode_impl(buf, len, out, false); });
+}
+
+extern "C" int zpx_jpeg_entropy_decode_pieces(const uint8_t *buf, size_t len, zpx_jpeg_coeffs **out)
+{
+    return guarded([&] { return zpx_jpeg_entropy_decode_impl(buf, len, out, true); });
 }
 
 void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_bytes)
@@ -834,12 +903,27 @@ void zpx::jpeg_fill_frame(const JpegCoeffs &c, zpx_jpeg_frame *f, size_t *coeff_
             m = std::max<int64_t>(m, int64_t(c.grid[i].max_abs()) * c.max_q[i]);
         }
     }
+    if (c.pieces.valid) {
+        bits = c.pieces.bits;
+        for (int i = 0; i < c.n_comp; i++) m = std::max<int64_t>(m, int64_t(c.pieces.max_abs[i]) * c.max_q[i]);
+    }
     f->coeff_bits = bits;
     f->narrow = m <= 16384 ? 1 : 0;
     switch (jpeg_output_kind(c)) {
     case JpegOut::Gray: f->color = ZPX_JPEG_COLOR_GRAY; break;
     case JpegOut::RGB: f->color = ZPX_JPEG_COLOR_RGB; break;
     default: f->color = ZPX_JPEG_COLOR_YCBCR; break;
+    }
+    if (c.pieces.valid) {
+        f->layout = ZPX_COEFFS_PIECES;
+        f->pieces = c.pieces.data.ptr;
+        f->pieces_bytes = c.pieces.data_bytes();
+        for (int i = 0; i < 4; i++) {
+            const bool g = i < c.n_comp;
+            f->coeffs[i] = g ? c.pieces.index_of(i) : nullptr;
+            if (coeff_bytes) coeff_bytes[i] = g ? c.pieces.blocks[i] * sizeof(uint32_t) : 0;
+        }
+        return;
     }
     for (int i = 0; i < 4; i++) {
         const bool g = i < c.n_comp && c.has_grid[i];
@@ -860,6 +944,10 @@ extern "C" void zpx_jpeg_coeffs_free(zpx_jpeg_coeffs *c) { delete c; }
 extern "C" int zpx_jpeg_coeffs_widen(zpx_jpeg_coeffs *cc, int bits)
 {
     if (!cc || (bits != 8 && bits != 16 && bits != 32)) return ZPX_E_INVALID_ARGUMENT;
+    if (cc->c.pieces.valid) { // pieces are int8 or int16
+        if (bits == 32) return ZPX_E_UNSUPPORTED;
+        return bits == 16 && !cc->c.pieces.widen() ? ZPX_E_OUT_OF_MEMORY : ZPX_OK;
+    }
     for (int i = 0; i < 4; i++)
         if (cc->c.has_grid[i] && !cc->c.grid[i].widen_to(bits)) return ZPX_E_OUT_OF_MEMORY;
     return ZPX_OK;
@@ -1436,49 +1524,59 @@ extern "C" int zpx_debug_png_stall(zpx_ctx *ctx, uint32_t spin_limit, double *se
 extern "C" int64_t zpx_debug_jpeg_parallel_scans(void) { return jpeg_parallel_scans(); }
 extern "C" int64_t zpx_debug_jpeg_parallel_progressive(void) { return jpeg_parallel_progressive(); }
 
-// Test hook for the sparse coefficient records (JpegSparse): decodes `buf` in
-// record mode and expands the records on the host with the mapping of
-// jpeg_sparse_expand_kernel, into int32 grids laid out component after
-// component (blocks x 64, natural order).  Returns the number of records, 0
-// when the frame was decoded into grids instead, or -(error code).
+// Test hook for the compact coefficient pieces (JpegPieces): decodes `buf`
+// in pieces mode and expands them on the host, as jpeg_pieces_expand_kernel
+// does, into int32 grids laid out component after component (blocks x 64,
+// natural order), checking the layout's invariants on the way (piece 0 zero,
+// every block's pieces inside the data and in order, nothing nonzero past a
+// block's last piece's values).  Returns the number of blocks, 0 when the
+// frame was decoded into grids instead, or -(error code).
 extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, int32_t *grids, size_t grid_elems)
 {
     return guarded([&]() -> int64_t {
         JpegCoeffs c;
         if (int e = jpeg_entropy_decode(buf, len, c, 1, true)) return -int64_t(e);
-        const JpegSparse &sp = c.sparse;
-        if (!sp.valid) return 0;
-        size_t base[4] = {}, total = 0;
+        const JpegPieces &p = c.pieces;
+        if (!p.valid) return 0;
+        size_t total = 0, blocks = 0;
         for (int i = 0; i < c.n_comp; i++) {
-            base[i] = total;
-            total += size_t(c.mxx) * c.myy * c.comp[i].h * c.comp[i].v * 64;
+            total += p.blocks[i] * 64;
+            blocks += p.blocks[i];
         }
         if (total > grid_elems) return -int64_t(ZPX_E_INVALID_ARGUMENT);
-        memset(grids, 0, total * sizeof(int32_t));
-        int bpm = 0;
-        for (int k = 0; k < sp.ns; k++) bpm += c.comp[sp.scan_comp[k]].h * c.comp[sp.scan_comp[k]].v;
-        const uint8_t *cnt = static_cast<const uint8_t *>(sp.counts.ptr);
-        const uint8_t *data = static_cast<const uint8_t *>(sp.data.ptr);
-        const uint32_t *groups = static_cast<const uint32_t *>(sp.groups.ptr);
-        size_t off = 0;
-        for (size_t r = 0; r < sp.nrec; r++) {
-            if (r % 64 == 0 && groups[r / 64] != off) return -int64_t(ZPX_E_PANIC);
-            const size_t mcu = r / bpm;
-            int t = static_cast<int>(r % bpm), k = 0;
-            while (k + 1 < sp.ns && t >= c.comp[sp.scan_comp[k]].h * c.comp[sp.scan_comp[k]].v) {
-                t -= c.comp[sp.scan_comp[k]].h * c.comp[sp.scan_comp[k]].v;
-                k++;
+        const uint8_t *data = static_cast<const uint8_t *>(p.data.ptr);
+        for (int k = 0; k < 16; k++)
+            if (data[k]) return -int64_t(ZPX_E_PANIC);
+        static const uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                        12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                        35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                        58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+        const int per = p.bits == 8 ? 16 : 8;
+        int32_t *o = grids;
+        for (int ci = 0; ci < c.n_comp; ci++) {
+            const uint32_t *ix = p.index_of(ci);
+            for (size_t blk = 0; blk < p.blocks[ci]; blk++, o += 64) {
+                const uint32_t np = ix[blk] & 15, first = ix[blk] >> 4;
+                for (int i = 0; i < 64; i++) o[i] = 0;
+                if (np == 0) {
+                    if (first != 0) return -int64_t(ZPX_E_PANIC);
+                    continue;
+                }
+                if (first == 0 || first + np > p.npieces || np * static_cast<uint32_t>(per) > uint32_t(64 + per - 1)) return -int64_t(ZPX_E_PANIC);
+                for (uint32_t z = 0; z < np * per && z < 64; z++) {
+                    int32_t v;
+                    if (p.bits == 8) {
+                        v = static_cast<int8_t>(data[size_t(first) * 16 + z]);
+                    } else {
+                        int16_t h;
+                        memcpy(&h, data + size_t(first) * 16 + 2 * z, 2);
+                        v = h;
+                    }
+                    o[kZz[z]] = v;
+                }
             }
-            const int ci = sp.scan_comp[k], h = c.comp[ci].h, v = c.comp[ci].v;
-            const size_t my = mcu / c.mxx, mx = mcu % c.mxx;
-            const size_t bx = h * mx + t % h, by = v * my + t / h;
-            int32_t *blk = grids + base[ci] + (by * size_t(c.mxx * h) + bx) * 64;
-            const uint8_t *d = data + off;
-            const int n = cnt[r];
-            for (int i = 0; i < n; i++) blk[d[i]] = static_cast<int16_t>(d[n + 2 * i] | d[n + 2 * i + 1] << 8);
-            off += 3 * size_t(n);
         }
-        return off == sp.bytes ? int64_t(sp.nrec) : -int64_t(ZPX_E_PANIC);
+        return int64_t(blocks);
     });
 }
 

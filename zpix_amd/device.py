@@ -92,7 +92,7 @@ class _Plan:
 class JpegBatch:
     """A batch of JPEG frames resident in HBM, reconstructed by one plan.
 
-    items: host entropy results (`jpeg.Coefficients`); `slots[i]` picks which
+    items: host entropy results (`jpeg.Coefficients`, grids or pieces); `slots[i]` picks which
     item fills device slot i (a slot owns its own copy of the grids and its
     own output, so repeating an item does not share any buffer).
     output: "rgba" (fused reconstruct + rgbaPixels) or "planes".
@@ -107,7 +107,9 @@ class JpegBatch:
         self.slots = list(range(len(items))) if slots is None else list(slots)
         self.output = output
         frames = (_lib.zpx_jpeg_frame * len(self.slots))()
+        # (a pieces frame: its index arrays in coeff_bytes, then its pieces)
         in_bytes = sum(_align(b) for i in self.slots for b in items[i].coeff_bytes)
+        in_bytes += sum(_align(int(items[i].frame.pieces_bytes)) for i in self.slots if items[i].frame.layout == 1)
         self.layouts = [jpeg_layout(items[i].frame) for i in self.slots]
         if output == "rgba":
             out_sizes = [_align(items[i].frame.width * items[i].frame.height * 4) for i in self.slots]
@@ -130,6 +132,12 @@ class JpegBatch:
                 host = np.ctypeslib.as_array(C.cast(items[i].frame.coeffs[c], C.POINTER(C.c_uint8)), shape=(n,))
                 self.coeff_arena[off_in:off_in + n].copy_(torch.from_numpy(host), non_blocking=False)
                 f.coeffs[c] = base_in + off_in
+                off_in += _align(n)
+            if f.layout == 1:
+                n = int(f.pieces_bytes)
+                host = np.ctypeslib.as_array(C.cast(items[i].frame.pieces, C.POINTER(C.c_uint8)), shape=(n,))
+                self.coeff_arena[off_in:off_in + n].copy_(torch.from_numpy(host), non_blocking=False)
+                f.pieces = base_in + off_in
                 off_in += _align(n)
             self.out_offsets.append(off_out)
             if output == "rgba":
