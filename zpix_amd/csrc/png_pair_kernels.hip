@@ -105,10 +105,16 @@ ZPX_PAIR_TRAITS(ZPX_PNG_TCA16, 8, 8)
 // loads, 64 rows per instruction, are the limit rather than issue
 // (tools/ubench/png_load_pattern: this load shape alone reads the stream at
 // 2.2 TB/s).  So FL stays 8.
+#ifndef ZPX_PNG_FL
+#define ZPX_PNG_FL 8
+#endif
+#ifndef ZPX_PNG_W
+#define ZPX_PNG_W 1
+#endif
 template <int DEPTH, bool MERGE>
 struct PairShape {
-    static constexpr int FL = 8;
-    static constexpr int W = 1;
+    static constexpr int FL = MERGE ? 8 : ZPX_PNG_FL;
+    static constexpr int W = MERGE ? 1 : ZPX_PNG_W;
 };
 
 // ---- packed 16-bit helpers (v_pk_*_u16, v_pk_add_f16)
@@ -349,7 +355,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
     // mod 32) spread with the rows' skews instead of colliding along a chain
     constexpr int RS = ZPX_PNG_RING_SWZ ? kSlots * 4 : kSlots * 4 + 4;
     auto rslot = [](int k, int row) {
-        return ((k & (kSlots - 1)) ^ (ZPX_PNG_RING_SWZ ? 8 * ((row >> 1) & 1) : 0)) * 4;
+        return ((k & (kSlots - 1)) ^ (ZPX_PNG_RING_SWZ ? (kSlots / 2) * ((row >> 1) & 1) : 0)) * 4;
     };
     constexpr int WG = kG * CW;             // boundary granules of one window (kG chunks)
     static_assert(WG % 2 == 0 && WG / 2 <= 64, "window loads are granule pairs, one per lane");
