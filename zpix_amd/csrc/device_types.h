@@ -34,13 +34,16 @@ struct DevPiecesExpand {
 };
 
 // The planar block kernel's task space for one plan group (frames of one
-// geometry): per component c, rows[c] block rows of segs[c] 64-block
-// segments, tasks start[c] .. start[c+1) of every frame (start[c] =
-// per_frame for absent components).
+// geometry), MCU row by MCU row: in each, per component c, vrows[c] block
+// rows of segs[c] 64-block segments, tasks start[c] .. start[c+1) of the
+// MCU row (start[c] = per_row for absent components) -- so the tasks that
+// read one MCU row's coefficients run together (a ZPX_COEFFS_PIECES frame
+// keeps an MCU's blocks side by side).
 struct PlaneTaskGeom {
     int32_t segs[4], rows[4], start[4];
     int32_t hh[4], vv[4];    // 8 * h0 / h_c, 8 * v0 / v_c: the progressive block rule (decoder.zig:1649-1651)
-    int32_t per_frame, total;
+    int32_t vrows[4];        // block rows of component c per MCU row (v_c)
+    int32_t per_row, per_frame, total;
 };
 
 // One PNG unfilter job: a (pass of a) PNG image.  Rows are processed by the

@@ -70,7 +70,21 @@ __device__ __forceinline__ void wave_lds_order()
 //     whole-line stores (two half-line stores per lane: 1.35 / 1.72 ms
 //     against 1.26);
 //   - workgroups renumbered so that one XCD holds consecutive tasks (1.7 %).
-constexpr int kWavesPerEu8 = 3, kWavesPerEu16 = 2;
+#ifndef ZPX_JPEG_W8
+#define ZPX_JPEG_W8 3
+#endif
+constexpr int kWavesPerEu8 = ZPX_JPEG_W8, kWavesPerEu16 = 2;
+#ifndef ZPX_JPEG_W444
+#define ZPX_JPEG_W444 3
+#endif
+// waves per EU of an instance (the dense 4:4:4 int8 instance: ZPX_JPEG_W444,
+// an A/B knob; its pieces twin spills at 4)
+template <typename CoefT, int H0, int V0, int HC, int VC, bool ZZ>
+constexpr int block_waves_per_eu()
+{
+    return sizeof(CoefT) == 2 ? kWavesPerEu16
+                              : (!ZZ && H0 == 1 && V0 == 1 && HC == 1 && VC == 1 ? ZPX_JPEG_W444 : kWavesPerEu8);
+}
 constexpr int kStoreAux = 2; // nt
 
 // Samples stay in the signed domain (sample - 128, the IDCT's clamp range
@@ -382,7 +396,7 @@ __device__ __forceinline__ void static_for(F &&f)
 }
 
 template <typename CoefT, bool NARROW, int H0, int V0, int HC, int VC, int COLOR, bool ZZ = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(CoefT) == 2 ? kWavesPerEu16 : kWavesPerEu8)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(block_waves_per_eu<CoefT, H0, V0, HC, VC, ZZ>())))
 void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int tasks_per_frame, int total_tasks)
 {
     constexpr bool kGray = COLOR == ZPX_JPEG_COLOR_GRAY;
@@ -874,10 +888,13 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
         PTask k;
         const int f = t / geo.per_frame;
         const int r = t - f * geo.per_frame;
-        const int c = (r >= geo.start[1]) + (r >= geo.start[2]) + (r >= geo.start[3]);
-        const int rr = r - geo.start[c];
-        k.by = rr / geo.segs[c];
-        k.bx0 = (rr - k.by * geo.segs[c]) * 64;
+        const int my = r / geo.per_row; // the MCU row, then its component c's block rows
+        const int q = r - my * geo.per_row;
+        const int c = (q >= geo.start[1]) + (q >= geo.start[2]) + (q >= geo.start[3]);
+        const int rr = q - geo.start[c];
+        const int yr = rr / geo.segs[c];
+        k.by = my * geo.vrows[c] + yr;
+        k.bx0 = (rr - yr * geo.segs[c]) * 64;
         const auto &fr = *(reinterpret_cast<CFrame>(reinterpret_cast<uintptr_t>(frames)) + f);
         k.grid = uptr(fr.coeffs[c]);
         k.plane = uptr(fr.planes[c]);
@@ -1095,22 +1112,26 @@ int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const Jp
     if (!narrow || (coeff_bits != 8 && coeff_bits != 16)) return -2;
     if (g.ncomp < 1 || g.ncomp > 4) return -2;
     PlaneTaskGeom geo{};
-    int64_t per = 0;
+    int64_t row = 0; // tasks per MCU row
     for (int c = 0; c < 4; c++) {
-        geo.start[c] = static_cast<int32_t>(per);
+        geo.start[c] = static_cast<int32_t>(row);
+        geo.segs[c] = 1;
         if (c >= g.ncomp) continue;
         if (g.h[c] <= 0 || g.v[c] <= 0) return -2;
         const int gw = g.max_mxx * g.h[c];
         geo.segs[c] = (gw + 63) / 64;
         geo.rows[c] = g.max_myy * g.v[c];
+        geo.vrows[c] = g.v[c];
         geo.hh[c] = 8 * (g.h[0] / g.h[c]);
         geo.vv[c] = 8 * (g.v[0] / g.v[c]);
-        per += int64_t(geo.segs[c]) * geo.rows[c];
+        row += int64_t(geo.segs[c]) * g.v[c];
     }
-    for (int c = g.ncomp; c < 4; c++) geo.start[c] = static_cast<int32_t>(per);
+    for (int c = g.ncomp; c < 4; c++) geo.start[c] = static_cast<int32_t>(row);
+    const int64_t per = row * g.max_myy;
     const int64_t total = per * n_frames;
-    if (total <= 0) return 0;
+    if (total <= 0 || row <= 0) return 0;
     if (total >= (int64_t(1) << 31)) return -2;
+    geo.per_row = static_cast<int32_t>(row);
     geo.per_frame = static_cast<int32_t>(per);
     geo.total = static_cast<int32_t>(total);
     auto kernel = pieces ? (coeff_bits == 8 ? jpeg_plane_block_kernel<int8_t, true> : jpeg_plane_block_kernel<int16_t, true>)
