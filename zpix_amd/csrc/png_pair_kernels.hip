@@ -104,7 +104,9 @@ ZPX_PAIR_TRAITS(ZPX_PNG_TCA16, 8, 8)
 // image starts at once and waits for the band above it, and the input
 // loads, 64 rows per instruction, are the limit rather than issue
 // (tools/ubench/png_load_pattern: this load shape alone reads the stream at
-// 2.2 TB/s).  So FL stays 8.
+// 2.2 TB/s).  Re-measured on the band slab (round 4, ZPX_PNG_FL=4
+// ZPX_PNG_W=2: 256 VGPRs, 17.9 KiB of LDS, no scratch): 2.335 / 2.355 ms
+// against 1.778 / 1.767 (gpurun_out/pnga).  So FL stays 8.
 #ifndef ZPX_PNG_FL
 #define ZPX_PNG_FL 8
 #endif
