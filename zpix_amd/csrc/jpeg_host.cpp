@@ -303,7 +303,7 @@ bool JpegPieces::widen()
 {
     if (bits == 16) return true;
     HostBuf nd;
-    if (!nd.alloc(cap * 16, false)) return false;
+    if (!nd.alloc((cap + 8) * 16, false)) return false;
     uint8_t *o = static_cast<uint8_t *>(nd.ptr);
     const int8_t *src = static_cast<const int8_t *>(data.ptr);
     memset(o, 0, 16);
@@ -572,32 +572,33 @@ class Decoder {
         JpegPieces &p;
         int put(int ci, size_t blk, int32_t *b, const uint8_t *pos, int n)
         {
-            // pos[] is in decode (zig-zag) order: the end of block follows
-            // the last nonzero entry (the DC entry is listed even when zero)
             int32_t m = p.max_abs[ci];
-            int eob = 0;
             for (int i = 0; i < n; i++) {
                 const int32_t v = b[pos[i]];
                 const int32_t a = v < 0 ? -v : v;
-                if (a > 32767 || v == INT32_MIN) return kSparseAbort;
-                m = a > m ? a : m;
-                if (v != 0) eob = kZigOf.z[pos[i]] + 1;
+                if (a > m || a < 0) m = a < 0 ? INT32_MAX : a;
             }
+            if (m > 32767) return kSparseAbort;
             p.max_abs[ci] = m;
             if (p.bits == 8 && m > 127 && !p.widen()) return kSparseAbort;
+            // pos[] is in decode (zig-zag) order and every AC entry is
+            // nonzero: the end of block follows the last entry, unless the
+            // block's only entry is a zero DC
             uint32_t &ix = p.index_of(ci)[blk];
-            if (eob == 0) {
+            if (n == 0 || (n == 1 && b[pos[0]] == 0)) {
                 ix = 0;
                 return 0;
             }
-            const int per = p.bits == 8 ? 16 : 8; // coefficients a piece
-            const size_t np = static_cast<size_t>((eob + per - 1) / per);
-            if (p.npieces + np > p.cap) return kSparseAbort;
+            const int eob = kZigOf.z[pos[n - 1]] + 1;
             uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + p.npieces * 16;
-            memset(d, 0, np * 16);
-            if (p.bits == 8) {
+            size_t np;
+            if (p.bits == 8) { // (the whole 64-byte block cleared: the data has that slack)
+                np = static_cast<size_t>((eob + 15) >> 4);
+                memset(d, 0, 64);
                 for (int i = 0; i < n; i++) reinterpret_cast<int8_t *>(d)[kZigOf.z[pos[i]]] = static_cast<int8_t>(b[pos[i]]);
             } else {
+                np = static_cast<size_t>((eob + 7) >> 3);
+                memset(d, 0, 128);
                 for (int i = 0; i < n; i++) {
                     const int16_t v = static_cast<int16_t>(b[pos[i]]);
                     memcpy(d + 2 * kZigOf.z[pos[i]], &v, 2);
@@ -967,7 +968,8 @@ int Decoder::sos(int32_t n)
     if (cap >= (size_t(1) << 28)) pieces = false;
     if (pieces) {
         JpegPieces &pc = o_.pieces;
-        if (!pc.index.alloc(nblocks * sizeof(uint32_t), true) || !pc.data.alloc(cap * 16, false))
+        // (+8 pieces: a block's writes clear its whole dense extent)
+        if (!pc.index.alloc(nblocks * sizeof(uint32_t), true) || !pc.data.alloc((cap + 8) * 16, false))
             return ZPX_E_OUT_OF_MEMORY;
         size_t first = 0;
         for (int c = 0; c < o_.n_comp; c++) {
