@@ -274,9 +274,14 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
     W = H = args.size
     out = {}
     d = S.jpeg_progressive_444(1000 + rank, W, H, args.quality)
-    t0 = time.perf_counter()
-    co = jpeg.Coefficients(d)
-    t_ent = time.perf_counter() - t0
+    # host entropy: the best of three decodes (the first also starts the
+    # decoder's worker threads)
+    t_ent = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        co = jpeg.Coefficients(d)
+        dt = time.perf_counter() - t0
+        t_ent = dt if t_ent is None else min(t_ent, dt)
     jb = device.JpegBatch([co], slots=[0] * args.images, output="rgba", ctx=ctx)
     if rank == 0:
         jb.launch(torch.cuda.current_stream().cuda_stream)

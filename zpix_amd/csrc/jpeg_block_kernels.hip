@@ -943,7 +943,10 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
             const uint32_t e = static_cast<uint32_t>(__shfl(static_cast<int>(ixv), I::B * i + lane % I::B));
             const uint32_t q = static_cast<uint32_t>((lane / I::B + I::P - (I::P == 8 ? i : 0)) % I::P);
             const uint32_t piece = q < (e & 15u) ? (e >> 4) + q : 0u;
-            glds16<ZPX_PLANE_DMA_NT != 0>(pz + static_cast<size_t>(piece) * 16, cimg + 1024 * i);
+            // (cached, not non-temporal: the lines a task fetches also hold
+            // the pieces of the MCU row's other blocks, which its
+            // neighbouring tasks read soon after)
+            glds16<false>(pz + static_cast<size_t>(piece) * 16, cimg + 1024 * i);
         }
     };
     int task;
