@@ -618,6 +618,114 @@ class Decoder {
             return o.grid[ci].store_sparse_fixed(blk, b, pos, n, max_abs[ci], overflow[ci]) ? 0 : ZPX_E_PANIC;
         }
     };
+    // Bit readers of a first scan's block (first_block).  MemberBits is the
+    // Decoder's own: huffman / receive_extend / bits above.  FastBits runs
+    // the same operations, byte for byte and bit for bit, on register copies
+    // of (ba_, bn_, pos_, unread_) -- bm_ is always 1 << (bn_ - 1) -- while
+    // at least kFastSlack input bytes remain, so no read reaches the end;
+    // an operation whose byte reads would meet a marker (0xFF not followed by
+    // 0x00), or a code longer than the 8-bit table, is handed to the member
+    // function with the state written back, and the copies reloaded after it.
+    // (The members, updated through `this` beside the int32 block stores,
+    // were reloaded and stored around every symbol.)
+    static constexpr size_t kFastSlack = 2048; // > any block's entropy-coded bytes (64 x 27 bits, stuffed x2)
+    struct MemberBits {
+        Decoder &d;
+        int huffman(const Huff &h, uint8_t &out) { return d.huffman(h, out); }
+        int receive_extend(uint8_t t, int32_t &out) { return d.receive_extend(t, out); }
+        int bits(int32_t n, uint32_t &out) { return d.bits(n, out); }
+    };
+    struct FastBits {
+        Decoder &d;
+        const uint8_t *src;
+        uint32_t ba;
+        int32_t bn;
+        size_t pos;
+        int unread;
+        explicit FastBits(Decoder &dd) : d(dd), src(dd.src_), ba(dd.ba_), bn(dd.bn_), pos(dd.pos_), unread(dd.unread_) {}
+        void sync()
+        {
+            d.ba_ = ba;
+            d.bn_ = bn;
+            d.bm_ = bn > 0 ? 1u << (bn - 1) : 0u;
+            d.pos_ = pos;
+            d.unread_ = unread;
+        }
+        void load()
+        {
+            ba = d.ba_;
+            bn = d.bn_;
+            pos = d.pos_;
+            unread = d.unread_;
+        }
+        // stuffed() + one step of ensure(): false (nothing read) at a marker
+        inline bool fill()
+        {
+            const uint8_t x = src[pos];
+            if (x != 0xff) {
+                pos += 1;
+                unread = 1;
+            } else {
+                if (src[pos + 1] != 0x00) return false;
+                pos += 2;
+                unread = 2;
+            }
+            ba = (ba << 8) | x;
+            bn += 8;
+            return true;
+        }
+        inline int huffman(const Huff &h, uint8_t &out)
+        {
+            if (h.num_codes != 0 && (bn >= 8 || fill())) {
+                const uint16_t lv = h.lut[(ba >> (bn - 8)) & 0xff];
+                if (lv != 0) {
+                    bn -= static_cast<int32_t>(lv & 0xff) - 1;
+                    out = static_cast<uint8_t>(lv >> 8);
+                    return 0;
+                }
+            }
+            sync();
+            const int e = d.huffman(h, out);
+            load();
+            return e;
+        }
+        inline int receive_extend(uint8_t t, int32_t &out)
+        {
+            while (bn < static_cast<int32_t>(t)) {
+                if (!fill()) {
+                    sync();
+                    const int e = d.receive_extend(t, out);
+                    load();
+                    return e;
+                }
+            }
+            bn -= t;
+            const int32_t thr = int32_t(1) << t;
+            int32_t v = static_cast<int32_t>((ba >> bn) & static_cast<uint32_t>(thr - 1));
+            if (v < (thr >> 1)) v += static_cast<int32_t>(0xffffffffu << t) + 1;
+            out = v;
+            return 0;
+        }
+        inline int bits(int32_t n, uint32_t &out)
+        {
+            while (bn < n) {
+                if (!fill()) {
+                    sync();
+                    const int e = d.bits(n, out);
+                    load();
+                    return e;
+                }
+            }
+            uint32_t r = ba >> (bn - n);
+            r &= n >= 32 ? 0xffffffffu : ((1u << n) - 1);
+            bn -= n;
+            out = r;
+            return 0;
+        }
+    };
+    template <class R>
+    int first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac, int32_t &dcv, int32_t *b, uint8_t *nzpos,
+                    int &nnz);
     template <class Sink>
     int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
             Sink &sink);
@@ -1081,6 +1189,57 @@ int Decoder::scan_loop(const Scan &sc, bool pieces)
 // body of processSos's MCU loop, :1300-1431).  b is all-zero on entry for
 // baseline scans; the positions a block writes are recorded and cleared
 // after its store.
+// One block of a first scan (processSos :1300-1345: the DC difference, then
+// the AC run/size loop with its end-of-band run), over a bit reader R: the
+// Decoder's own (MemberBits) or register copies of it (FastBits).
+template <class R>
+int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac, int32_t &dcv, int32_t *b,
+                         uint8_t *nzpos, int &nnz)
+{
+    int32_t zig = sc.zs;
+    if (zig == 0) {
+        zig++;
+        uint8_t t;
+        ZTRY(r.huffman(hdc, t));
+        if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+        int32_t delta;
+        ZTRY(r.receive_extend(t, delta));
+        dcv += delta;
+        b[0] = dcv << sc.al;
+        nzpos[nnz++] = 0;
+    }
+    if (zig <= sc.ze && eob_run_ > 0) {
+        eob_run_--;
+        return 0;
+    }
+    for (; zig <= sc.ze; zig++) {
+        uint8_t value;
+        ZTRY(r.huffman(hac, value));
+        const uint8_t v0r = value >> 4, v1 = value & 0x0f;
+        if (v1 != 0) {
+            zig += v0r;
+            if (zig > sc.ze) break;
+            int32_t ac;
+            ZTRY(r.receive_extend(v1, ac));
+            b[kUnzig[zig]] = ac << sc.al;
+            nzpos[nnz++] = kUnzig[zig];
+        } else {
+            if (v0r != 0x0f) {
+                eob_run_ = static_cast<uint16_t>(1u << v0r);
+                if (v0r != 0) {
+                    uint32_t x;
+                    ZTRY(r.bits(v0r, x));
+                    eob_run_ |= static_cast<uint16_t>(x);
+                }
+                eob_run_--;
+                break;
+            }
+            zig += 0x0f;
+        }
+    }
+    return 0;
+}
+
 template <class Sink>
 int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b,
                  uint8_t *nzpos, Sink &sink)
@@ -1111,48 +1270,14 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
             int nnz = 0;
             if (sc.ah != 0) {
                 ZTRY(refine(b, hac, sc.zs, sc.ze, int32_t(1) << sc.al));
+            } else if (len_ - pos_ >= kFastSlack) {
+                FastBits fb(*this); // (the block's bit reads in registers)
+                const int e = first_block(fb, sc, hdc, hac, dc[ci], b, nzpos, nnz);
+                fb.sync();
+                if (e) return e;
             } else {
-                int32_t zig = sc.zs;
-                if (zig == 0) {
-                    zig++;
-                    uint8_t t;
-                    ZTRY(huffman(hdc, t));
-                    if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
-                    int32_t delta;
-                    ZTRY(receive_extend(t, delta));
-                    dc[ci] += delta;
-                    b[0] = dc[ci] << sc.al;
-                    nzpos[nnz++] = 0;
-                }
-                if (zig <= sc.ze && eob_run_ > 0) {
-                    eob_run_--;
-                } else {
-                    for (; zig <= sc.ze; zig++) {
-                        uint8_t value;
-                        ZTRY(huffman(hac, value));
-                        const uint8_t v0r = value >> 4, v1 = value & 0x0f;
-                        if (v1 != 0) {
-                            zig += v0r;
-                            if (zig > sc.ze) break;
-                            int32_t ac;
-                            ZTRY(receive_extend(v1, ac));
-                            b[kUnzig[zig]] = ac << sc.al;
-                            nzpos[nnz++] = kUnzig[zig];
-                        } else {
-                            if (v0r != 0x0f) {
-                                eob_run_ = static_cast<uint16_t>(1u << v0r);
-                                if (v0r != 0) {
-                                    uint32_t x;
-                                    ZTRY(bits(v0r, x));
-                                    eob_run_ |= static_cast<uint16_t>(x);
-                                }
-                                eob_run_--;
-                                break;
-                            }
-                            zig += 0x0f;
-                        }
-                    }
-                }
+                MemberBits mb{*this};
+                ZTRY(first_block(mb, sc, hdc, hac, dc[ci], b, nzpos, nnz));
             }
             ZTRY(sink.put(ci, blk, b, nzpos, nnz));
             for (int i = 0; i < nnz; i++) b[nzpos[i]] = 0;
