@@ -634,6 +634,7 @@ class Decoder {
         int huffman(const Huff &h, uint8_t &out) { return d.huffman(h, out); }
         int receive_extend(uint8_t t, int32_t &out) { return d.receive_extend(t, out); }
         int bits(int32_t n, uint32_t &out) { return d.bits(n, out); }
+        int bit(bool &out) { return d.bit(out); }
     };
     struct FastBits {
         Decoder &d;
@@ -706,6 +707,18 @@ class Decoder {
             out = v;
             return 0;
         }
+        inline int bit(bool &out)
+        {
+            if (bn == 0 && !fill()) {
+                sync();
+                const int e = d.bit(out);
+                load();
+                return e;
+            }
+            out = ((ba >> (bn - 1)) & 1u) != 0;
+            bn--;
+            return 0;
+        }
         inline int bits(int32_t n, uint32_t &out)
         {
             while (bn < n) {
@@ -730,7 +743,8 @@ class Decoder {
     int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
             Sink &sink);
     // one block of a progressive scan, touching only the scan's band
-    int prog_block(const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc);
+    template <class R>
+    int prog_block(R &r, const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc);
     // coefficient z (zig-zag order) of block blk of component ci: set also
     // marks it nonzero in the block's mask (a refinement then visits only
     // the nonzero coefficients of its band; a coefficient never returns to
@@ -763,8 +777,10 @@ class Decoder {
     uint64_t prog_mask(int ci, size_t blk) const { return (*nz_[ci])[blk]; }
     // refine :1459-1518 / refineNonZeroes :1522-1549 of an AC band on the
     // grid itself, through the nonzero masks
-    int prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta);
-    int prog_refine_nonzero(int ci, size_t blk, uint64_t mask, int32_t zig, int32_t ze, int32_t nz, int32_t delta,
+    template <class R>
+    int prog_refine_ac(R &r, int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta);
+    template <class R>
+    int prog_refine_nonzero(R &r, int ci, size_t blk, uint64_t mask, int32_t zig, int32_t ze, int32_t nz, int32_t delta,
                             int32_t &zout);
     // the MCU loop of one scan, restart markers included (processSos
     // :1298-1455), from the scan's first entropy-coded byte
@@ -1264,7 +1280,11 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
             }
             const size_t blk = size_t(by) * size_t(mxx * hi) + size_t(bx);
             if (sc.prog) {
-                ZTRY(prog_block(sc, ci, blk, hdc, hac, dc));
+                // (the Decoder's own reader: a progressive scan reads a few
+                // bits a block -- a DC bit, an end-of-band run -- and copying
+                // the reader in and out per block cost more than it saved)
+                MemberBits mb{*this};
+                ZTRY(prog_block(mb, sc, ci, blk, hdc, hac, dc));
                 continue;
             }
             int nnz = 0;
@@ -1291,27 +1311,28 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
 // the whole block back; only the band can change, so only the band is read
 // and only the coefficients that changed are written -- the same grid, and
 // no cost for the blocks an EOB run skips.
-int Decoder::prog_block(const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc)
+template <class R>
+int Decoder::prog_block(R &r, const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc)
 {
     if (sc.ah != 0) {
         const int32_t delta = int32_t(1) << sc.al;
         if (sc.zs == 0) { // refine :1461-1470
             if (sc.ze != 0) return ZPX_E_PANIC;
             bool set;
-            ZTRY(bit(set));
+            ZTRY(r.bit(set));
             if (set) ZTRY(prog_set(ci, blk, 0, prog_get(ci, blk, 0) | delta));
             return 0;
         }
-        return prog_refine_ac(ci, blk, hac, sc.zs, sc.ze, delta);
+        return prog_refine_ac(r, ci, blk, hac, sc.zs, sc.ze, delta);
     }
     int32_t zig = sc.zs;
     if (zig == 0) {
         zig++;
         uint8_t t;
-        ZTRY(huffman(hdc, t));
+        ZTRY(r.huffman(hdc, t));
         if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
         int32_t delta;
-        ZTRY(receive_extend(t, delta));
+        ZTRY(r.receive_extend(t, delta));
         dc[ci] += delta;
         ZTRY(prog_set(ci, blk, 0, dc[ci] << sc.al));
     }
@@ -1321,20 +1342,20 @@ int Decoder::prog_block(const Scan &sc, int ci, size_t blk, const Huff &hdc, con
     }
     for (; zig <= sc.ze; zig++) {
         uint8_t value;
-        ZTRY(huffman(hac, value));
+        ZTRY(r.huffman(hac, value));
         const uint8_t v0r = value >> 4, v1 = value & 0x0f;
         if (v1 != 0) {
             zig += v0r;
             if (zig > sc.ze) break;
             int32_t ac;
-            ZTRY(receive_extend(v1, ac));
+            ZTRY(r.receive_extend(v1, ac));
             ZTRY(prog_set(ci, blk, zig, ac << sc.al));
         } else {
             if (v0r != 0x0f) {
                 eob_run_ = static_cast<uint16_t>(1u << v0r);
                 if (v0r != 0) {
                     uint32_t x;
-                    ZTRY(bits(v0r, x));
+                    ZTRY(r.bits(v0r, x));
                     eob_run_ |= static_cast<uint16_t>(x);
                 }
                 eob_run_--;
@@ -1353,7 +1374,8 @@ int Decoder::prog_block(const Scan &sc, int ci, size_t blk, const Huff &hdc, con
 // nonzero coefficient before it in zig-zag order, are read together (up to
 // 16 at a time: exactly the bits, and so the bytes, the reference's loop
 // reads one at a time).
-int Decoder::prog_refine_nonzero(int ci, size_t blk, uint64_t mask, int32_t zig, int32_t ze, int32_t nz,
+template <class R>
+int Decoder::prog_refine_nonzero(R &r, int ci, size_t blk, uint64_t mask, int32_t zig, int32_t ze, int32_t nz,
                                  int32_t delta, int32_t &zout)
 {
     if (zig > ze) {
@@ -1371,7 +1393,7 @@ int Decoder::prog_refine_nonzero(int ci, size_t blk, uint64_t mask, int32_t zig,
     while (m) {
         const int n = std::min(16, __builtin_popcountll(m));
         uint32_t corr;
-        ZTRY(bits(n, corr));
+        ZTRY(r.bits(n, corr));
         for (int k = n - 1; k >= 0; k--) {
             const int z = __builtin_ctzll(m);
             m &= m - 1;
@@ -1384,7 +1406,8 @@ int Decoder::prog_refine_nonzero(int ci, size_t blk, uint64_t mask, int32_t zig,
     return 0;
 }
 
-int Decoder::prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta)
+template <class R>
+int Decoder::prog_refine_ac(R &r, int ci, size_t blk, const Huff &h, int32_t zs, int32_t ze, int32_t delta)
 { // refine :1471-1518
     int32_t zig = zs;
     // (a coefficient this scan sets is outside the mask of the zeros the
@@ -1393,26 +1416,26 @@ int Decoder::prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32
         for (; zig <= ze; zig++) {
             int32_t z = 0;
             uint8_t value;
-            ZTRY(huffman(h, value));
+            ZTRY(r.huffman(h, value));
             const uint8_t v0 = value >> 4, v1 = value & 0x0f;
             if (v1 == 0) {
                 if (v0 != 0x0f) {
                     eob_run_ = static_cast<uint16_t>(1u << v0);
                     if (v0 != 0) {
                         uint32_t x;
-                        ZTRY(bits(v0, x));
+                        ZTRY(r.bits(v0, x));
                         eob_run_ |= static_cast<uint16_t>(x);
                     }
                     break;
                 }
             } else if (v1 == 1) {
                 bool positive;
-                ZTRY(bit(positive));
+                ZTRY(r.bit(positive));
                 z = positive ? delta : -delta;
             } else {
                 return ZPX_E_UNEXPECTED_HUFFMAN_CODE;
             }
-            ZTRY(prog_refine_nonzero(ci, blk, prog_mask(ci, blk), zig, ze, v0, delta, zig));
+            ZTRY(prog_refine_nonzero(r, ci, blk, prog_mask(ci, blk), zig, ze, v0, delta, zig));
             if (zig > ze) return ZPX_E_TOO_MANY_COEFFICIENTS;
             if (z != 0) ZTRY(prog_set(ci, blk, zig, z));
         }
@@ -1420,7 +1443,7 @@ int Decoder::prog_refine_ac(int ci, size_t blk, const Huff &h, int32_t zs, int32
     if (eob_run_ > 0) {
         eob_run_--;
         int32_t ignored;
-        ZTRY(prog_refine_nonzero(ci, blk, prog_mask(ci, blk), zig, ze, -1, delta, ignored));
+        ZTRY(prog_refine_nonzero(r, ci, blk, prog_mask(ci, blk), zig, ze, -1, delta, ignored));
     }
     return 0;
 }
