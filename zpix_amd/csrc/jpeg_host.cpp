@@ -745,6 +745,14 @@ class Decoder {
     // one block of a progressive scan, touching only the scan's band
     template <class R>
     int prog_block(R &r, const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc);
+    // (out of line: inlined into mcu() beside the baseline path's register
+    // reader, the progressive decode ran 10-20 % slower; tools/prog_ab.py)
+    __attribute__((noinline)) int prog_block_member(const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac,
+                                                    int32_t *dc)
+    {
+        MemberBits mb{*this};
+        return prog_block(mb, sc, ci, blk, hdc, hac, dc);
+    }
     // coefficient z (zig-zag order) of block blk of component ci: set also
     // marks it nonzero in the block's mask (a refinement then visits only
     // the nonzero coefficients of its band; a coefficient never returns to
@@ -1283,8 +1291,7 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
                 // (the Decoder's own reader: a progressive scan reads a few
                 // bits a block -- a DC bit, an end-of-band run -- and copying
                 // the reader in and out per block cost more than it saved)
-                MemberBits mb{*this};
-                ZTRY(prog_block(mb, sc, ci, blk, hdc, hac, dc));
+                ZTRY(prog_block_member(sc, ci, blk, hdc, hac, dc));
                 continue;
             }
             int nnz = 0;
