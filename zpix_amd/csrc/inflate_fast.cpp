@@ -132,6 +132,25 @@ bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind
         }
     }
     const int nroot = 1 << root;
+    // the root, shortest codes first: with the codes of < l bits complete in
+    // the first 2^(l-1) entries, one copy doubles them to 2^l, and each code
+    // of l bits is then one store (4,096 strided stores a 12-bit root before)
+    {
+        uint16_t ord[320];
+        int end[17] = {};
+        for (int l = 1; l <= root; l++) end[l] = end[l - 1] + count[l];
+        int at[17];
+        for (int l = 1; l <= root; l++) at[l] = end[l - 1];
+        for (int s = 0; s < n; s++)
+            if (lens[s] && lens[s] <= root) ord[at[lens[s]]++] = static_cast<uint16_t>(s);
+        t[0] = 0;
+        int size = 1;
+        for (int l = 1; l <= root; l++) {
+            memcpy(t + size, t, sizeof(uint32_t) * static_cast<size_t>(size));
+            size <<= 1;
+            for (int i = end[l - 1]; i < end[l]; i++) t[rev[ord[i]]] = result(kind, ord[i]) | uint32_t(l);
+        }
+    }
     int used = nroot;
     bool fits = true;
     for (int i = 0; i < nlong; i++) {
@@ -145,12 +164,9 @@ bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind
     if (!fits) return false;
     for (int s = 0; s < n; s++) {
         const int l = lens[s];
-        if (!l) continue;
+        if (l <= root) continue;
         const uint32_t r = rev[s];
-        if (l <= root) {
-            const uint32_t e = result(kind, s) | uint32_t(l);
-            for (uint32_t k = r; k < uint32_t(nroot); k += (1u << l)) t[k] = e;
-        } else {
+        {
             const uint32_t p = r & (uint32_t(nroot) - 1), rest = r >> root;
             const uint32_t off = payload(t[p]), sb = extra_of(t[p]);
             const uint32_t e = result(kind, s) | uint32_t(l - root);
