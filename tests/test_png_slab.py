@@ -68,17 +68,25 @@ def check_slab(st, slab=None):
             assert list(reg[:128]) == ft
             sk, mx = skews(ft, rows)
             ngroups = (nchunks + mx + 7) // 8
+            # per group and lane: the group windows of rows 2 lane and
+            # 2 lane + 1 interleaved two bytes at a time (a0 a1 b0 b1 a2 a3
+            # b2 b3 ...), as 2 NQ pieces: piece h NQ + q at tile h, piece q
             pieces = np.asarray(reg[128:128 + ngroups * 2 * nq * 1024]).reshape(ngroups, 2, nq, 64, 16)
+            pad = 8 * cb * ngroups + 8 * cb * 128
+            win = np.zeros((128, ngroups, 16 * nq), np.uint8)
             for r in range(128):
                 row = (np.asarray(stream[off + (base + r) * (rb + 1) + 1: off + (base + r) * (rb + 1) + 1 + rb])
                        if r < rows else np.zeros(0, np.uint8))
-                pad = 8 * cb * ngroups + 8 * cb * 128
                 ext = np.zeros(pad + len(row) + pad, np.uint8)
                 ext[pad:pad + len(row)] = row
                 for g in range(ngroups):
                     s0 = pad + (8 * g - sk[r]) * cb
-                    want = ext[s0:s0 + 16 * nq].reshape(nq, 16)
-                    assert np.array_equal(pieces[g, r % 2, :, r // 2], want), (b, r, g)
+                    win[r, g] = ext[s0:s0 + 16 * nq]
+            for lane in range(64):
+                a = win[2 * lane].reshape(ngroups, 8 * nq, 2)
+                bb = win[2 * lane + 1].reshape(ngroups, 8 * nq, 2)
+                inter = np.concatenate([a, bb], axis=2).reshape(ngroups, 2, nq, 16)
+                assert np.array_equal(pieces[:, :, :, lane], inter), (b, lane)
             b += 1
     assert b == nb
 

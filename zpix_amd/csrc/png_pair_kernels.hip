@@ -44,7 +44,8 @@
 // and a separate add and shift for Avg), against ~21 per byte one row per lane.
 //
 // Memory: every lane burst-loads its two rows' next group of kG = 8 chunks one
-// group ahead through buffer descriptors (every load and store of the group
+// group ahead (from the band slab, the rows interleaved two bytes at a time:
+// png_slab.cpp) through buffer descriptors (every load and store of the group
 // loop is unconditional -- out-of-range offsets read zero / drop the store --
 // so s_waitcnt counts stay exact); each reconstructed chunk is expanded to
 // its 16 output bytes (colour key, 16-bit order) into a per-row LDS ring of
@@ -155,7 +156,10 @@ __device__ __forceinline__ PairFilter half_filter(int ft, int h)
     return PairFilter{keep << sh, force << sh};
 }
 
-// One byte pair: out = (f + predictor) mod 256 per half.
+// One byte pair: out = (f + predictor) mod 256 per half.  f's bytes 1 and 3
+// may hold anything (the slab's interleaved bytes): the add is per 16-bit
+// half (v_pk_add_u16), so nothing carries between the rows, and the mask
+// keeps each half's low byte.
 __device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t b, uint32_t c, PairFilter pf)
 {
     const h16x2 va = ash(b) - ash(c); // b - c: pa = |va|
@@ -169,7 +173,8 @@ __device__ __forceinline__ uint32_t recon_pair(uint32_t f, uint32_t a, uint32_t 
     const uint32_t ab = a | (b << 8);
     const uint32_t cav = c | (__builtin_amdgcn_lerp(a, b, 0u) << 8); // avg = (a + b) >> 1 per byte (v_lerp_u8)
     const uint32_t t = __builtin_amdgcn_perm(cav, ab, sel);
-    return (f + t) & 0x00ff00ffu;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, f) + __builtin_bit_cast(u16x2, t)) & 0x00ff00ffu;
 }
 
 // ---- output of one chunk: the 16 bytes store_chunk writes (readImagePass
@@ -665,14 +670,20 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                         up[4 * w + b] = __builtin_amdgcn_perm(dh, plo[w], 0x0c000c04u | static_cast<uint32_t>(b) << 16 |
                                                                              static_cast<uint32_t>(b));
                 }
-                // ---- filtered bytes of both rows' chunks, packed
+                // ---- filtered bytes of both rows' chunks, packed: the
+                // slab interleaves the rows two bytes at a time, so dword m
+                // of the group (A0: the first 2 CB, A1: the rest) is byte
+                // pair 2k of the packed form as is, and shifted down a byte
+                // pair 2k + 1 (bytes 1 and 3 left over: recon_pair's add
+                // is per half)
                 uint32_t f[CB];
 #pragma unroll
-                for (int w = 0; w < CW; w++)
-#pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        f[4 * w + b] = __builtin_amdgcn_perm(A1[st * CW + w], A0[st * CW + w],
-                                                             0x0c000c00u | (4u + b) << 16 | static_cast<uint32_t>(b));
+                for (int k = 0; k < CB / 2; k++) {
+                    const int m = st * (CB / 2) + k;
+                    const uint32_t d = m < GD ? A0[m] : A1[m - GD];
+                    f[2 * k] = d;
+                    f[2 * k + 1] = d >> 8;
+                }
                 // ---- reconstruct CB byte pairs, left to right
                 uint32_t o[CB];
 #pragma unroll
@@ -722,7 +733,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                     wave_lds_sync(); // fst is rewritten at the next flush
                 }
             }
-        }
+                }
         // ---- row tails: the last (< 2 FL) unflushed chunks, the last partial
         gu8 *out0 = obase + static_cast<size_t>(2 * lane) * orow_bytes;
         gu8 *out1 = out0 + orow_bytes;

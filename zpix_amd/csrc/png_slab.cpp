@@ -15,9 +15,14 @@
 //   slab   = u64 region offset per band (every band of every non-empty pass,
 //            Adam7 order), then the regions, 256-byte aligned
 //   region = the band's 128 filter-type bytes (0 for rows past the pass),
-//            then per group g, row half h (row 2 lane + h), piece q < NQ:
-//            1 KiB = 64 lanes x 16 bytes, the bytes [16 q, 16 q + 16) of the
-//            row's group window (chunk 8 g - skew(r) on, zeros outside the row)
+//            then per group g, tile h < 2, piece q < NQ: 1 KiB = 64 lanes x
+//            16 bytes, piece h NQ + q of the lane's two group windows (rows
+//            2 lane and 2 lane + 1, each from its chunk 8 g - skew(r) on,
+//            zeros outside the row) interleaved two bytes at a time:
+//            a0 a1 b0 b1 a2 a3 b2 b3 ... -- so a loaded dword holds two
+//            byte pairs of the kernel's packed form (row 2j in the low
+//            16-bit half, 2j+1 in the high) and the kernel unpacks with a
+//            shift instead of a v_perm per pair
 //
 // NQ = 8 CB / 16 (6 for 3- and 6-byte pixels, else 8), and a band has
 // ceil((chunks + max skew) / 8) groups, exactly the groups the kernel walks.
@@ -130,35 +135,40 @@ void fill_band(const DevPngPass &p, const SlabGeom &sg, uint32_t base, uint8_t *
     const uint8_t *rowp[128];
     for (int r = 0; r < 128; r++)
         rowp[r] = static_cast<uint32_t>(r) < rows ? p.filtered + size_t(base + r) * (rb + 1) + 1 : nullptr;
-    // destination order: each (g, h) tile of NQ KiB is written whole,
-    // lane by lane, from 64 rows x 16 NQ bytes (21 ms per 4K tc8
-    // image on the build host, memcpy of the same bytes 6.5;
-    // non-temporal stores, 16 bytes a line at a time: 53 ms)
-    for (int g = 0; g < ngroups; g++)
-        for (int h = 0; h < 2; h++) {
-            uint8_t *gdst = groups + size_t(g) * gbytes + size_t(h) * nq * 1024;
-            for (int lane = 0; lane < 64; lane++) {
-                const int r = 2 * lane + h;
-                const uint8_t *row = rowp[r];
-                const int64_t start = (int64_t(8) * g - skew[r]) * sg.cb; // the group window's first byte
-                uint8_t *dst = gdst + size_t(lane) * 16;
-                if (row && start >= 0 && start + 16 * nq <= int64_t(rb)) {
-                    for (int q = 0; q < nq; q++)
-                        _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + q * 1024),
-                                         _mm_loadu_si128(reinterpret_cast<const __m128i *>(row + start + 16 * q)));
-                    continue;
-                }
-                for (int q = 0; q < nq; q++) {
-                    alignas(16) uint8_t piece[16];
-                    for (int i = 0; i < 16; i++) {
-                        const int64_t x = start + 16 * q + i;
-                        piece[i] = (row && x >= 0 && x < int64_t(rb)) ? row[x] : 0;
-                    }
-                    _mm_storeu_si128(reinterpret_cast<__m128i *>(dst + q * 1024),
-                                     _mm_load_si128(reinterpret_cast<const __m128i *>(piece)));
-                }
-            }
+    // destination order: each group's two NQ KiB tiles are written lane by
+    // lane from the lane's two rows' windows (16 NQ bytes each), their
+    // 16-byte pieces interleaved by 16-bit units (unpacklo / unpackhi)
+    auto window = [&](int r, int g, int q, __m128i &v) {
+        const uint8_t *row = rowp[r];
+        const int64_t start = (int64_t(8) * g - skew[r]) * sg.cb + 16 * q; // this piece's first byte
+        if (row && start >= 0 && start + 16 <= int64_t(rb)) {
+            v = _mm_loadu_si128(reinterpret_cast<const __m128i *>(row + start));
+            return;
         }
+        alignas(16) uint8_t piece[16];
+        for (int i = 0; i < 16; i++) {
+            const int64_t x = start + i;
+            piece[i] = (row && x >= 0 && x < int64_t(rb)) ? row[x] : 0;
+        }
+        v = _mm_load_si128(reinterpret_cast<const __m128i *>(piece));
+    };
+    for (int g = 0; g < ngroups; g++) {
+        uint8_t *gdst = groups + size_t(g) * gbytes;
+        for (int lane = 0; lane < 64; lane++)
+            for (int q = 0; q < nq; q++) {
+                __m128i a, b;
+                window(2 * lane, g, q, a);
+                window(2 * lane + 1, g, q, b);
+                // pieces 2q and 2q + 1 of the interleaved pair: tile p / NQ, piece p % NQ
+                const int p0 = 2 * q, p1 = 2 * q + 1;
+                _mm_storeu_si128(reinterpret_cast<__m128i *>(gdst + size_t(p0 / nq) * nq * 1024 + size_t(p0 % nq) * 1024 +
+                                                             size_t(lane) * 16),
+                                 _mm_unpacklo_epi16(a, b));
+                _mm_storeu_si128(reinterpret_cast<__m128i *>(gdst + size_t(p1 / nq) * nq * 1024 + size_t(p1 % nq) * 1024 +
+                                                             size_t(lane) * 16),
+                                 _mm_unpackhi_epi16(a, b));
+            }
+    }
     const size_t end = off + 128 + size_t(ngroups) * gbytes; // (the next region starts at its alignment)
     memset(slab + end, 0, align_up(end) - end);
 }

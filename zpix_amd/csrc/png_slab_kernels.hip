@@ -14,10 +14,12 @@
 //   2. each row's window of the 16 groups, from its first chunk 8 g0 - skew
 //      on, read as whole dwords with consecutive lanes on consecutive dwords
 //      of one row (whole lines per instruction) into an LDS tile;
-//   3. the 16-byte pieces in the slab's order (piece q of row 2 lane + h's
-//      group window at 128 + ((2 g + h) NQ + q) KiB + 16 lane of the region),
-//      eight lanes on eight consecutive pieces, so every store instruction
-//      writes whole 128-byte lines; bytes outside the row are zeros.
+//   3. the 16-byte pieces in the slab's order (piece p = h NQ + q of rows
+//      2 lane and 2 lane + 1's group windows interleaved two bytes at a
+//      time -- 8 bytes of each row -- at 128 + ((2 g + h) NQ + q) KiB +
+//      16 lane of the region), eight lanes on eight consecutive pieces, so
+//      every store instruction writes whole 128-byte lines; bytes outside a
+//      row are zeros.
 // Streaming and HBM-bound: each stream byte is read once (plus the partial
 // lines at a window's ends) and each slab byte written once.
 #include <hip/hip_runtime.h>
@@ -120,29 +122,35 @@ __global__ __launch_bounds__(256) void png_slab_kernel(const DevSlabBand *__rest
             const int l = idx & 7, rest = idx >> 3;
             const int q = rest % NQ, gh = rest / NQ, h = gh & 1, gl = gh >> 1;
             const int g = g0 + gl;
-            const int rl = 2 * l + h, r = R0 + rl;
-            v4u v = v4u{0, 0, 0, 0};
-            if (static_cast<uint32_t>(r) < rows) {
-                const uint32_t local = (win_start(r, g0) & 15u) + static_cast<uint32_t>(8 * gl * CB + 16 * q);
+            const int pc = h * NQ + q; // the piece of the interleaved pair
+            // 8 bytes of each of the two rows (2 dwords), zeros outside the row
+            auto half = [&](int rl, uint32_t &d0, uint32_t &d1) __attribute__((always_inline)) {
+                const int r = R0 + rl;
+                d0 = d1 = 0;
+                if (static_cast<uint32_t>(r) >= rows) return;
+                const uint32_t local = (win_start(r, g0) & 15u) + static_cast<uint32_t>(8 * gl * CB + 8 * pc);
                 const uint32_t *t = tile + rl * RS + (local >> 2);
                 const uint32_t sh = local & 3u;
-                const uint32_t w0 = t[0], w1 = t[1], w2 = t[2], w3 = t[3], w4 = t[4];
-                v = v4u{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                        __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
-                const int p = (8 * g - skew[r]) * CB + 16 * q; // the piece's first byte in the row
-                if (p < 0 || p + 16 > static_cast<int>(rb)) { // a row edge: zeros outside [0, rb)
+                const uint32_t w0 = t[0], w1 = t[1], w2 = t[2];
+                d0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                d1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                const int p = (8 * g - skew[r]) * CB + 8 * pc; // the first byte in the row
+                if (p < 0 || p + 8 > static_cast<int>(rb)) { // a row edge: zeros outside [0, rb)
+                    uint32_t m0 = 0, m1 = 0;
 #pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        uint32_t m = 0;
-#pragma unroll
-                        for (int b = 0; b < 4; b++) {
-                            const int x = p + 4 * e + b;
-                            m |= (x >= 0 && x < static_cast<int>(rb)) ? 0xffu << (8 * b) : 0u;
-                        }
-                        v[e] &= m;
+                    for (int b = 0; b < 4; b++) {
+                        m0 |= (p + b >= 0 && p + b < static_cast<int>(rb)) ? 0xffu << (8 * b) : 0u;
+                        m1 |= (p + 4 + b >= 0 && p + 4 + b < static_cast<int>(rb)) ? 0xffu << (8 * b) : 0u;
                     }
+                    d0 &= m0;
+                    d1 &= m1;
                 }
-            }
+            };
+            uint32_t a0, a1, b0, b1;
+            half(2 * l, a0, a1);
+            half(2 * l + 1, b0, b1);
+            const v4u v = v4u{__builtin_amdgcn_perm(b0, a0, 0x05040100u), __builtin_amdgcn_perm(b0, a0, 0x07060302u),
+                              __builtin_amdgcn_perm(b1, a1, 0x05040100u), __builtin_amdgcn_perm(b1, a1, 0x07060302u)};
             if (g < ngroups) {
                 const int lane = (R0 >> 1) + l;
                 *reinterpret_cast<v4u *>(groups + (static_cast<size_t>(2 * g + h) * NQ + q) * 1024 + lane * 16) = v;
