@@ -326,7 +326,24 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
                      "traffic": atraffic, "algorithmic_bytes_per_launch": pb.bytes},
         "host_inflate_mpix_s": round(W * H / t_inf / 1e6, 1),
         "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64, configs[4]"}}
+    abytes = pb.bytes
     del pb
+    torch.cuda.empty_cache()
+    # the same from the inflated stream: the paired-row kernel's stream instance
+    sb = device.PngBatch([st], slots=[0] * args.images, ctx=ctx, layout="stream")
+    if rank == 0:
+        sb.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        if not np.array_equal(sb.output_tensor(0).cpu().numpy().reshape(-1)[:want.size], want.reshape(-1)):
+            raise SystemExit("parity failure: Adam7 RGBA16 PNG from the stream != oracle")
+    swall, skern = timed_steps(torch, dist, sb.launch, steps, args.warmup, ws)
+    sb.status(torch.cuda.current_stream().cuda_stream)
+    out["png_adam7_rgba16"]["stream_input"] = {
+        "value": round(sb.pixels * ws * steps / swall / 1e6, 1), "kernel_ms_per_launch": round(skern, 3),
+        "frac": round(abytes / (skern * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+        "traffic": traffic_of(args, "adam7_rgba16_stream"),
+        "note": "inflated stream in HBM -> the paired-row kernel's stream instance (both launches)"}
+    del sb
     torch.cuda.empty_cache()
     # Image.rgbaPixels of that NRGBA64 output (image.zig:103-130, the
     # premultiply of color.zig:73-89), resident batch, one plan launch
@@ -748,6 +765,7 @@ def main():
         torch.cuda.empty_cache()
     # ------------------------------------------------------------ PNG (configs[2])
     if not args.no_png:
+        from zpix_amd import _lib
         t0 = time.perf_counter()
         mine = shard_images(args.images * ws, rank, ws)
         pdatas = [S.png_tc8_mixed(i, W, H) for i in mine[:args.distinct]]
@@ -787,31 +805,47 @@ def main():
         del pb
         torch.cuda.empty_cache()
         # the same images from the inflated stream (what parseIdat hands
-        # readImagePass, png/decoder.zig:516-523): every launch builds the
-        # band slab on the device (png_slab_kernels.hip), then the kernel
-        sb = device.PngBatch(streams, slots=slots, ctx=ctx, layout="stream")
-        if rank == 0:
-            sb.launch(torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize()
-            got = sb.output_tensor(0).cpu().numpy().reshape(H, W, 4)
-            if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
-                raise SystemExit("parity failure: GPU PNG from the stream (device slab) != source pixels")
-        swall, skern = timed_steps(torch, dist, sb.launch, steps, args.warmup, ws)
-        sb.status(torch.cuda.current_stream().cuda_stream)
-        sach = sb.bytes / (skern * 1e-3) / 1e9
+        # readImagePass, png/decoder.zig:516-523): the paired-row kernel's
+        # stream instance reads it as is; beside it the round-4 path, a band
+        # slab built on the device at every launch (png_slab_kernels.hip), then
+        # the slab instance (test switch png_device_slab)
+        def stream_line(dev_slab):
+            prev = _lib.lib().zpx_debug_option(b"png_device_slab", int(dev_slab))
+            try:
+                sb = device.PngBatch(streams, slots=slots, ctx=ctx, layout="stream")
+            finally:
+                _lib.lib().zpx_debug_option(b"png_device_slab", prev)
+            if rank == 0:
+                sb.launch(torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                got = sb.output_tensor(0).cpu().numpy().reshape(H, W, 4)
+                if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
+                    raise SystemExit("parity failure: GPU PNG from the stream != source pixels")
+            swall, skern = timed_steps(torch, dist, sb.launch, steps, args.warmup, ws)
+            sb.status(torch.cuda.current_stream().cuda_stream)
+            r = (sb.pixels * ws * steps / swall / 1e6, skern, sb.bytes)
+            del sb
+            torch.cuda.empty_cache()
+            return r
+
+        sv, skern, sbytes = stream_line(False)
+        sach = sbytes / (skern * 1e-3) / 1e9
+        dv, dkern, _ = stream_line(True)
+        dach = sbytes / (dkern * 1e-3) / 1e9
         pres["stream_input"] = {
-            "value": round(sb.pixels * ws * steps / swall / 1e6, 1), "unit": "MPixels/sec",
+            "value": round(sv, 1), "unit": "MPixels/sec",
             "kernel_ms_per_launch": round(skern, 3),
             "roofline": {"bound": "hbm", "achieved": round(sach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(sach / PEAK_HBM_GBS, 4), "kernel": "png_slab_kernel<12> + " + pkernel,
-                         "traffic": (traffic_of(args, "png_slab_build") + ptraffic
-                                     if traffic_of(args, "png_slab_build") and ptraffic else None),
-                         "algorithmic_bytes_per_launch": sb.bytes},
-            "note": "inflated stream in HBM -> band slab built on the device -> unfilter: both kernels inside the "
-                    "timed plan; algorithmic bytes = stream read + RGBA write (the slab's write and re-read are "
-                    "the layout's cost)"}
-        del sb
-        torch.cuda.empty_cache()
+                         "frac": round(sach / PEAK_HBM_GBS, 4), "kernel": pkernel + " (stream instance)",
+                         "traffic": traffic_of(args, "png_stream"), "algorithmic_bytes_per_launch": sbytes},
+            "note": "inflated stream in HBM -> unfilter -> RGBA, one kernel reading the stream as is",
+            "device_slab": {
+                "value": round(dv, 1), "kernel_ms_per_launch": round(dkern, 3),
+                "frac": round(dach / PEAK_HBM_GBS, 4), "kernel": "png_slab_kernel<12> + " + pkernel,
+                "traffic": (traffic_of(args, "png_slab_build") + ptraffic
+                            if traffic_of(args, "png_slab_build") and ptraffic else None),
+                "note": "the same with the band slab built on the device at every launch, then the slab "
+                        "instance (test switch png_device_slab)"}}
         if result:
             result["png"] = pres
         else:

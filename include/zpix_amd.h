@@ -381,9 +381,9 @@ enum zpx_png_depth {
  * ZPX_PNG_INPUT_PAD readable bytes.  SLAB: the same bytes rearranged per
  * 128-row band in the order the paired-row kernel reads them
  * (zpx_png_stream_slab builds it on the host; only for frames that kernel
- * takes, i.e. zpx_png_stream_slab succeeds).  A STREAM frame the paired-row
- * kernel takes gets the same slab built on the device at each launch of its
- * plan (png_slab_kernels.hip), so both layouts run on the same kernel. */
+ * takes, i.e. zpx_png_stream_slab succeeds).  The paired-row kernel reads
+ * either: a STREAM frame straight from the stream (its stream instance), a
+ * SLAB frame with whole-line loads. */
 enum zpx_png_layout { ZPX_PNG_LAYOUT_STREAM = 0, ZPX_PNG_LAYOUT_SLAB = 1 };
 
 /* One PNG image after host inflate (parseIdat, png/decoder.zig:404-545). */
@@ -622,6 +622,9 @@ int zpx_debug_shard_fake_comm(int on);
  *   "jpeg_sparse" 0: the batch pipeline uploads dense coefficient grids
  *                 (default 1: ZPX_COEFFS_PIECES);
  *   "png_pair"    0: PNG frames use the one-row-per-lane kernel (default 1);
+ *   "png_device_slab" 1: stream-layout PNG frames on the paired-row kernel
+ *                 get their band slab built on the device at each launch
+ *                 and read it (default 0: the kernel reads the stream);
  *   "qoi_segment" pixels per lane segment of the QOI encoder (16..4096;
  *                 default 0 = 128). */
 int zpx_debug_option(const char *name, int value);

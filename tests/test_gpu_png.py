@@ -105,16 +105,43 @@ def test_png_tc8_mixed_filters(w, h):
     assert_same_png(P.decode(data), O.png_decode(data))
 
 
-@pytest.mark.parametrize("layout", ["auto", "stream"])
+class _device_slab:
+    """Test switch png_device_slab: stream-layout frames on the paired-row
+    kernel get their band slab built on the device (png_slab_kernels.hip)
+    and the kernel's slab instance reads it."""
+
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        from zpix_amd import _lib
+        self.prev = _lib.lib().zpx_debug_option(b"png_device_slab", int(self.on))
+
+    def __exit__(self, *a):
+        from zpix_amd import _lib
+        _lib.lib().zpx_debug_option(b"png_device_slab", self.prev)
+
+
+LAYOUTS = ["auto", "stream", "stream_devslab"]
+
+
+def _layout(layout):
+    return ("stream" if layout.startswith("stream") else layout), _device_slab(layout.endswith("devslab"))
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
 def test_png_bench_size_roundtrip(layout):
     """4096^2 tc8 with per-row Sub/Up/Avg/Paeth: the GPU unfilter must return
     exactly the generator's raw pixels (unfilter(filter(x)) == x), from the
-    host-built band slab ("auto") and from the inflated stream ("stream":
-    the plan builds the slab on the device at every launch)."""
+    host-built band slab ("auto"), from the inflated stream ("stream": the
+    kernel's stream instance) and from a slab the plan builds on the device
+    at every launch ("stream_devslab")."""
     raw, filt = S.png_filtered_tc8(0, 4096, 4096)
     data = S.encode_png(4096, 4096, 8, 2, filt.tobytes())
     st = P.Stream(data)
-    batch = device.PngBatch([st], slots=[0, 0], layout=layout)
+    lay, sw = _layout(layout)
+    with sw:
+        batch = device.PngBatch([st], slots=[0, 0], layout=lay)
     assert [f.layout for f in batch.frames] == [int(layout == "auto")] * 2
     for _ in range(2):  # relaunch: scratch must be re-initialised every call
         batch.launch(torch.cuda.current_stream().cuda_stream)
@@ -159,16 +186,18 @@ def test_rgba_pixels_every_kind(where, name):
     assert np.array_equal(got.rgba_pixels(), want.rgba_pixels())
 
 
-@pytest.mark.parametrize("layout", ["auto", "stream"])
+@pytest.mark.parametrize("layout", LAYOUTS)
 def test_png_adam7_rgba16_4k_matches_oracle(layout):
     """configs[4] PNG at its bench size: 4096^2 Adam7 RGBA16 -> NRGBA64 (7
     passes scattered by mergePassInto), bit-exact against the oracle, twice
-    through one plan (relaunch), plus zpx_plan_status; host slab and
-    device-built slab."""
+    through one plan (relaunch), plus zpx_plan_status; host slab, the
+    stream, device-built slab."""
     data = S.png_rgba16_adam7(2000, 4096, 4096)
     want = O.png_decode(data).pixels
     st = P.Stream(data)
-    batch = device.PngBatch([st], slots=[0, 0], layout=layout)
+    lay, sw = _layout(layout)
+    with sw:
+        batch = device.PngBatch([st], slots=[0, 0], layout=lay)
     for _ in range(2):
         batch.launch(torch.cuda.current_stream().cuda_stream)
     batch.status(torch.cuda.current_stream().cuda_stream)
@@ -177,24 +206,27 @@ def test_png_adam7_rgba16_4k_matches_oracle(layout):
         assert np.array_equal(got.reshape(-1)[:want.size], want.reshape(-1))
 
 
-@pytest.mark.parametrize("layout", ["stream", "auto", "mixed"])
+@pytest.mark.parametrize("layout", ["stream", "auto", "mixed", "stream_devslab", "mixed_devslab"])
 @pytest.mark.parametrize("depth,ct,il", [(8, 2, 0), (8, 6, 1), (16, 6, 1), (16, 2, 0), (8, 0, 0), (16, 0, 0),
                                          (8, 2, 1)])
 def test_png_plan_layouts(layout, depth, ct, il):
     """zpx_png_plan on both input layouts: the band slab (paired-row kernel,
-    zpx_png_stream_slab) and the inflated stream (one-row-per-lane kernel),
-    and both in one plan (two launches), bit-exact against the oracle, in
-    one ragged batch of four sizes."""
+    zpx_png_stream_slab) and the inflated stream (the paired-row kernel's
+    stream instance where it takes the image, else the one-row-per-lane
+    kernel; *_devslab: the slab built on the device from it), and both in
+    one plan (two launches), bit-exact against the oracle, in one ragged
+    batch of four sizes."""
     datas = [S.png_generic(depth * 100 + ct * 10 + il + k, w, h, depth, ct, interlace=il, filters=(0, 1, 2, 3, 4))
              for k, (w, h) in enumerate([(17, 5), (130, 200), (33, 129), (300, 260)])]
     streams = [P.Stream(d) for d in datas]
-    b = device.PngBatch(streams, layout=layout)
+    lay, sw = layout.split("_")[0], _device_slab(layout.endswith("devslab"))
+    with sw:
+        b = device.PngBatch(streams, layout=lay)
     # (auto: a slab wherever the paired-row kernel takes the image -- not
-    # the smallest Adam7 passes -- and always the 300 x 260 one; a stream
-    # frame the paired-row kernel takes gets its slab built on the device)
-    slab = [layout == "auto" or (layout == "mixed" and i % 2 == 0) for i in range(4)]
+    # the smallest Adam7 passes -- and always the 300 x 260 one)
+    slab = [lay == "auto" or (lay == "mixed" and i % 2 == 0) for i in range(4)]
     assert [f.layout for f in b.frames] == [int(s and st.slab() is not None) for s, st in zip(slab, streams)]
-    assert b.frames[3].layout == (1 if layout == "auto" else 0)
+    assert b.frames[3].layout == (1 if lay == "auto" else 0)
     b.launch(torch.cuda.current_stream().cuda_stream)
     b.status(torch.cuda.current_stream().cuda_stream)
     for s, d in enumerate(datas):

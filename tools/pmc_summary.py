@@ -31,7 +31,7 @@ KEYS = [
     (r"jpeg_block_kernel<([^>]*)>", None),
     (r"jpeg_rgba_kernel", "jpeg_rgba"),
     (r"png_slab_kernel<(\d+)>", "png_slab_cb{0}"),
-    (r"png_pair_kernel<(\d+), (\w+), (\w+)>", "png_pair_d{0}{2}"),
+    (r"png_pair_kernel<(\d+), (\w+), (\w+), (\w+)>", "png_pair_d{0}{2}{3}"),
     (r"png_unfilter_kernel", "png_unfilter"),
     (r"rgba_batch_kernel<6>", "rgba_pixels"),  # (NRGBA64, the bench's rgbaPixels line)
     (r"rgba_pixels_kernel", "rgba_pixels_generic"),
@@ -47,7 +47,8 @@ def short_name(name):
                 return "jpeg_block<" + m.group(1).replace(" ", "") + ">"
             g = m.groups()
             if key.startswith("png_pair"):
-                return "png_pair_d{}{}".format(g[0], "_merge" if g[2] == "true" else "")
+                return "png_pair_d{}{}{}".format(g[0], "_merge" if g[2] == "true" else "",
+                                                 "_stream" if g[3] == "true" else "")
             return key.format(*g)
     return None
 
@@ -72,10 +73,19 @@ def summarise(base):
     return out
 
 
+# FETCH_SIZE -> bytes read per kernel: x2 for the 16-B-per-lane coalesced
+# streams (the guide's gfx950 correction); the paired-row kernel's stream
+# instance reads 16 B per lane from 64 rows per instruction, a shape the
+# ubench (tools/ubench/png_load_pattern.hip) calibrated at 0.817 tallied per
+# byte streamed
+FETCH_SCALE = {"png_pair_d6_stream": 1 / 0.817, "png_pair_d15_stream": 1 / 0.817,
+               "png_pair_d15_merge_stream": 1 / 0.817}
+
+
 def hbm(out, *keys):
     if not all(k in out and "FETCH_SIZE" in out[k] and "WRITE_SIZE" in out[k] for k in keys):
         return None
-    f = sum(2 * out[k]["FETCH_SIZE"] * 1024 for k in keys)
+    f = sum(FETCH_SCALE.get(k, 2) * out[k]["FETCH_SIZE"] * 1024 for k in keys)
     w = sum(out[k]["WRITE_SIZE"] * 1024 for k in keys)
     return {"fetch_bytes_per_launch": f, "write_bytes_per_launch": w, "hbm_bytes_per_launch": f + w,
             "kernels": list(keys)}
@@ -90,6 +100,8 @@ LINES = {
     "planar_int16": ("jpeg_plane_block_i16",),
     "png": ("png_pair_d6",),
     "png_slab_build": ("png_slab_cb12",),
+    "png_stream": ("png_pair_d6_stream",),
+    "adam7_rgba16_stream": ("png_pair_d15_stream", "png_pair_d15_merge_stream"),
     "adam7_rgba16": ("png_pair_d15", "png_pair_d15_merge"),
     "rgba_pixels_nrgba64": ("rgba_pixels",),
     "pieces_rgba": ("jpeg_block_pieces",),

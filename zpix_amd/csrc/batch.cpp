@@ -437,9 +437,10 @@ int Pipeline::issue_png(Slot &s)
     PngStream &ps = d.ps;
     const uint32_t W = ps.width, H = ps.height;
     const size_t stride = it.dst_stride ? it.dst_stride : size_t(W) * 4;
-    // the inflated stream goes up as is; the paired-row kernel's band slab
-    // is built from it on the device (png_slab_kernels.hip), else the
-    // one-row-per-lane kernel reads the stream
+    // the inflated stream goes up as is, and the kernel reads it: the
+    // paired-row kernel's stream instance, or the one-row-per-lane kernel
+    // (under the test switch png_device_slab the paired-row kernel's band
+    // slab is built from it on the device first, png_slab_kernels.hip)
     const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
                                    ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
     const size_t in_len = ps.data_len + ZPX_PNG_INPUT_PAD;
@@ -484,7 +485,8 @@ int Pipeline::issue_png(Slot &s)
     std::vector<uint64_t> slab_off;
     std::vector<DevSlabBand> sjobs;
     uint32_t slab_groups = 0;
-    if (pair) {
+    const bool dev_slab = pair && opt(Opt::PngDeviceSlab);
+    if (dev_slab) {
         const size_t slab_b = png_dev_slab_layout(f, slab_off);
         HIPCHK(ctx_, s.dslab.reserve(slab_b));
         png_dev_slab_jobs(f, slab_off, s.din.as<uint8_t>(), in_len, s.dslab.as<uint8_t>(), sjobs, slab_groups);
@@ -529,7 +531,7 @@ int Pipeline::issue_png(Slot &s)
     if (!slab_off.empty()) memcpy(h + table_at, slab_off.data(), slab_off.size() * sizeof(uint64_t));
     if (sjobs_b) memcpy(h + sjobs_at, sjobs.data(), sjobs_b);
     HIPCHK(ctx_, hipMemcpyAsync(dd, h, desc_b, hipMemcpyHostToDevice, ctx_->stream));
-    if (pair) {
+    if (dev_slab) {
         // the slab: its band table, then the bands from the stream (once the
         // stream has landed: the compute stream waits for ev_in above)
         HIPCHK(ctx_, hipMemcpyAsync(s.dslab.ptr, dd + table_at, slab_off.size() * sizeof(uint64_t),
@@ -552,14 +554,14 @@ int Pipeline::issue_png(Slot &s)
     // first launch reports through sticky -- clear it for this item (the
     // slot's words are reused) and read both words after the last launch
     HIPCHK(ctx_, hipMemsetAsync(s.dctl.as<uint32_t>() + 3, 0, 4, ctx_->stream));
-    const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, dp, dsch, ns, s.dctl.as<uint32_t>(),
+    const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, !dev_slab, dp, dsch, ns, s.dctl.as<uint32_t>(),
                                            s.dbound.as<uint64_t>(), granules, ctx_->stream)
                          : launch_png_unfilter(ps.depth, dp, dsch, ns, s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(),
                                                granules, ctx_->stream);
     if (lrc)
         return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
     // Adam7: pass 6 merges the staged passes once the first launch is done
-    if (ns2 && launch_png_pair_merge(ps.depth, ps.use_transparent, dp, dsch + ns, ns2, s.dctl.as<uint32_t>(),
+    if (ns2 && launch_png_pair_merge(ps.depth, ps.use_transparent, !dev_slab, dp, dsch + ns, ns2, s.dctl.as<uint32_t>(),
                                      s.dbound.as<uint64_t>(), granules, ctx_->stream))
         return hip_fail(ctx_, hipGetLastError(), "batch: png adam7 merge pass");
     HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost, ctx_->stream));

@@ -63,13 +63,16 @@ uint32_t png_default_spin_limit();
 // png_pair_kernels.hip: two rows per lane, 128-row bands (the byte-aligned
 // depths whose chunk is 16 output bytes); the rest take launch_png_unfilter
 bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width, uint64_t out_stride);
-// trns: the images carry a tRNS colour key (RGB8 / RGB16; one value per launch)
-int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                    uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit = 0);
+// trns: the images carry a tRNS colour key (RGB8 / RGB16; one value per
+// launch); stream: the passes' `filtered` is the inflated stream itself
+// (ZPX_PNG_LAYOUT_STREAM), else their band slabs
+int launch_png_pair(int depth, bool trns, bool stream, const DevPngPass *passes, const DevPngBand *sched,
+                    uint32_t nsched, uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s,
+                    uint32_t spin_limit = 0);
 // the second launch of an Adam7 group: its pass-6 bands (sched), merged with
 // the staged passes 1-5 into whole even rows (the 4- and 8-byte-pixel depths)
-int launch_png_pair_merge(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s);
+int launch_png_pair_merge(int depth, bool trns, bool stream, const DevPngPass *passes, const DevPngBand *sched,
+                          uint32_t nsched, uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s);
 
 // png_slab_kernels.hip: the band slab of `njobs` bands built on the device
 // (cb: the depth's chunk bytes, 12 or 16; max_groups: the most groups any of

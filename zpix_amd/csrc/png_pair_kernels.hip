@@ -337,7 +337,7 @@ constexpr int kNt = 2;
 // an offset every buffer access drops (stores) or reads as zero (loads)
 constexpr int kOOR = 0x7ffffff0;
 
-template <int DEPTH, bool TRNS, bool MERGE>
+template <int DEPTH, bool TRNS, bool MERGE, bool STREAM>
 __global__ __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(PairShape<DEPTH, MERGE>::W, PairShape<DEPTH, MERGE>::W)))
 void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__restrict__ sched, uint32_t nsched,
@@ -408,12 +408,23 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const uint32_t base = bd.band * 128;
         const uint32_t band_rows = min(128u, ps.rows - base);
         const bool ok0 = 2u * lane < band_rows, ok1 = 2u * lane + 1 < band_rows;
-        // the band's slab region (png_slab.cpp): its 128 filter bytes, then
-        // its groups, from the frame's band offset table (scalar loads)
-        typedef const __attribute__((address_space(4))) uint64_t *CU64;
-        const uint8_t *region =
-            ps.filtered + *(reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(ps.filtered)) + ps.slab_band0 + bd.band);
-        const int ft0 = region[2 * lane], ft1 = region[2 * lane + 1]; // (0 past the pass)
+        // STREAM: the band's rows in the inflated stream (filter byte, then
+        // rb bytes each); else the band's slab region (png_slab.cpp): its 128
+        // filter bytes, then its groups, from the frame's band offset table
+        // (scalar loads)
+        const uint8_t *region;
+        int ft0, ft1;
+        if constexpr (STREAM) {
+            region = ps.filtered + static_cast<size_t>(base) * (rb + 1);
+            ft0 = ok0 ? region[static_cast<size_t>(2 * lane) * (rb + 1)] : 0;
+            ft1 = ok1 ? region[static_cast<size_t>(2 * lane + 1) * (rb + 1)] : 0;
+        } else {
+            typedef const __attribute__((address_space(4))) uint64_t *CU64;
+            region = ps.filtered +
+                     *(reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(ps.filtered)) + ps.slab_band0 + bd.band);
+            ft0 = region[2 * lane];
+            ft1 = region[2 * lane + 1]; // (0 past the pass)
+        }
 
         // skew over the band's 128 rows (row 2j = low half of lane j, 2j+1 high)
         const uint64_t R0 = __ballot(!(ft0 >= 2) || lane == 0 || !ok0);
@@ -446,10 +457,21 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // its first (k < 0) are zeros: it outputs zeros there, the zero
         // left / up / up-left its first chunk starts from.  The prefetch past
         // the last group reads out of range (zeros).
+        //   STREAM: each lane reads its rows' group windows straight from the
+        // stream, NQ unaligned 16-byte loads a row from chunk 8 g - skew on
+        // (64 rows per instruction); the chunks before a row's first read the
+        // rows above and are zeroed in registers (the group loop's ramp), and
+        // the bytes past a row's end are the next row's, which only the
+        // row's own unstored tail bytes read.  The descriptor spans the
+        // band's rows + ZPX_PNG_INPUT_PAD, so the prefetch past the last
+        // group reads zeros.
         constexpr int NQ = 8 * CB / 16;
         static_assert(NQ * 4 == GD, "a group is NQ 16-byte pieces per row");
-        const uint64_t extent = 128ull + static_cast<uint64_t>((nsteps + kG - 1) / kG) * 2 * NQ * 1024;
+        const uint64_t extent = STREAM ? static_cast<uint64_t>(band_rows) * (rb + 1) + ZPX_PNG_INPUT_PAD
+                                       : 128ull + static_cast<uint64_t>((nsteps + kG - 1) / kG) * 2 * NQ * 1024;
         const Rsrc in_rsrc = make_rsrc(region, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
+        const int soff0 = static_cast<int>(2 * lane * (rb + 1) + 1) - skew0 * CB; // row 2j's chunk 0 - skew0
+        const int soff1 = static_cast<int>((2 * lane + 1) * (rb + 1) + 1) - skew1 * CB;
 
         // boundary hand-off: the previous band's last row (read by lanes
         // 0..WG/2-1, one granule pair each; offsets out of range otherwise)
@@ -490,8 +512,10 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
 #pragma unroll
             for (int q = 0; q < NQ; q++) {
-                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
-                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
+                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(
+                    in_rsrc, STREAM ? soff0 + g0 * CB + 16 * q : gb + q * 1024, 0, 0);
+                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(
+                    in_rsrc, STREAM ? soff1 + g0 * CB + 16 * q : gb + (NQ + q) * 1024, 0, 0);
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     d0[4 * q + e] = a[e];
@@ -640,6 +664,19 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             W = Wn;
             load_group(B0, B1, g0 + kG);
             load_window(Wn, g0 + kG);
+            if constexpr (STREAM) {
+                if (g0 < max_skew) { // the ramp: a row's chunks before its first are zeros
+#pragma unroll
+                    for (int i = 0; i < kG; i++) {
+                        const bool z0 = g0 + i < skew0, z1 = g0 + i < skew1;
+#pragma unroll
+                        for (int w = 0; w < CW; w++) {
+                            A0[i * CW + w] = z0 ? 0u : A0[i * CW + w];
+                            A1[i * CW + w] = z1 ? 0u : A1[i * CW + w];
+                        }
+                    }
+                }
+            }
             if (wait_prev) {
                 // the window must carry this launch's epoch in every granule
                 // the band reads (chunks < nchunks); else poll
@@ -676,13 +713,24 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 // pair 2k of the packed form as is, and shifted down a byte
                 // pair 2k + 1 (bytes 1 and 3 left over: recon_pair's add
                 // is per half)
+                // (STREAM: A0 / A1 are the two rows' windows, one v_perm a
+                // pair)
                 uint32_t f[CB];
+                if constexpr (STREAM) {
 #pragma unroll
-                for (int k = 0; k < CB / 2; k++) {
-                    const int m = st * (CB / 2) + k;
-                    const uint32_t d = m < GD ? A0[m] : A1[m - GD];
-                    f[2 * k] = d;
-                    f[2 * k + 1] = d >> 8;
+                    for (int w = 0; w < CW; w++)
+#pragma unroll
+                        for (int b = 0; b < 4; b++)
+                            f[4 * w + b] = __builtin_amdgcn_perm(A1[st * CW + w], A0[st * CW + w],
+                                                                 0x0c000c00u | (4u + b) << 16 | static_cast<uint32_t>(b));
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CB / 2; k++) {
+                        const int m = st * (CB / 2) + k;
+                        const uint32_t d = m < GD ? A0[m] : A1[m - GD];
+                        f[2 * k] = d;
+                        f[2 * k + 1] = d >> 8;
+                    }
                 }
                 // ---- reconstruct CB byte pairs, left to right
                 uint32_t o[CB];
@@ -800,7 +848,7 @@ __global__ void png_pair_ctl_kernel(uint32_t *ctl)
     ctl[2] = 0;
 }
 
-template <int DEPTH, bool TRNS, bool MERGE = false>
+template <int DEPTH, bool TRNS, bool MERGE, bool STREAM>
 void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched, uint32_t *ctl,
                    uint64_t *boundary, uint32_t band_granules, uint32_t spin_limit, hipStream_t s)
 {
@@ -808,7 +856,7 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
     // function-local static, initialised once even from concurrent threads)
     static const int per_cu = [] {
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH, TRNS, MERGE>, 64, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, png_pair_kernel<DEPTH, TRNS, MERGE, STREAM>, 64, 0) != hipSuccess ||
             occ < 1)
             occ = 4;
         return occ;
@@ -816,7 +864,7 @@ void launch_pair_t(const DevPngPass *passes, const DevPngBand *sched, uint32_t n
     const uint32_t want = static_cast<uint32_t>(device_cu_count() * per_cu);
     const uint32_t grid = nsched < want ? nsched : want;
     hipLaunchKernelGGL(png_pair_ctl_kernel, dim3(1), dim3(1), 0, s, ctl);
-    hipLaunchKernelGGL((png_pair_kernel<DEPTH, TRNS, MERGE>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl,
+    hipLaunchKernelGGL((png_pair_kernel<DEPTH, TRNS, MERGE, STREAM>), dim3(grid), dim3(64), 0, s, passes, sched, nsched, ctl,
                        boundary, band_granules, spin_limit);
 }
 
@@ -853,45 +901,41 @@ bool png_pair_supported(int depth, int interlace, bool use_trns, uint32_t width,
     return in_band < 0x7ffffff0ull && 128ull * yf * out_stride < 0x7ffffff0ull;
 }
 
-int launch_png_pair(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                    uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s, uint32_t spin_limit)
+namespace {
+template <bool MERGE, bool STREAM>
+int dispatch_pair(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
+                  uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, uint32_t sl, hipStream_t s)
 {
-    const uint32_t sl = spin_limit ? spin_limit : png_default_spin_limit();
+#define ZPX_PAIR(D, K) launch_pair_t<D, K, MERGE, STREAM>(passes, sched, nsched, ctl, boundary, band_granules, sl, s)
     switch (depth) {
-#define ZPX_CASE(D) case D: launch_pair_t<D, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
-        ZPX_CASE(ZPX_PNG_G8) ZPX_CASE(ZPX_PNG_G16) ZPX_CASE(ZPX_PNG_TCA8) ZPX_CASE(ZPX_PNG_TCA16)
-#undef ZPX_CASE
-    case ZPX_PNG_TC8:
-        if (trns) launch_pair_t<ZPX_PNG_TC8, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        else launch_pair_t<ZPX_PNG_TC8, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        break;
-    case ZPX_PNG_TC16:
-        if (trns) launch_pair_t<ZPX_PNG_TC16, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        else launch_pair_t<ZPX_PNG_TC16, false>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        break;
-    default: return -2;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_png_pair_merge(int depth, bool trns, const DevPngPass *passes, const DevPngBand *sched, uint32_t nsched,
-                          uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s)
-{
-    const uint32_t sl = png_default_spin_limit();
-    switch (depth) {
-    case ZPX_PNG_TCA8: launch_pair_t<ZPX_PNG_TCA8, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
-    case ZPX_PNG_TCA16: launch_pair_t<ZPX_PNG_TCA16, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s); break;
-    case ZPX_PNG_TC8:
-        if (trns) launch_pair_t<ZPX_PNG_TC8, true, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        else launch_pair_t<ZPX_PNG_TC8, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        break;
-    case ZPX_PNG_TC16:
-        if (trns) launch_pair_t<ZPX_PNG_TC16, true, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        else launch_pair_t<ZPX_PNG_TC16, false, true>(passes, sched, nsched, ctl, boundary, band_granules, sl, s);
-        break;
+    case ZPX_PNG_G8: if constexpr (!MERGE) { ZPX_PAIR(ZPX_PNG_G8, false); break; } else return -2;
+    case ZPX_PNG_G16: if constexpr (!MERGE) { ZPX_PAIR(ZPX_PNG_G16, false); break; } else return -2;
+    case ZPX_PNG_TCA8: ZPX_PAIR(ZPX_PNG_TCA8, false); break;
+    case ZPX_PNG_TCA16: ZPX_PAIR(ZPX_PNG_TCA16, false); break;
+    case ZPX_PNG_TC8: if (trns) ZPX_PAIR(ZPX_PNG_TC8, true); else ZPX_PAIR(ZPX_PNG_TC8, false); break;
+    case ZPX_PNG_TC16: if (trns) ZPX_PAIR(ZPX_PNG_TC16, true); else ZPX_PAIR(ZPX_PNG_TC16, false); break;
     default: return -2; // (Gray8 / Gray16 are never interlaced on this kernel: png_pair_supported)
     }
+#undef ZPX_PAIR
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+} // namespace
+
+int launch_png_pair(int depth, bool trns, bool stream, const DevPngPass *passes, const DevPngBand *sched,
+                    uint32_t nsched, uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s,
+                    uint32_t spin_limit)
+{
+    const uint32_t sl = spin_limit ? spin_limit : png_default_spin_limit();
+    return stream ? dispatch_pair<false, true>(depth, trns, passes, sched, nsched, ctl, boundary, band_granules, sl, s)
+                  : dispatch_pair<false, false>(depth, trns, passes, sched, nsched, ctl, boundary, band_granules, sl, s);
+}
+
+int launch_png_pair_merge(int depth, bool trns, bool stream, const DevPngPass *passes, const DevPngBand *sched,
+                          uint32_t nsched, uint32_t *ctl, uint64_t *boundary, uint32_t band_granules, hipStream_t s)
+{
+    const uint32_t sl = png_default_spin_limit();
+    return stream ? dispatch_pair<true, true>(depth, trns, passes, sched, nsched, ctl, boundary, band_granules, sl, s)
+                  : dispatch_pair<true, false>(depth, trns, passes, sched, nsched, ctl, boundary, band_granules, sl, s);
 }
 
 } // namespace zpx

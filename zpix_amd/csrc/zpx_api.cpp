@@ -337,11 +337,13 @@ struct PngGroup {
     int depth = 0;
     bool pair = false; // png_pair_kernel (128-row bands) or png_unfilter_kernel (64)
     bool trns = false; // (pair kernel) the images carry a tRNS colour key
+    bool stream = false; // (pair kernel) its stream instance: the frames' inflated streams as they are
     DevBuf passes, sched, scratch, boundary;
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
     DevBuf staging, merge_jobs; // Adam7 passes 1-5 and pass 6's merge jobs (Adam7Stage)
-    // stream-layout frames of the paired-row kernel: their band slabs, built
-    // on the device before the kernel (png_slab_kernels.hip)
+    // stream-layout frames of the paired-row kernel under the test switch
+    // png_device_slab: their band slabs, built on the device before the
+    // kernel (png_slab_kernels.hip)
     DevBuf dslab, slab_jobs;
     uint32_t nslab_jobs = 0, slab_max_groups = 0;
     uint32_t nsched2 = 0;       // bands of the second launch (Adam7 pass 6), after the first nsched
@@ -615,13 +617,13 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
     plan->ctx = ctx;
     plan->kind = 2;
     // one launch per (depth, kernel): the paired-row kernel takes what it supports
-    std::map<std::tuple<int, bool, bool>, std::vector<int>> by_depth; // (depth, pair kernel, colour key)
+    std::map<std::tuple<int, bool, bool, bool>, std::vector<int>> by_depth; // (depth, pair kernel, colour key, stream)
     for (int i = 0; i < n_frames; i++) {
         if (frames[i].depth < ZPX_PNG_G1 || frames[i].depth > ZPX_PNG_TCA16) return ZPX_E_INVALID_ARGUMENT;
         const bool trns = frames[i].use_transparent != 0;
-        // the paired-row kernel reads band slabs: a stream-layout frame it
-        // takes gets its slab built on the device at each launch; the rest
-        // take the one-row-per-lane kernel
+        // the paired-row kernel takes the stream layout (its stream
+        // instance) and the slab layout; the rest take the one-row-per-lane
+        // kernel
         const bool pair_ok = png_use_pair(frames[i].depth, frames[i].interlace, trns, frames[i].width,
                                           frames[i].out_stride);
         if (frames[i].layout > ZPX_PNG_LAYOUT_SLAB) return ZPX_E_INVALID_ARGUMENT;
@@ -630,7 +632,9 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
             return ZPX_E_INVALID_ARGUMENT;
         }
         const bool pair = pair_ok;
-        by_depth[{frames[i].depth, pair, pair && trns}].push_back(i);
+        // (png_device_slab: stream frames get a device slab, read as slabs)
+        const bool stream = pair && frames[i].layout == ZPX_PNG_LAYOUT_STREAM && !opt(Opt::PngDeviceSlab);
+        by_depth[{frames[i].depth, pair, pair && trns, stream}].push_back(i);
     }
     uint64_t bytes = 0;
     for (auto &kv : by_depth) {
@@ -638,6 +642,7 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
         g->depth = std::get<0>(kv.first);
         g->pair = std::get<1>(kv.first);
         g->trns = std::get<2>(kv.first);
+        g->stream = std::get<3>(kv.first);
         std::vector<DevPngPass> passes;
         std::vector<uint32_t> rowbytes;
         Adam7Stage a7;
@@ -645,7 +650,7 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
         std::vector<std::vector<uint64_t>> slab_off(kv.second.size());
         std::vector<size_t> slab_at(kv.second.size(), 0);
         size_t slab_total = 0;
-        for (size_t k = 0; k < kv.second.size() && g->pair; k++) {
+        for (size_t k = 0; k < kv.second.size() && g->pair && !g->stream; k++) {
             const zpx_png_frame &f = frames[kv.second[k]];
             if (f.layout != ZPX_PNG_LAYOUT_STREAM) continue;
             slab_at[k] = slab_total;
@@ -656,7 +661,7 @@ static int zpx_png_plan_create_impl(zpx_ctx *ctx, const zpx_png_frame *frames, i
         for (size_t k = 0; k < kv.second.size(); k++) {
             const int idx = kv.second[k];
             zpx_png_frame f = frames[idx];
-            if (g->pair && f.layout == ZPX_PNG_LAYOUT_STREAM) {
+            if (g->pair && !g->stream && f.layout == ZPX_PNG_LAYOUT_STREAM) {
                 uint8_t *d_slab = g->dslab.as<uint8_t>() + slab_at[k];
                 HIPCHK(ctx, hipMemcpy(d_slab, slab_off[k].data(), slab_off[k].size() * sizeof(uint64_t),
                                       hipMemcpyHostToDevice));
@@ -785,7 +790,7 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
         if (g->nslab_jobs && launch_png_slab(png_slab_chunk_bytes(g->depth), g->slab_jobs.as<DevSlabBand>(),
                                              g->nslab_jobs, g->slab_max_groups, st))
             return hip_fail(ctx, hipGetLastError(), "png slab kernel launch");
-        const int rc = g->pair ? launch_png_pair(g->depth, g->trns, g->passes.as<DevPngPass>(),
+        const int rc = g->pair ? launch_png_pair(g->depth, g->trns, g->stream, g->passes.as<DevPngPass>(),
                                                  g->sched.as<DevPngBand>(), g->nsched, g->scratch.as<uint32_t>(),
                                                  g->boundary.as<uint64_t>(), g->band_bytes, st)
                                : launch_png_unfilter(g->depth, g->passes.as<DevPngPass>(), g->sched.as<DevPngBand>(),
@@ -793,7 +798,7 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
                                                      g->band_bytes, st);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
         // Adam7: pass 6 merges the staged passes once the first launch is done
-        if (g->nsched2 && launch_png_pair_merge(g->depth, g->trns, g->passes.as<DevPngPass>(),
+        if (g->nsched2 && launch_png_pair_merge(g->depth, g->trns, g->stream, g->passes.as<DevPngPass>(),
                                                 g->sched.as<DevPngBand>() + g->nsched, g->nsched2,
                                                 g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes,
                                                 st))
@@ -1252,12 +1257,9 @@ static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint
     if (int e = png_parse(buf, len, ps, png_inflate_threads())) return e;
     const size_t out_len = size_t(ps.width) * ps.height * ps.out_bpp;
     DevBuf din, dout, dmax;
-    // the paired-row kernel reads the band slab (png_slab.cpp)
-    const bool slab = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, ps.width,
-                                   size_t(ps.width) * ps.out_bpp) &&
-                      png_stream_build_slab(ps, png_inflate_threads()) == ZPX_OK;
-    const void *hin = slab ? ps.slab.ptr : ps.data.ptr;
-    const size_t in_len = slab ? ps.slab_len : ps.data_len + ZPX_PNG_INPUT_PAD;
+    // the inflated stream goes up as is (both kernels read it)
+    const void *hin = ps.data.ptr;
+    const size_t in_len = ps.data_len + ZPX_PNG_INPUT_PAD;
     HIPCHK(ctx, din.alloc(in_len));
     HIPCHK(ctx, hipMemcpyAsync(din.ptr, hin, in_len, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, dout.alloc(out_len));
@@ -1272,7 +1274,7 @@ static int zpx_png_decode_impl(zpx_ctx *ctx, const zpx_allocator *al, const uint
     f.use_transparent = ps.use_transparent;
     memcpy(f.transparent, ps.transparent, 6);
     f.filtered = din.as<uint8_t>();
-    f.layout = slab ? ZPX_PNG_LAYOUT_SLAB : ZPX_PNG_LAYOUT_STREAM;
+    f.layout = ZPX_PNG_LAYOUT_STREAM;
     f.out = dout.as<uint8_t>();
     f.out_stride = size_t(ps.width) * ps.out_bpp;
     f.max_index = ps.kind == ZPX_PALETTED ? dmax.as<int32_t>() : nullptr;
@@ -1465,7 +1467,7 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
     HIPCHK(ctx, hipMemcpy(dsched.ptr, &only, sizeof(DevPngBand), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
-    const int rc = pair ? launch_png_pair(ZPX_PNG_TC8, false, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
+    const int rc = pair ? launch_png_pair(ZPX_PNG_TC8, false, false, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
                                           ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream, spin_limit)
                         : launch_png_unfilter(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
                                               ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream,
@@ -1503,8 +1505,10 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
 
 namespace zpx {
 namespace {
-std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}}; // JpegStrip, JpegSparse, PngPair, QoiSegment
-const char *const kOptNames[static_cast<int>(Opt::Count)] = {"jpeg_strip", "jpeg_sparse", "png_pair", "qoi_segment"};
+// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}};
+const char *const kOptNames[static_cast<int>(Opt::Count)] = {"jpeg_strip", "jpeg_sparse", "png_pair", "qoi_segment",
+                                                             "png_device_slab"};
 } // namespace
 int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
 } // namespace zpx

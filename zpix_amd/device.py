@@ -187,11 +187,11 @@ class PngBatch:
         """layout: "auto" uploads each image's host-built band slab where
         the paired-row kernel takes it (Stream.slab), else the inflated
         stream; "stream" always the inflated stream, as parseIdat hands it to
-        readImagePass (png/decoder.zig:516-523) -- for the images the
-        paired-row kernel takes, every launch then builds their slab on the
-        device first (png_slab_kernels.hip; what png.decode and the batch
-        pipeline do); "mixed" (tests) slabs for even item indices, streams
-        for odd ones."""
+        readImagePass (png/decoder.zig:516-523), which the kernels read as
+        is (the paired-row kernel's stream instance; what png.decode and the
+        batch pipeline do); "mixed" (tests) slabs for even item indices,
+        streams for odd ones.  The plan is made here, so the test switch
+        png_device_slab applies as it is set now."""
         torch = _torch()
         self.ctx = ctx or context.default(device)
         self.device = torch.device("cuda", self.ctx.device)
