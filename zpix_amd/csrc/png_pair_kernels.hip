@@ -44,8 +44,10 @@
 // and a separate add and shift for Avg), against ~21 per byte one row per lane.
 //
 // Memory: every lane burst-loads its two rows' next group of kG = 8 chunks one
-// group ahead (from the band slab, the rows interleaved two bytes at a time:
-// png_slab.cpp) through buffer descriptors (every load and store of the group
+// group ahead -- from the band slab (the rows interleaved two bytes at a time,
+// png_slab.cpp: 1 KiB contiguous per instruction), or, in the STREAM
+// instance, from the inflated stream as parseIdat hands it over (16-byte
+// unaligned loads, 64 rows per instruction) -- through buffer descriptors (every load and store of the group
 // loop is unconditional -- out-of-range offsets read zero / drop the store --
 // so s_waitcnt counts stay exact); each reconstructed chunk is expanded to
 // its 16 output bytes (colour key, 16-bit order) into a per-row LDS ring of
@@ -508,18 +510,39 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // instructions per group is fixed and s_waitcnt counts stay exact:
         // a group waits only for the loads issued one group earlier
         uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
-        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
-            const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
+        // STREAM: row 2j's pieces back to back with the group (its window's
+        // 1-2 lines per lane stay in the L1 between them), row 2j+1's
+        // mid-group (load_row1).  64 x 4K tc8 2.38 ms with the two rows'
+        // pieces alternating, 2.24 back to back, 2.21 with the second row
+        // mid-group; Adam7 RGBA16 6.21, 5.68-5.91, 5.73-5.76 (gpurun_out/sab,
+        // sab2, sa72); non-temporal loads 3.53 / 8.85, sc0 no change.
+        auto load_row1 = [&](uint32_t (&d1)[GD], int g0) {
 #pragma unroll
             for (int q = 0; q < NQ; q++) {
-                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(
-                    in_rsrc, STREAM ? soff0 + g0 * CB + 16 * q : gb + q * 1024, 0, 0);
-                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(
-                    in_rsrc, STREAM ? soff1 + g0 * CB + 16 * q : gb + (NQ + q) * 1024, 0, 0);
+                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, soff1 + g0 * CB + 16 * q, 0, 0);
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    d0[4 * q + e] = a[e];
-                    d1[4 * q + e] = b[e];
+                for (int e = 0; e < 4; e++) d1[4 * q + e] = b[e];
+            }
+        };
+        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
+            if constexpr (STREAM) {
+#pragma unroll
+                for (int q = 0; q < NQ; q++) {
+                    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, soff0 + g0 * CB + 16 * q, 0, 0);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) d0[4 * q + e] = a[e];
+                }
+            } else {
+                const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
+#pragma unroll
+                for (int q = 0; q < NQ; q++) {
+                    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
+                    const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        d0[4 * q + e] = a[e];
+                        d1[4 * q + e] = b[e];
+                    }
                 }
             }
         };
@@ -642,6 +665,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         };
 
         load_group(B0, B1, 0);
+        if constexpr (STREAM) load_row1(B1, 0);
         load_window(Wn, 0);
         // A group waits for its inputs with s_waitcnt vmcnt(N), N = the
         // vector memory operations issued since them: the previous group's
@@ -691,6 +715,8 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             }
 #pragma unroll
             for (int st = 0; st < kG; st++) {
+                if constexpr (STREAM)
+                    if (st == kG / 2) load_row1(B1, g0 + kG);
                 // ---- the row above, one step late: row 2j reads lane j-1's
                 // high row (DPP wave_shr:1; lane 0's `old` is the previous
                 // band's last row, zero without one), row 2j+1 its own low row
