@@ -15,7 +15,9 @@ rank 0, timed and reported apart ("gather"); zpix_amd/shard.py holds the
 placement, shared with tests/test_distributed.py.
 
 The PNG workload (configs[2]: 64 x 4096^2 tc8, mixed Sub/Up/Avg/Paeth rows)
-is measured in the same run and reported under "png" (disable: --no-png).
+is measured in the same run and reported under "png" (disable: --no-png):
+from the inflated stream in HBM, as parseIdat hands it to readImagePass,
+with the host-built band slab as its "slab_input" sub-line.
 """
 from __future__ import annotations
 
@@ -317,19 +319,16 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
             raise SystemExit("parity failure: Adam7 RGBA16 PNG != oracle")
     wall, kern_ms = timed_steps(torch, dist, pb.launch, steps, args.warmup, ws)
     pb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
-    atraffic = traffic_of(args, "adam7_rgba16")
-    out["png_adam7_rgba16"] = {
-        "value": round(pb.pixels * ws * steps / wall / 1e6, 1), "unit": "MPixels/sec",
-        "kernel_ms_per_launch": round(kern_ms, 3),
-        "roofline": {"bound": "hbm", "achieved": round(pb.bytes / (kern_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": round(pb.bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                     "traffic": atraffic, "algorithmic_bytes_per_launch": pb.bytes},
-        "host_inflate_mpix_s": round(W * H / t_inf / 1e6, 1),
-        "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64, configs[4]"}}
     abytes = pb.bytes
+    slab_line = {
+        "value": round(pb.pixels * ws * steps / wall / 1e6, 1), "kernel_ms_per_launch": round(kern_ms, 3),
+        "frac": round(abytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+        "traffic": traffic_of(args, "adam7_rgba16_slab_input"),
+        "note": "the band slab built on the host (zpx_png_stream_slab) and uploaded -> the slab instance"}
     del pb
     torch.cuda.empty_cache()
-    # the same from the inflated stream: the paired-row kernel's stream instance
+    # the line: from the inflated stream, the paired-row kernel's stream
+    # instance (both launches) -- the path png.decode and the batch pipeline take
     sb = device.PngBatch([st], slots=[0] * args.images, ctx=ctx, layout="stream")
     if rank == 0:
         sb.launch(torch.cuda.current_stream().cuda_stream)
@@ -338,11 +337,17 @@ def bench_config5(args, torch, dist, ws, rank, ctx, S, device, jpeg, png):
             raise SystemExit("parity failure: Adam7 RGBA16 PNG from the stream != oracle")
     swall, skern = timed_steps(torch, dist, sb.launch, steps, args.warmup, ws)
     sb.status(torch.cuda.current_stream().cuda_stream)
-    out["png_adam7_rgba16"]["stream_input"] = {
-        "value": round(sb.pixels * ws * steps / swall / 1e6, 1), "kernel_ms_per_launch": round(skern, 3),
-        "frac": round(abytes / (skern * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-        "traffic": traffic_of(args, "adam7_rgba16_stream"),
-        "note": "inflated stream in HBM -> the paired-row kernel's stream instance (both launches)"}
+    out["png_adam7_rgba16"] = {
+        "value": round(sb.pixels * ws * steps / swall / 1e6, 1), "unit": "MPixels/sec",
+        "kernel_ms_per_launch": round(skern, 3),
+        "roofline": {"bound": "hbm", "achieved": round(abytes / (skern * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(abytes / (skern * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                     "traffic": traffic_of(args, "adam7_rgba16_stream"), "algorithmic_bytes_per_launch": abytes,
+                     "kernel": "png_pair_kernel<TCA16> (stream instance, two launches)"},
+        "host_inflate_mpix_s": round(W * H / t_inf / 1e6, 1),
+        "config": {"workload": f"{args.images}x {W}x{H} Adam7 RGBA16 PNG -> NRGBA64 from the inflated stream, "
+                               "configs[4]"},
+        "slab_input": slab_line}
     del sb
     torch.cuda.empty_cache()
     # Image.rgbaPixels of that NRGBA64 output (image.zig:103-130, the
@@ -793,22 +798,24 @@ def main():
         pv = pb.pixels * ws * steps / wall / 1e6
         ach = pb.bytes / (kern_ms * 1e-3) / 1e9
         pkernel = "png_pair_kernel<TC8>"
-        ptraffic = traffic_of(args, "png")
-        pres = {"metric": "MPixels/sec decoded (4K truecolor-8 PNG, mixed Sub/Up/Avg/Paeth)", "value": round(pv, 1),
-                "unit": "MPixels/sec", "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
-                "config": {"workload": f"{args.images}x {W}x{H} tc8 PNG unfilter -> RGBA, configs[2]"},
-                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": ptraffic, "kernel": pkernel,
-                             "kernel_ms_per_launch": round(kern_ms, 3), "algorithmic_bytes_per_launch": pb.bytes},
-                "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1),
-                "host_slab_mpix_s": round(args.distinct * W * H / t_slab / 1e6, 1)}
+        slab_traffic = traffic_of(args, "png_slab_input")
+        slab_line = {
+            "value": round(pv, 1), "unit": "MPixels/sec", "kernel_ms_per_launch": round(kern_ms, 3),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": slab_traffic,
+                         "kernel": pkernel + " (slab instance)", "algorithmic_bytes_per_launch": pb.bytes},
+            "host_slab_mpix_s": round(args.distinct * W * H / t_slab / 1e6, 1),
+            "note": "the band slab built on the host (zpx_png_stream_slab, png_slab.cpp) and uploaded; the kernel "
+                    "reads 1 KiB contiguous per load instruction"}
         del pb
         torch.cuda.empty_cache()
-        # the same images from the inflated stream (what parseIdat hands
-        # readImagePass, png/decoder.zig:516-523): the paired-row kernel's
-        # stream instance reads it as is; beside it the round-4 path, a band
-        # slab built on the device at every launch (png_slab_kernels.hip), then
-        # the slab instance (test switch png_device_slab)
+
+        # the line: the images from the inflated stream (what parseIdat hands
+        # readImagePass, png/decoder.zig:516-523), read as is by the
+        # paired-row kernel's stream instance -- the path png.decode and the
+        # batch pipeline take.  Beside it the round-4 path: a band slab built
+        # on the device at every launch (png_slab_kernels.hip), then the slab
+        # instance (test switch png_device_slab)
         def stream_line(dev_slab):
             prev = _lib.lib().zpx_debug_option(b"png_device_slab", int(dev_slab))
             try:
@@ -822,30 +829,34 @@ def main():
                 if not np.array_equal(got[..., :3], raw.reshape(H, W, 3)):
                     raise SystemExit("parity failure: GPU PNG from the stream != source pixels")
             swall, skern = timed_steps(torch, dist, sb.launch, steps, args.warmup, ws)
-            sb.status(torch.cuda.current_stream().cuda_stream)
-            r = (sb.pixels * ws * steps / swall / 1e6, skern, sb.bytes)
+            sb.status(torch.cuda.current_stream().cuda_stream)  # raises "Hip" if any timed launch timed out
+            r = (sb.pixels * ws * steps / swall / 1e6, swall, skern, sb.bytes)
             del sb
             torch.cuda.empty_cache()
             return r
 
-        sv, skern, sbytes = stream_line(False)
+        sv, swall, skern, sbytes = stream_line(False)
         sach = sbytes / (skern * 1e-3) / 1e9
-        dv, dkern, _ = stream_line(True)
+        dv, _, dkern, _ = stream_line(True)
         dach = sbytes / (dkern * 1e-3) / 1e9
-        pres["stream_input"] = {
-            "value": round(sv, 1), "unit": "MPixels/sec",
-            "kernel_ms_per_launch": round(skern, 3),
-            "roofline": {"bound": "hbm", "achieved": round(sach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(sach / PEAK_HBM_GBS, 4), "kernel": pkernel + " (stream instance)",
-                         "traffic": traffic_of(args, "png_stream"), "algorithmic_bytes_per_launch": sbytes},
-            "note": "inflated stream in HBM -> unfilter -> RGBA, one kernel reading the stream as is",
-            "device_slab": {
-                "value": round(dv, 1), "kernel_ms_per_launch": round(dkern, 3),
-                "frac": round(dach / PEAK_HBM_GBS, 4), "kernel": "png_slab_kernel<12> + " + pkernel,
-                "traffic": (traffic_of(args, "png_slab_build") + ptraffic
-                            if traffic_of(args, "png_slab_build") and ptraffic else None),
-                "note": "the same with the band slab built on the device at every launch, then the slab "
-                        "instance (test switch png_device_slab)"}}
+        dtraffic = traffic_of(args, "png_slab_build")
+        pres = {"metric": "MPixels/sec decoded (4K truecolor-8 PNG, mixed Sub/Up/Avg/Paeth)", "value": round(sv, 1),
+                "unit": "MPixels/sec", "steps": steps, "ms_per_step": round(swall / steps * 1e3, 3),
+                "config": {"workload": f"{args.images}x {W}x{H} tc8 PNG unfilter -> RGBA from the inflated stream, "
+                                       "configs[2]"},
+                "roofline": {"bound": "hbm", "achieved": round(sach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(sach / PEAK_HBM_GBS, 4), "traffic": traffic_of(args, "png_stream"),
+                             "kernel": pkernel + " (stream instance)", "kernel_ms_per_launch": round(skern, 3),
+                             "algorithmic_bytes_per_launch": sbytes},
+                "note": "inflated stream in HBM -> unfilter -> RGBA: one kernel, the whole device path",
+                "host_inflate_mpix_s": round(args.distinct * W * H / t_inf / 1e6, 1),
+                "slab_input": slab_line,
+                "device_slab": {
+                    "value": round(dv, 1), "kernel_ms_per_launch": round(dkern, 3),
+                    "frac": round(dach / PEAK_HBM_GBS, 4), "kernel": "png_slab_kernel<12> + " + pkernel,
+                    "traffic": dtraffic + slab_traffic if dtraffic and slab_traffic else None,
+                    "note": "the stream with the band slab built on the device at every launch, then the slab "
+                            "instance (test switch png_device_slab)"}}
         if result:
             result["png"] = pres
         else:

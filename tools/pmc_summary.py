@@ -98,11 +98,11 @@ LINES = {
     "progressive_444": ("jpeg_block_444_i8",),
     "planar_int8": ("jpeg_plane_block_i8",),
     "planar_int16": ("jpeg_plane_block_i16",),
-    "png": ("png_pair_d6",),
+    "png_stream": ("png_pair_d6_stream",),  # the png line (from the inflated stream)
+    "png_slab_input": ("png_pair_d6",),
     "png_slab_build": ("png_slab_cb12",),
-    "png_stream": ("png_pair_d6_stream",),
-    "adam7_rgba16_stream": ("png_pair_d15_stream", "png_pair_d15_merge_stream"),
-    "adam7_rgba16": ("png_pair_d15", "png_pair_d15_merge"),
+    "adam7_rgba16_stream": ("png_pair_d15_stream", "png_pair_d15_merge_stream"),  # the Adam7 line
+    "adam7_rgba16_slab_input": ("png_pair_d15", "png_pair_d15_merge"),
     "rgba_pixels_nrgba64": ("rgba_pixels",),
     "pieces_rgba": ("jpeg_block_pieces",),
     "pieces_planes": ("jpeg_plane_block_i8_pieces",),

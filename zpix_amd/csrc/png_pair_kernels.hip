@@ -47,7 +47,9 @@
 // group ahead -- from the band slab (the rows interleaved two bytes at a time,
 // png_slab.cpp: 1 KiB contiguous per instruction), or, in the STREAM
 // instance, from the inflated stream as parseIdat hands it over (16-byte
-// unaligned loads, 64 rows per instruction) -- through buffer descriptors (every load and store of the group
+// unaligned loads, a row's window on consecutive lanes, turned round into
+// the row-per-lane registers through an LDS staging area) -- through buffer
+// descriptors (every load and store of the group
 // loop is unconditional -- out-of-range offsets read zero / drop the store --
 // so s_waitcnt counts stay exact); each reconstructed chunk is expanded to
 // its 16 output bytes (colour key, 16-bit order) into a per-row LDS ring of
@@ -375,6 +377,32 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
     __shared__ __attribute__((aligned(16))) uint32_t fst[128];
     __shared__ __attribute__((aligned(16))) uint32_t fso[128];
     __shared__ __attribute__((aligned(16))) uint32_t fsr[128];
+    // STREAM: the group's stream windows arrive in units (row half h, window
+    // part u), each loaded with kSP consecutive lanes on one row's kSP
+    // pieces (a row's bytes contiguous per lane group, ~11-16 rows per
+    // instruction instead of 64) and turned round through this staging area
+    // into the row-per-lane registers.  The whole window a unit (kWH 1) for
+    // 12-byte chunks (6 KiB of staging: the wave's LDS is then 40,464 bytes,
+    // four waves a CU); halves for 16-byte chunks (4 KiB)
+    constexpr int kWH = CB == 12 ? 1 : 2; // window parts per unit row
+    constexpr int kSP = (8 * CB / 16) / kWH; // pieces per row per unit (3, 4 or 6)
+    __shared__ __attribute__((aligned(16))) uint32_t stage[STREAM ? 64 * kSP * 4 : 4];
+    // per-lane LDS byte offsets: unit write of instruction i (lane-piece n =
+    // 64 i + lane: row n / kSP, piece n % kSP), and the row-per-lane read of
+    // piece p; a row's pieces are permuted so that a 16-lane ds_read_b128
+    // group meets 64 distinct banks: xor row & 3 (4 a row), rotated by
+    // row / 8 (6 a row: rows 24 dwords apart pair up 8 lanes apart)
+    auto slot = [](int r, int pc) {
+        return kSP == 4 ? (pc ^ (r & 3)) : kSP == 6 ? (pc + (r >> 3)) % 6 : pc;
+    };
+    uint32_t stw[kSP], str[kSP];
+#pragma unroll
+    for (int i = 0; i < kSP; i++) {
+        const int n = 64 * i + static_cast<int>(threadIdx.x), r = n / kSP, pc = n % kSP;
+        stw[i] = static_cast<uint32_t>((r * kSP + slot(r, pc)) * 16);
+        const int j = static_cast<int>(threadIdx.x);
+        str[i] = static_cast<uint32_t>((j * kSP + slot(j, i)) * 16);
+    }
     constexpr int kTrash = 128 * RS;
 
     const int lane = threadIdx.x;
@@ -459,10 +487,11 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // its first (k < 0) are zeros: it outputs zeros there, the zero
         // left / up / up-left its first chunk starts from.  The prefetch past
         // the last group reads out of range (zeros).
-        //   STREAM: each lane reads its rows' group windows straight from the
-        // stream, NQ unaligned 16-byte loads a row from chunk 8 g - skew on
-        // (64 rows per instruction); the chunks before a row's first read the
-        // rows above and are zeroed in registers (the group loop's ramp), and
+        //   STREAM: the rows' group windows (chunk 8 g - skew on) come
+        // straight from the stream, unaligned 16-byte loads through the
+        // staging area (load_units / xfer); the chunks before a row's first
+        // read the rows above and are zeroed in registers (the group loop's
+        // ramp), and
         // the bytes past a row's end are the next row's, which only the
         // row's own unstored tail bytes read.  The descriptor spans the
         // band's rows + ZPX_PNG_INPUT_PAD, so the prefetch past the last
@@ -474,6 +503,17 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const Rsrc in_rsrc = make_rsrc(region, extent > 0x7ffffff0ull ? 0x7ffffff0u : static_cast<uint32_t>(extent));
         const int soff0 = static_cast<int>(2 * lane * (rb + 1) + 1) - skew0 * CB; // row 2j's chunk 0 - skew0
         const int soff1 = static_cast<int>((2 * lane + 1) * (rb + 1) + 1) - skew1 * CB;
+        // (STREAM) each unit load's lane offset: the row's window start +
+        // its piece, per row half h and instruction i
+        int voff[2][kSP];
+        if constexpr (STREAM) {
+#pragma unroll
+            for (int i = 0; i < kSP; i++) {
+                const int n = 64 * i + lane;
+                voff[0][i] = __shfl(soff0, n / kSP) + 16 * (n % kSP);
+                voff[1][i] = __shfl(soff1, n / kSP) + 16 * (n % kSP);
+            }
+        }
 
         // boundary hand-off: the previous band's last row (read by lanes
         // 0..WG/2-1, one granule pair each; offsets out of range otherwise)
@@ -510,39 +550,52 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         // instructions per group is fixed and s_waitcnt counts stay exact:
         // a group waits only for the loads issued one group earlier
         uint32_t A0[GD], A1[GD], B0[GD], B1[GD];
-        // STREAM: row 2j's pieces back to back with the group (its window's
-        // 1-2 lines per lane stay in the L1 between them), row 2j+1's
-        // mid-group (load_row1).  64 x 4K tc8 2.38 ms with the two rows'
-        // pieces alternating, 2.24 back to back, 2.21 with the second row
-        // mid-group; Adam7 RGBA16 6.21, 5.68-5.91, 5.73-5.76 (gpurun_out/sab,
-        // sab2, sa72); non-temporal loads 3.53 / 8.85, sc0 no change.
-        auto load_row1 = [&](uint32_t (&d1)[GD], int g0) {
+        // STREAM: the next group's units are loaded at the group's start and
+        // turned round at steps 4-7 (4 units) or 4 and 6 (2).  64 x 4K, ms
+        // (gpurun_out/sab, sab2, sa72, lds1, full1): tc8 2.38 with each lane
+        // loading its own rows' pieces (64 rows an instruction, the two rows
+        // alternating), 2.24 a row's pieces back to back, 2.21 with the
+        // second row mid-group, 2.01 through this staging in half windows,
+        // 1.98 in whole windows; Adam7 RGBA16 6.21, 5.68-5.91, 5.73-5.76,
+        // 5.24 (halves); non-temporal loads 3.53 / 8.85, sc0 no change.
+        v4u T[2][kWH][kSP]; // the next group's units: row half, window part, instruction
+        auto load_units = [&](int g0) {
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int u = 0; u < kWH; u++)
+#pragma unroll
+                    for (int i = 0; i < kSP; i++)
+                        T[h][u][i] = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, voff[h][i],
+                                                                           g0 * CB + 16 * kSP * u, 0);
+        };
+        // unit (h, u) through the staging area into B0 / B1 (in order behind
+        // the previous unit's reads: one wave's LDS instructions do not pass
+        // each other)
+        auto xfer = [&](uint32_t (&d)[GD], int h, int u) {
+#pragma unroll
+            for (int i = 0; i < kSP; i++)
+                *reinterpret_cast<v4u *>(reinterpret_cast<uint8_t *>(stage) + stw[i]) = T[h][u][i];
+            wave_lds_sync();
+#pragma unroll
+            for (int p = 0; p < kSP; p++) {
+                const v4u v = *reinterpret_cast<const v4u *>(reinterpret_cast<const uint8_t *>(stage) + str[p]);
+#pragma unroll
+                for (int e = 0; e < 4; e++) d[4 * (u * kSP + p) + e] = v[e];
+            }
+            wave_lds_sync();
+        };
+        // the slab: each lane's two rows' group pieces, 1 KiB contiguous per instruction
+        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
+            const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
 #pragma unroll
             for (int q = 0; q < NQ; q++) {
-                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, soff1 + g0 * CB + 16 * q, 0, 0);
+                const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
+                const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
 #pragma unroll
-                for (int e = 0; e < 4; e++) d1[4 * q + e] = b[e];
-            }
-        };
-        auto load_group = [&](uint32_t (&d0)[GD], uint32_t (&d1)[GD], int g0) {
-            if constexpr (STREAM) {
-#pragma unroll
-                for (int q = 0; q < NQ; q++) {
-                    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, soff0 + g0 * CB + 16 * q, 0, 0);
-#pragma unroll
-                    for (int e = 0; e < 4; e++) d0[4 * q + e] = a[e];
-                }
-            } else {
-                const int gb = 128 + (g0 / kG) * 2 * NQ * 1024 + lane * 16;
-#pragma unroll
-                for (int q = 0; q < NQ; q++) {
-                    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + q * 1024, 0, 0);
-                    const v4u b = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, gb + (NQ + q) * 1024, 0, 0);
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        d0[4 * q + e] = a[e];
-                        d1[4 * q + e] = b[e];
-                    }
+                for (int e = 0; e < 4; e++) {
+                    d0[4 * q + e] = a[e];
+                    d1[4 * q + e] = b[e];
                 }
             }
         };
@@ -664,8 +717,15 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             }
         };
 
-        load_group(B0, B1, 0);
-        if constexpr (STREAM) load_row1(B1, 0);
+        if constexpr (STREAM) {
+            load_units(0);
+#pragma unroll
+            for (int u = 0; u < kWH; u++) xfer(B0, 0, u);
+#pragma unroll
+            for (int u = 0; u < kWH; u++) xfer(B1, 1, u);
+        } else {
+            load_group(B0, B1, 0);
+        }
         load_window(Wn, 0);
         // A group waits for its inputs with s_waitcnt vmcnt(N), N = the
         // vector memory operations issued since them: the previous group's
@@ -686,7 +746,8 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
                 A1[i] = B1[i];
             }
             W = Wn;
-            load_group(B0, B1, g0 + kG);
+            if constexpr (STREAM) load_units(g0 + kG);
+            else load_group(B0, B1, g0 + kG);
             load_window(Wn, g0 + kG);
             if constexpr (STREAM) {
                 if (g0 < max_skew) { // the ramp: a row's chunks before its first are zeros
@@ -715,8 +776,15 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
             }
 #pragma unroll
             for (int st = 0; st < kG; st++) {
-                if constexpr (STREAM)
-                    if (st == kG / 2) load_row1(B1, g0 + kG);
+                if constexpr (STREAM && kWH == 2) { // the units of the next group, steps 4-7
+                    if (st == 4) xfer(B0, 0, 0);
+                    if (st == 5) xfer(B0, 0, 1);
+                    if (st == 6) xfer(B1, 1, 0);
+                    if (st == 7) xfer(B1, 1, 1);
+                } else if constexpr (STREAM) { // steps 4 and 6
+                    if (st == 4) xfer(B0, 0, 0);
+                    if (st == 6) xfer(B1, 1, 0);
+                }
                 // ---- the row above, one step late: row 2j reads lane j-1's
                 // high row (DPP wave_shr:1; lane 0's `old` is the previous
                 // band's last row, zero without one), row 2j+1 its own low row
