@@ -264,3 +264,23 @@ def test_png_device_slab_matches_model(depth, ct, w, h, il):
     _lib.check(_lib.lib().zpx_debug_png_device_slab(ctx.handle, st.handle, out.ctypes.data, n.value, C.byref(n)),
                ctx.handle)
     check_slab(st, out)
+
+
+def test_png_plans_recreated_at_same_addresses():
+    """Plans of one geometry made and destroyed back to back (their boundary
+    buffers handed out again at the same addresses): each plan's launches
+    use epochs from a base of its own (png_epoch_base), so granules a
+    destroyed plan wrote -- which another XCD's L2 may still hold -- never
+    pass for this launch's; every launch bit-exact, slab and stream
+    instances alternating."""
+    datas = [S.png_tc8_mixed(70 + i, 640, 1000) for i in range(2)]
+    streams = [P.Stream(d) for d in datas]
+    want = [O.png_decode(d).pixels.reshape(-1) for d in datas]
+    for k in range(6):
+        b = device.PngBatch(streams, slots=[0, 1] * 4, layout=("stream", "auto")[k % 2])
+        for _ in range(2):
+            b.launch(torch.cuda.current_stream().cuda_stream)
+        b.status(torch.cuda.current_stream().cuda_stream)
+        for s in range(8):
+            assert np.array_equal(b.output_tensor(s).cpu().numpy().reshape(-1)[:want[s % 2].size], want[s % 2]), (k, s)
+        del b

@@ -189,6 +189,14 @@ DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_
 int jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, DevBuf &planes, DevBuf &desc,
                         HostBuf &hdesc, uint8_t *out, hipStream_t st);
 
+// First epoch of a PNG control block {epoch, ticket, status, sticky}: each
+// plan and batch slot starts its launches' epochs at a base of its own (a
+// process-wide counter from a per-process seed, 2^20 launches apart), so a
+// boundary granule written under another control block -- a destroyed
+// plan's buffer handed out again at the same address, whose line another
+// XCD's L2 may still hold -- never carries an epoch this one's launches use.
+uint32_t png_epoch_base(); // zpx_api.cpp
+
 // The unfilter kernel addresses one band (64 filtered rows + the input pad)
 // through a buffer descriptor with a 31-bit byte range, and row offsets in
 // 32-bit registers: a pass whose band would exceed it is rejected

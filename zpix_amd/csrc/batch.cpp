@@ -241,10 +241,12 @@ int Pipeline::setup()
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming));
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_kernel, hipEventDisableTiming));
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
-        // PNG control words {epoch, ticket, status, pad}: zero once; every
-        // launch bumps the epoch (png_ctl_kernel), so they are never cleared
+        // PNG control words {epoch, ticket, status, pad}: set once (the
+        // slot's own epoch base, png_epoch_base); every launch bumps the
+        // epoch (png_ctl_kernel), so they are never cleared
         HIPCHK(ctx_, s->dctl.alloc(16));
-        HIPCHK(ctx_, hipMemsetAsync(s->dctl.ptr, 0, 16, ctx_->stream));
+        const uint32_t ctl0[4] = {png_epoch_base(), 0, 0, 0};
+        HIPCHK(ctx_, hipMemcpy(s->dctl.ptr, ctl0, 16, hipMemcpyHostToDevice));
         if (!s->hstatus.alloc(16, true)) return ZPX_E_OUT_OF_MEMORY;
         slots_.push_back(std::move(s));
     }

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <unistd.h>
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
@@ -347,7 +348,6 @@ struct PngGroup {
     DevBuf dslab, slab_jobs;
     uint32_t nslab_jobs = 0, slab_max_groups = 0;
     uint32_t nsched2 = 0;       // bands of the second launch (Adam7 pass 6), after the first nsched
-    size_t scratch_zero_bytes = 0;
 };
 
 struct RgbaGroup {
@@ -508,6 +508,14 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
     return guarded([&] { return zpx_jpeg_plan_create_impl(ctx, frames, n_frames, output, out); });
 }
 
+uint32_t zpx::png_epoch_base()
+{
+    static std::atomic<uint32_t> next{static_cast<uint32_t>(
+        std::chrono::steady_clock::now().time_since_epoch().count() ^ (uint64_t(getpid()) << 12))};
+    const uint32_t b = next.fetch_add(1u << 20, std::memory_order_relaxed);
+    return b == 0 || b == ~0u ? 1u : b; // (tag 0 marks never-written granules)
+}
+
 static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPass> &passes_in,
                            const std::vector<uint32_t> &pass_rowbytes)
 {
@@ -530,11 +538,11 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
     if (!sched.empty())
         HIPCHK(ctx, hipMemcpy(g.sched.ptr, sched.data(), sched.size() * sizeof(DevPngBand), hipMemcpyHostToDevice));
     // control words {epoch, ticket, status, pad}; the boundary granules start
-    // with tag 0 and every launch uses a fresh epoch >= 1, so neither needs
-    // clearing per launch
-    g.scratch_zero_bytes = 16;
+    // with tag 0 and every launch uses a fresh epoch from the plan's own base
+    // (png_epoch_base), so neither needs clearing per launch
     HIPCHK(ctx, g.scratch.alloc(16));
-    HIPCHK(ctx, hipMemset(g.scratch.ptr, 0, 16));
+    const uint32_t ctl0[4] = {png_epoch_base(), 0, 0, 0};
+    HIPCHK(ctx, hipMemcpy(g.scratch.ptr, ctl0, 16, hipMemcpyHostToDevice));
     const size_t bbytes = std::max<size_t>(1, size_t(base)) * g.band_bytes * sizeof(uint64_t);
     HIPCHK(ctx, g.boundary.alloc(bbytes));
     HIPCHK(ctx, hipMemset(g.boundary.ptr, 0, bbytes));
@@ -1458,7 +1466,8 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
     const DevPngBand only{0, 1}; // band 1 alone: band 0 never runs, so never publishes
     const uint32_t granules = static_cast<uint32_t>(png_band_granules(ZPX_PNG_TC8, rb));
     HIPCHK(ctx, ctl.alloc(16));
-    HIPCHK(ctx, hipMemset(ctl.ptr, 0, 16));
+    const uint32_t ctl0[4] = {png_epoch_base(), 0, 0, 0};
+    HIPCHK(ctx, hipMemcpy(ctl.ptr, ctl0, 16, hipMemcpyHostToDevice));
     HIPCHK(ctx, bound.alloc(size_t(2) * granules * sizeof(uint64_t)));
     HIPCHK(ctx, hipMemset(bound.ptr, 0, size_t(2) * granules * sizeof(uint64_t)));
     HIPCHK(ctx, dpass.alloc(sizeof(DevPngPass)));
