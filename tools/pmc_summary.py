@@ -4,6 +4,10 @@ traffic per launch that bench.py reports as roofline.traffic.
 
 Usage: python3 tools/pmc_summary.py <pass dir root> [traffic.json out] [images] [size]
 
+Per kernel instance, each counter is the median over its dispatches of the
+per-dispatch total (the bench's batch launches outnumber its small check
+launches of the same instance).
+
 HBM bytes: FETCH_SIZE x 2 (gfx950 tallies a 128-B streaming read request as
 64 B, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KiB.  A bench line
 whose plan runs several kernels (Adam7: two launches of the paired-row
@@ -36,6 +40,7 @@ KEYS = [
     (r"rgba_batch_kernel<6>", "rgba_pixels"),  # (NRGBA64, the bench's rgbaPixels line)
     (r"rgba_pixels_kernel", "rgba_pixels_generic"),
     (r"jpeg_sparse_expand", "jpeg_sparse_expand"),
+    (r"jpeg_pieces_expand", "jpeg_pieces_expand"),
 ]
 
 
@@ -63,12 +68,17 @@ def summarise(base):
             short = short_name(r["Kernel_Name"])
             if short:
                 acc[short][(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
+    # per kernel instance and counter: the MEDIAN over its dispatches of the
+    # per-dispatch total.  (A run's parity gates and single-image checks
+    # launch the same instance on far smaller plans; a mean over all
+    # dispatches mixed them in -- Adam7 RGBA16 read 19.6 GB a launch that
+    # way, 23.5 with the median.)
     out = {}
     for k, d in acc.items():
         per = collections.defaultdict(list)
         for (cn, _), vals in d.items():
             per[cn].append(sum(vals))
-        out[k] = {cn: sum(v) / len(v) for cn, v in per.items()}
+        out[k] = {cn: sorted(v)[len(v) // 2] for cn, v in per.items()}
         out[k]["dispatches"] = max(len(v) for v in per.values())
     return out
 
