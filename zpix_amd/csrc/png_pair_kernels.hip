@@ -565,9 +565,12 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
 #pragma unroll
                 for (int u = 0; u < kWH; u++)
 #pragma unroll
-                    for (int i = 0; i < kSP; i++)
-                        T[h][u][i] = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, voff[h][i],
-                                                                           g0 * CB + 16 * kSP * u, 0);
+                    for (int i = 0; i < kSP; i++) // (the whole offset in voffset: the
+                        // range check leaves a raw buffer's soffset out, and past the
+                        // band's last group these offsets must read zeros, not the
+                        // bytes after the stream)
+                        T[h][u][i] = __builtin_amdgcn_raw_buffer_load_b128(
+                            in_rsrc, voff[h][i] + g0 * CB + 16 * kSP * u, 0, 0);
         };
         // unit (h, u) through the staging area into B0 / B1 (in order behind
         // the previous unit's reads: one wave's LDS instructions do not pass
