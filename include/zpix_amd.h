@@ -33,7 +33,12 @@
 extern "C" {
 #endif
 
-#define ZPX_ABI_VERSION 1
+/* Version of this header's structs and entry points.  2: zpx_jpeg_frame
+ * gained `layout`, `pieces` and `pieces_bytes` (ZPX_COEFFS_PIECES), which
+ * changed its size, so an array of version-1 frames is read at the wrong
+ * offsets; zpx_abi_version() returns the library's value, and a binding
+ * checks it against the header it was generated from. */
+#define ZPX_ABI_VERSION 2
 
 typedef struct zpx_ctx zpx_ctx;
 
@@ -138,6 +143,8 @@ enum zpx_status {
 #define ZPX_OK ZPX_E_OK
 /* Name of any status code ("Ok", "UnexpectedEof", ... as in the reference). */
 const char *zpx_error_name(int code);
+/* ZPX_ABI_VERSION of the library's build. */
+int zpx_abi_version(void);
 /* Detail message of the last failure on this context (never NULL). */
 const char *zpx_last_error(const zpx_ctx *ctx);
 
@@ -406,8 +413,10 @@ typedef struct zpx_png_frame {
  * readImagePass (png/decoder.zig:649-1149, 1289-1373).  Filter bytes must be
  * valid (<= 4): the host checks them (InvalidFilterType) before planning.
  * Kernels: the paired-row kernel for RGB8/RGBA8/Gray8/Gray16/RGB16/RGBA16
- * (interlaced or not, tRNS colour keys on RGB; either layout: a STREAM frame's
- * slab is built on the device inside the launch), the one-row-per-lane kernel
+ * (interlaced or not, tRNS colour keys on RGB; either layout: its stream
+ * instance reads a STREAM frame's inflated rows directly, its slab instance
+ * a SLAB frame's band slab -- a slab built on the device from a STREAM frame
+ * is a test-only path, the switch "png_device_slab"), the one-row-per-lane kernel
  * for every other depth (sub-byte gray, paletted, gray+alpha) and for STREAM
  * frames the paired-row kernel declines (png_pair_supported: e.g. rows shorter
  * than one 12/16-byte chunk, bands past the 2 GiB buffer range). */
@@ -626,7 +635,11 @@ int zpx_debug_shard_fake_comm(int on);
  *                 get their band slab built on the device at each launch
  *                 and read it (default 0: the kernel reads the stream);
  *   "qoi_segment" pixels per lane segment of the QOI encoder (16..4096;
- *                 default 0 = 128). */
+ *                 default 0 = 128);
+ *   "png_epoch_cycle" epochs a PNG control block cycles through before its
+ *                 boundary buffer is cleared and the epoch re-based (>= 4;
+ *                 default 0 = 2^20, the whole window; blocks created after
+ *                 the call take it): a short cycle runs the wrap path. */
 int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the
  * ZPX_COEFFS_PIECES form the batch pipeline uploads and

@@ -9,7 +9,8 @@
 //     the image, pass 6 pointing at its merge job, and
 //     png_plan_bands putting passes 6-7 (and only those) in the second
 //     launch's schedule;
-//   - dev_jpeg_frame: the quant-pair tables of the block kernel's row pass.
+//   - dev_jpeg_frame: the quant-pair tables of the block kernel's row pass;
+//   - the PNG epoch windows and cycle (check_epoch_windows).
 // Prints "ok" and exits 0, or names the first failed check and exits 1.
 #include <cstdio>
 #include <cstdlib>
@@ -48,6 +49,69 @@ static void check_schedule(const std::vector<DevPngPass> &passes, uint32_t band_
         if (s[t].band > 0) CHECK(ticket.at({s[t].pass, s[t].band - 1}) < t);
         if (t > 0) CHECK(p[s[t - 1].pass].row_bytes >= p[s[t].pass].row_bytes); // longest first
     }
+}
+
+// PNG epoch windows (api_internal.h, PngControl): every live owner holds a
+// window of its own, never window 0; a released window is handed out again
+// only after every other free one; the registry is exhausted at 4095 live
+// owners; the control kernel's epoch sequence (png_epoch_next) never leaves
+// [base + 1, base + cycle), never reaches 0, and png_epoch_wraps predicts
+// exactly the launches at which it wraps.
+static void check_epoch_windows()
+{
+    const uint32_t n = kPngEpochWindows - 1;
+    std::vector<int> owners(n + 8);
+    std::vector<uint32_t> got;
+    std::map<uint32_t, int> seen;
+    for (uint32_t i = 0; i < n; i++) { // (other blocks of this process may hold none: no GPU here)
+        const uint32_t w = png_epoch_window_acquire(&owners[i]);
+        CHECK(w >= 1 && w < kPngEpochWindows);
+        CHECK(seen.count(w) == 0);
+        seen[w] = int(i);
+        got.push_back(w);
+    }
+    CHECK(png_epoch_window_acquire(&owners[n]) == 0); // exhausted
+    CHECK(!png_epoch_window_release(got[5], &owners[6])); // not its owner
+    CHECK(png_epoch_window_owned(got[5], &owners[5]) && !png_epoch_window_owned(got[5], &owners[6]));
+    CHECK(png_epoch_window_release(got[5], &owners[5]));
+    CHECK(!png_epoch_window_owned(got[5], &owners[5]));
+    CHECK(png_epoch_window_acquire(&owners[n + 1]) == got[5]); // the only free one
+    CHECK(png_epoch_window_release(got[5], &owners[n + 1]));
+    CHECK(png_epoch_window_release(got[7], &owners[7]));
+    // round robin: got[5] was returned first, but the cursor stands past
+    // got[5]'s window, so got[7]'s window comes first unless it lies before
+    const uint32_t a = png_epoch_window_acquire(&owners[n + 2]), b = png_epoch_window_acquire(&owners[n + 3]);
+    CHECK(a != b && (a == got[5] || a == got[7]) && (b == got[5] || b == got[7]));
+    CHECK(png_epoch_window_release(a, &owners[n + 2]) && png_epoch_window_release(b, &owners[n + 3]));
+    for (uint32_t i = 0; i < n; i++)
+        if (i != 5 && i != 7) CHECK(png_epoch_window_release(got[i], &owners[i]));
+    CHECK(!png_epoch_window_release(0, nullptr));
+    // a freed registry hands out a window other than the one just returned
+    const uint32_t c = png_epoch_window_acquire(&owners[0]);
+    CHECK(c != 0 && c != got[n - 1]);
+    CHECK(png_epoch_window_release(c, &owners[0]));
+
+    // the epoch sequence of one block, simulated over several cycles
+    for (uint32_t cycle : {4u, 5u, 17u}) {
+        const uint32_t base = 3 * kPngEpochWindow;
+        uint32_t e = base, shadow = base;
+        for (int launch = 0; launch < 100; launch++) {
+            const int k = launch % 3 == 0 ? 2 : 1; // (an Adam7 item: two launches)
+            if (png_epoch_wraps(shadow, base, cycle, k)) shadow = e = base; // the host's re-base
+            for (int i = 0; i < k; i++) {
+                const uint32_t nx = png_epoch_next(e, base, cycle);
+                CHECK(nx > e); // no wrap inside launches the host announced
+                e = nx;
+                CHECK(e > base && e < base + cycle && e != 0);
+            }
+            shadow = e;
+        }
+    }
+    // the device's own wrap (launches the host does not see) and the extremes
+    CHECK(png_epoch_next(5 * kPngEpochWindow + 9, 5 * kPngEpochWindow, 10) == 5 * kPngEpochWindow + 1);
+    const uint32_t top = (kPngEpochWindows - 1) * kPngEpochWindow;
+    CHECK(png_epoch_next(top + kPngEpochWindow - 1, top, kPngEpochWindow) == top + 1); // 0xffffffff -> never 0
+    CHECK(png_epoch_next(0, top, kPngEpochWindow) == top + 1); // a corrupted word re-enters the window
 }
 
 int main()
@@ -166,6 +230,7 @@ int main()
                 CHECK((v & 0xffff) == uint32_t(jf.qt[c][8 * r + lo[k]]) && (v >> 16) == uint32_t(jf.qt[c][8 * r + hi[k]]));
             }
 
+    check_epoch_windows();
     if (fails) return 1;
     printf("ok\n");
     return 0;

@@ -269,7 +269,7 @@ def test_png_device_slab_matches_model(depth, ct, w, h, il):
 def test_png_plans_recreated_at_same_addresses():
     """Plans of one geometry made and destroyed back to back (their boundary
     buffers handed out again at the same addresses): each plan's launches
-    use epochs from a base of its own (png_epoch_base), so granules a
+    use epochs from a window of their own (PngControl), so granules a
     destroyed plan wrote -- which another XCD's L2 may still hold -- never
     pass for this launch's; every launch bit-exact, slab and stream
     instances alternating."""
@@ -284,3 +284,71 @@ def test_png_plans_recreated_at_same_addresses():
         for s in range(8):
             assert np.array_equal(b.output_tensor(s).cpu().numpy().reshape(-1)[:want[s % 2].size], want[s % 2]), (k, s)
         del b
+
+
+class _EpochCycle:
+    """Test switch png_epoch_cycle: control blocks created inside the block
+    cycle through `n` epochs, so their launches wrap (PngControl)."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        from zpix_amd import _lib
+        self.prev = _lib.lib().zpx_debug_option(b"png_epoch_cycle", self.n)
+
+    def __exit__(self, *exc):
+        from zpix_amd import _lib
+        _lib.lib().zpx_debug_option(b"png_epoch_cycle", self.prev)
+
+
+EPOCH_CASES = {
+    "tc8": lambda seed: S.png_tc8_mixed(seed, 700, 900),            # paired-row kernel
+    "adam7_rgba16": lambda seed: S.png_rgba16_adam7(seed, 300, 520),  # two launches a plan launch
+    "ga8": lambda seed: S.png_generic(seed, 333, 300, 8, 4),          # one-row-per-lane kernel
+}
+
+
+@pytest.mark.parametrize("case", sorted(EPOCH_CASES))
+def test_png_epoch_cycle_wraps_with_changing_input(case):
+    """A plan whose control block wraps its epoch cycle every few launches
+    (png_epoch_cycle 4; Adam7 groups take two epochs a launch): the input
+    bytes change between launches -- two images of one geometry, different
+    filters and pixels, swapped in place -- so a band that took a granule
+    left from an earlier launch would unfilter from the wrong row above and
+    differ.  Every launch bit-exact against the oracle (readImagePass,
+    png/decoder.zig:798-842)."""
+    a, b = EPOCH_CASES[case](301), EPOCH_CASES[case](302)
+    st = torch.cuda.current_stream().cuda_stream
+    with _EpochCycle(4):
+        streams = [P.Stream(a), P.Stream(b)]
+        want = [O.png_decode(d).pixels.reshape(-1) for d in (a, b)]
+        data = [s.filtered() for s in streams]
+        assert len(data[0]) == len(data[1])
+        bt = device.PngBatch(streams, slots=[0], layout="stream")
+        n = len(data[0])
+        for k in range(11):
+            bt.in_arena[:n].copy_(torch.from_numpy(data[k % 2]))
+            bt.out_arena.zero_()
+            bt.launch(st)
+            bt.status(st)
+            got = bt.output_tensor(0).cpu().numpy().reshape(-1)[:want[k % 2].size]
+            assert np.array_equal(got, want[k % 2]), k
+
+
+def test_png_epoch_cycle_wraps_in_batch_slots():
+    """The batch pipeline's slots with a 4-epoch cycle: one slot decodes PNGs
+    of changing geometry one after the other (so a granule may stay unread
+    for many launches), wrapping several times; every image bit-exact."""
+    from zpix_amd import batch
+    bufs = []
+    for i in range(14):
+        w, h = 90 + 37 * (i % 5), 140 + 61 * (i % 3)
+        bufs.append(S.png_rgba16_adam7(400 + i, w, h) if i % 3 == 0 else S.png_tc8_mixed(400 + i, w, h))
+    with _EpochCycle(4):
+        res = batch.decode_rgba(bufs, host_threads=1, depth=1)
+    for data, r in zip(bufs, res):
+        img = O.png_decode(data)
+        want = img.rgba_pixels().reshape(img.height, img.width, 4)
+        assert r.status == "Ok"
+        assert np.array_equal(r.rgba.cpu().numpy(), want)

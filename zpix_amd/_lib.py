@@ -147,8 +147,11 @@ class zpx_gather_stats(C.Structure):
 
 
 # every symbol include/zpix_amd.h declares (checked by tests/test_abi.py)
+# ZPX_ABI_VERSION of include/zpix_amd.h that the structs below mirror
+ABI_VERSION = 2
+
 EXPORTS = [
-    "zpx_error_name", "zpx_last_error", "zpx_ctx_create", "zpx_ctx_destroy", "zpx_ctx_stream",
+    "zpx_abi_version", "zpx_error_name", "zpx_last_error", "zpx_ctx_create", "zpx_ctx_destroy", "zpx_ctx_stream",
     "zpx_ctx_device", "zpx_ctx_synchronize", "zpx_image_free", "zpx_image_rgba_pixels",
     "zpx_jpeg_decode", "zpx_jpeg_load", "zpx_jpeg_probe_buffer", "zpx_jpeg_decode_rgba",
     "zpx_png_decode", "zpx_png_load", "zpx_png_probe_buffer", "zpx_from_buffer", "zpx_from_file_path",
@@ -178,6 +181,7 @@ def lib():
     L = C.CDLL(LIB_PATH)
     vp, i32, sz, u8p = C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_uint8)
     sig = {
+        "zpx_abi_version": (i32, []),
         "zpx_error_name": (C.c_char_p, [i32]),
         "zpx_last_error": (C.c_char_p, [vp]),
         "zpx_ctx_create": (i32, [i32, C.POINTER(vp)]),
@@ -249,6 +253,8 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.zpx_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} is ABI version {L.zpx_abi_version()}; this binding mirrors {ABI_VERSION}")
     _lib = L
     return L
 

@@ -189,13 +189,64 @@ DevImage dev_image_of(const zpx_image *img, const void *d_pixels, const void *d_
 int jpeg_planes_to_rgba(zpx_ctx *ctx, const JpegCoeffs &c, zpx_jpeg_frame f, DevBuf &planes, DevBuf &desc,
                         HostBuf &hdesc, uint8_t *out, hipStream_t st);
 
-// First epoch of a PNG control block {epoch, ticket, status, sticky}: each
-// plan and batch slot starts its launches' epochs at a base of its own (a
-// process-wide counter from a per-process seed, 2^20 launches apart), so a
-// boundary granule written under another control block -- a destroyed
-// plan's buffer handed out again at the same address, whose line another
-// XCD's L2 may still hold -- never carries an epoch this one's launches use.
-uint32_t png_epoch_base(); // zpx_api.cpp
+// PNG control block of a plan group or batch slot (device_types.h layout:
+// {epoch, ticket, status, sticky, base, cycle, 0, 0}) and the epoch window
+// it owns.  Boundary granules carry the epoch of the launch that wrote them;
+// a band accepts a granule only when it carries its own launch's epoch.  So
+// a launch's epoch must differ from every tag its boundary buffer may hold:
+//   - windows: every live block owns a window of its own (a process-wide
+//     registry, handed out round robin from a per-process start and
+//     returned when the block is destroyed), so two blocks never share an
+//     epoch -- a destroyed block's buffer handed out again at the same
+//     address holds tags of another window;
+//   - cycle: a block's launches take base + 1 .. base + cycle - 1 in turn
+//     (png_epoch_next: never 0, never base).  Before the launches that would
+//     wrap the cycle, prepare() clears the boundary buffer and re-bases the
+//     epoch on the launch stream, so a granule left from any earlier launch
+//     -- a slot's previous image of another geometry, a timed-out launch --
+//     holds a tag no later launch of this cycle uses.  (Launches the host
+//     does not issue -- a captured graph replayed -- wrap on the device
+//     without the clear; a plan's launches rewrite every granule they read,
+//     so its granules hold the previous launch's epoch, never the next.)
+// The cycle is kPngEpochWindow (2^20 launches) unless the test switch
+// "png_epoch_cycle" sets a shorter one (>= 4).
+uint32_t png_epoch_window_acquire(const void *owner); // 0: every window is taken
+bool png_epoch_window_release(uint32_t window, const void *owner);
+bool png_epoch_window_owned(uint32_t window, const void *owner);
+// The launches that would wrap: the control kernel's next `launches` epochs
+// from `shadow` leave the cycle (host mirror of png_epoch_next).
+inline bool png_epoch_wraps(uint32_t shadow, uint32_t base, uint32_t cycle, int launches)
+{
+    for (int i = 0; i < launches; i++) {
+        const uint32_t e = png_epoch_next(shadow, base, cycle);
+        if (e <= shadow) return true;
+        shadow = e;
+    }
+    return false;
+}
+class PngControl {
+  public:
+    PngControl() = default;
+    PngControl(const PngControl &) = delete;
+    PngControl &operator=(const PngControl &) = delete;
+    ~PngControl();
+    // Takes a window and allocates + initialises the block on the current
+    // device (synchronously).  ZPX_E_OUT_OF_MEMORY when all 4095 windows
+    // belong to live blocks.
+    int init(zpx_ctx *ctx);
+    // Before enqueueing `launches` control-kernel launches on `st`: checks
+    // that the block still owns its window (ZPX_E_PANIC otherwise) and, when
+    // one of them would wrap the cycle, clears `boundary` (bytes) and resets
+    // the epoch to base on `st` first.
+    int prepare(zpx_ctx *ctx, int launches, void *boundary, size_t bytes, hipStream_t st);
+    uint32_t *words() const { return ctl_.as<uint32_t>(); }
+    uint32_t window() const { return window_; }
+    uint32_t wraps() const { return wraps_; } // re-bases so far (tests)
+
+  private:
+    DevBuf ctl_;
+    uint32_t window_ = 0, base_ = 0, cycle_ = 0, shadow_ = 0, wraps_ = 0;
+};
 
 // The unfilter kernel addresses one band (64 filtered rows + the input pad)
 // through a buffer descriptor with a 31-bit byte range, and row offsets in

@@ -74,7 +74,8 @@ struct Decoded {
 };
 
 struct Slot {
-    DevBuf din, dout, dimg, ddesc, dctl, dbound, dgrid, dstage; // dstage: Adam7 passes 1-5 (Adam7Stage)
+    DevBuf din, dout, dimg, ddesc, dbound, dgrid, dstage; // dstage: Adam7 passes 1-5 (Adam7Stage)
+    PngControl ctl; // PNG control block and its epoch window
     DevBuf dslab; // the paired-row kernel's band slab, built on the device (png_slab_kernels.hip)
     HostBuf hdesc, hstatus; // pinned descriptor staging, PNG status word
     hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
@@ -241,12 +242,10 @@ int Pipeline::setup()
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming));
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_kernel, hipEventDisableTiming));
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
-        // PNG control words {epoch, ticket, status, pad}: set once (the
-        // slot's own epoch base, png_epoch_base); every launch bumps the
-        // epoch (png_ctl_kernel), so they are never cleared
-        HIPCHK(ctx_, s->dctl.alloc(16));
-        const uint32_t ctl0[4] = {png_epoch_base(), 0, 0, 0};
-        HIPCHK(ctx_, hipMemcpy(s->dctl.ptr, ctl0, 16, hipMemcpyHostToDevice));
+        // PNG control block: set once (the slot's own epoch window,
+        // PngControl); every launch moves the epoch on (png_ctl_kernel),
+        // and issue_png re-bases it, clearing the boundary, before a wrap
+        if (int e = s->ctl.init(ctx_)) return e;
         if (!s->hstatus.alloc(16, true)) return ZPX_E_OUT_OF_MEMORY;
         slots_.push_back(std::move(s));
     }
@@ -555,18 +554,22 @@ int Pipeline::issue_png(Slot &s)
     // folds the previous launch's status into `sticky`, so an Adam7 item's
     // first launch reports through sticky -- clear it for this item (the
     // slot's words are reused) and read both words after the last launch
-    HIPCHK(ctx_, hipMemsetAsync(s.dctl.as<uint32_t>() + 3, 0, 4, ctx_->stream));
-    const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, !dev_slab, dp, dsch, ns, s.dctl.as<uint32_t>(),
+    HIPCHK(ctx_, hipMemsetAsync(s.ctl.words() + 3, 0, 4, ctx_->stream));
+    // (a slot's images differ in geometry, so a granule may outlive many
+    // launches unread: before the launches that would wrap the epoch cycle
+    // the boundary buffer is cleared)
+    if (int e = s.ctl.prepare(ctx_, ns2 ? 2 : 1, s.dbound.ptr, s.dbound.bytes, ctx_->stream)) return e;
+    const int lrc = pair ? launch_png_pair(ps.depth, ps.use_transparent, !dev_slab, dp, dsch, ns, s.ctl.words(),
                                            s.dbound.as<uint64_t>(), granules, ctx_->stream)
-                         : launch_png_unfilter(ps.depth, dp, dsch, ns, s.dctl.as<uint32_t>(), s.dbound.as<uint64_t>(),
+                         : launch_png_unfilter(ps.depth, dp, dsch, ns, s.ctl.words(), s.dbound.as<uint64_t>(),
                                                granules, ctx_->stream);
     if (lrc)
         return hip_fail(ctx_, hipGetLastError(), "batch: png kernel");
     // Adam7: pass 6 merges the staged passes once the first launch is done
-    if (ns2 && launch_png_pair_merge(ps.depth, ps.use_transparent, !dev_slab, dp, dsch + ns, ns2, s.dctl.as<uint32_t>(),
+    if (ns2 && launch_png_pair_merge(ps.depth, ps.use_transparent, !dev_slab, dp, dsch + ns, ns2, s.ctl.words(),
                                      s.dbound.as<uint64_t>(), granules, ctx_->stream))
         return hip_fail(ctx_, hipGetLastError(), "batch: png adam7 merge pass");
-    HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.dctl.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost, ctx_->stream));
+    HIPCHK(ctx_, hipMemcpyAsync(s.hstatus.ptr, s.ctl.words() + 2, 8, hipMemcpyDeviceToHost, ctx_->stream));
     s.check_png = true;
     if (rgba_native) {
         if (direct) {

@@ -105,6 +105,23 @@ struct DevPngBand {
     uint32_t band;
 };
 
+// PNG control block, kPngCtlWords device words:
+//   {epoch, ticket, status, sticky, base, cycle, 0, 0}
+// Each launch's control kernel moves `epoch` on with png_epoch_next; the
+// block owns the epoch window [base, base + kPngEpochWindow) (PngControl,
+// api_internal.h), base = window index * kPngEpochWindow with index >= 1,
+// and its launches cycle through base + 1 .. base + cycle - 1 of it.  So an
+// epoch is never 0 (the tag of never-written granules) nor another live
+// block's, whatever the number of launches.
+constexpr int kPngCtlWords = 8;
+constexpr uint32_t kPngEpochWindow = 1u << 20;
+constexpr uint32_t kPngEpochWindows = 4096; // (window 0 holds tag 0: never handed out)
+// (constexpr: a host and device function both)
+constexpr uint32_t png_epoch_next(uint32_t epoch, uint32_t base, uint32_t cycle)
+{
+    return epoch + 1u - base < cycle ? epoch + 1u : base + 1u;
+}
+
 } // namespace zpx
 
 namespace zpx {

@@ -754,12 +754,13 @@ __global__ __launch_bounds__(64) void png_unfilter_kernel(const DevPngPass *__re
     }
 }
 
-// Per-launch control block: epoch++ (fresh granule tags, so the boundary
-// buffer never needs clearing), ticket = 0, the previous launch's status
+// Per-launch control block: the next epoch of the block's window (fresh
+// granule tags, so the boundary buffer needs clearing only when the cycle
+// wraps: PngControl::prepare), ticket = 0, the previous launch's status
 // folded into the sticky word (read and cleared by zpx_plan_status), status = 0.
 __global__ void png_ctl_kernel(uint32_t *ctl)
 {
-    ctl[0] += 1;
+    ctl[0] = png_epoch_next(ctl[0], ctl[4], ctl[5]);
     ctl[1] = 0;
     ctl[3] |= ctl[2];
     ctl[2] = 0;

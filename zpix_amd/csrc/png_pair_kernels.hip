@@ -935,11 +935,12 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
     }
 }
 
-// Per-launch control block (as png_kernels.hip): epoch++, ticket = 0, the
-// previous launch's status folded into the sticky word, status = 0.
+// Per-launch control block (as png_kernels.hip): the next epoch of the
+// block's window, ticket = 0, the previous launch's status folded into the
+// sticky word, status = 0.
 __global__ void png_pair_ctl_kernel(uint32_t *ctl)
 {
-    ctl[0] += 1;
+    ctl[0] = png_epoch_next(ctl[0], ctl[4], ctl[5]);
     ctl[1] = 0;
     ctl[3] |= ctl[2];
     ctl[2] = 0;

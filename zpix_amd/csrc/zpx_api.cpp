@@ -35,6 +35,8 @@ static const char *const kErrorNames[] = {
 #undef ZPX_NAME_
 };
 
+extern "C" int zpx_abi_version(void) { return ZPX_ABI_VERSION; }
+
 extern "C" const char *zpx_error_name(int code)
 {
     if (code < 0 || code >= ZPX_E__COUNT) return "Unknown";
@@ -118,9 +120,19 @@ DevImage zpx::dev_image_of(const zpx_image *img, const void *d_pixels, const voi
     return m;
 }
 
+// A Paletted image's palette as the colour kernels read it: at most 256
+// entries (an index byte's range; the kernel reads entry i < palette_len),
+// present whenever it has any
+static bool palette_ok(const zpx_image &im)
+{
+    if (im.kind != ZPX_PALETTED) return true;
+    return im.palette_len >= 0 && im.palette_len <= 256 && (im.palette_len == 0 || im.palette != nullptr);
+}
+
 extern "C" int zpx_dev_rgba_pixels(zpx_ctx *ctx, const zpx_image *img, uint8_t *out, void *stream)
 {
     if (!ctx || !img || !out) return ZPX_E_INVALID_ARGUMENT;
+    if (!palette_ok(*img)) return ZPX_E_INVALID_ARGUMENT;
     if (img->min_x != 0 || img->min_y != 0) return ZPX_E_UNSUPPORTED; // decoders always return min = (0,0)
     CtxScope s(ctx);
     const DevImage m = dev_image_of(img, img->pixels, img->palette);
@@ -135,6 +147,7 @@ static int zpx_image_rgba_pixels_impl(zpx_ctx *ctx, const zpx_allocator *al, con
     if (!ctx || !img || !out || !out_len) return ZPX_E_INVALID_ARGUMENT;
     *out = nullptr;
     *out_len = 0;
+    if (!palette_ok(*img)) return ZPX_E_INVALID_ARGUMENT;
     if (img->min_x != 0 || img->min_y != 0) return ZPX_E_UNSUPPORTED;
     CtxScope s(ctx);
     const size_t w = size_t(img->max_x - img->min_x), h = size_t(img->max_y - img->min_y);
@@ -142,9 +155,10 @@ static int zpx_image_rgba_pixels_impl(zpx_ctx *ctx, const zpx_allocator *al, con
     DevBuf dpix, dpal, dout;
     HIPCHK(ctx, dpix.alloc(img->pixels_len));
     HIPCHK(ctx, hipMemcpyAsync(dpix.ptr, img->pixels, img->pixels_len, hipMemcpyHostToDevice, ctx->stream));
-    if (img->kind == ZPX_PALETTED && img->palette) {
+    if (img->kind == ZPX_PALETTED && img->palette_len > 0) { // (its palette_len entries: the rest are never read)
         HIPCHK(ctx, dpal.alloc(256 * sizeof(zpx_color)));
-        HIPCHK(ctx, hipMemcpyAsync(dpal.ptr, img->palette, 256 * sizeof(zpx_color), hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(dpal.ptr, img->palette, size_t(img->palette_len) * sizeof(zpx_color),
+                                   hipMemcpyHostToDevice, ctx->stream));
     }
     HIPCHK(ctx, dout.alloc(n));
     const DevImage m = dev_image_of(img, dpix.ptr, dpal.ptr);
@@ -339,7 +353,8 @@ struct PngGroup {
     bool pair = false; // png_pair_kernel (128-row bands) or png_unfilter_kernel (64)
     bool trns = false; // (pair kernel) the images carry a tRNS colour key
     bool stream = false; // (pair kernel) its stream instance: the frames' inflated streams as they are
-    DevBuf passes, sched, scratch, boundary;
+    DevBuf passes, sched, boundary;
+    PngControl ctl; // {epoch, ticket, status, sticky, ...} and the group's epoch window
     uint32_t nsched = 0, band_bytes = 0, nbands = 0;
     DevBuf staging, merge_jobs; // Adam7 passes 1-5 and pass 6's merge jobs (Adam7Stage)
     // stream-layout frames of the paired-row kernel under the test switch
@@ -508,12 +523,79 @@ extern "C" int zpx_jpeg_plan_create(zpx_ctx *ctx, const zpx_jpeg_frame *frames, 
     return guarded([&] { return zpx_jpeg_plan_create_impl(ctx, frames, n_frames, output, out); });
 }
 
-uint32_t zpx::png_epoch_base()
+// ---- PNG epoch windows (api_internal.h, PngControl)
+namespace {
+std::mutex g_win_mu;
+const void *g_win_owner[kPngEpochWindows] = {};
+uint32_t g_win_next = 0; // next window to try (0: not yet seeded)
+} // namespace
+
+uint32_t zpx::png_epoch_window_acquire(const void *owner)
 {
-    static std::atomic<uint32_t> next{static_cast<uint32_t>(
-        std::chrono::steady_clock::now().time_since_epoch().count() ^ (uint64_t(getpid()) << 12))};
-    const uint32_t b = next.fetch_add(1u << 20, std::memory_order_relaxed);
-    return b == 0 || b == ~0u ? 1u : b; // (tag 0 marks never-written granules)
+    constexpr uint32_t n = kPngEpochWindows - 1; // windows 1 .. n
+    std::lock_guard<std::mutex> lk(g_win_mu);
+    if (g_win_next == 0) // (a per-process start: two processes' blocks rarely share windows either)
+        g_win_next = 1 + static_cast<uint32_t>((uint64_t(getpid()) * 2654435761u) % n);
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t w = 1 + (g_win_next - 1 + k) % n;
+        if (g_win_owner[w]) continue;
+        g_win_owner[w] = owner;
+        g_win_next = w % n + 1; // round robin: a returned window is the last to be handed out again
+        return w;
+    }
+    return 0;
+}
+
+bool zpx::png_epoch_window_release(uint32_t window, const void *owner)
+{
+    std::lock_guard<std::mutex> lk(g_win_mu);
+    if (window == 0 || window >= kPngEpochWindows || g_win_owner[window] != owner) return false;
+    g_win_owner[window] = nullptr;
+    return true;
+}
+
+bool zpx::png_epoch_window_owned(uint32_t window, const void *owner)
+{
+    std::lock_guard<std::mutex> lk(g_win_mu);
+    return window != 0 && window < kPngEpochWindows && g_win_owner[window] == owner;
+}
+
+zpx::PngControl::~PngControl()
+{
+    if (window_) (void)png_epoch_window_release(window_, this);
+}
+
+int zpx::PngControl::init(zpx_ctx *ctx)
+{
+    if (!window_) window_ = png_epoch_window_acquire(this);
+    if (!window_) {
+        ctx->last_error = "png: every epoch window belongs to a live plan or batch slot (4095)";
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+    const int c = opt(Opt::PngEpochCycle);
+    base_ = window_ * kPngEpochWindow;
+    cycle_ = c >= 4 && uint32_t(c) < kPngEpochWindow ? uint32_t(c) : kPngEpochWindow;
+    shadow_ = base_;
+    HIPCHK(ctx, ctl_.alloc(kPngCtlWords * sizeof(uint32_t)));
+    const uint32_t w[kPngCtlWords] = {base_, 0, 0, 0, base_, cycle_, 0, 0};
+    HIPCHK(ctx, hipMemcpy(ctl_.ptr, w, sizeof(w), hipMemcpyHostToDevice));
+    return ZPX_OK;
+}
+
+int zpx::PngControl::prepare(zpx_ctx *ctx, int launches, void *boundary, size_t bytes, hipStream_t st)
+{
+    if (!png_epoch_window_owned(window_, this)) {
+        ctx->last_error = "png: control block launched without its epoch window";
+        return ZPX_E_PANIC;
+    }
+    if (png_epoch_wraps(shadow_, base_, cycle_, launches)) {
+        HIPCHK(ctx, hipMemsetAsync(boundary, 0, bytes, st));
+        HIPCHK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctl_.ptr), static_cast<int>(base_), 1, st));
+        shadow_ = base_;
+        wraps_++;
+    }
+    for (int i = 0; i < launches; i++) shadow_ = png_epoch_next(shadow_, base_, cycle_);
+    return ZPX_OK;
 }
 
 static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPass> &passes_in,
@@ -537,15 +619,14 @@ static int png_build_group(zpx_ctx *ctx, PngGroup &g, const std::vector<DevPngPa
     HIPCHK(ctx, g.sched.alloc(std::max<size_t>(1, sched.size()) * sizeof(DevPngBand)));
     if (!sched.empty())
         HIPCHK(ctx, hipMemcpy(g.sched.ptr, sched.data(), sched.size() * sizeof(DevPngBand), hipMemcpyHostToDevice));
-    // control words {epoch, ticket, status, pad}; the boundary granules start
-    // with tag 0 and every launch uses a fresh epoch from the plan's own base
-    // (png_epoch_base), so neither needs clearing per launch
-    HIPCHK(ctx, g.scratch.alloc(16));
-    const uint32_t ctl0[4] = {png_epoch_base(), 0, 0, 0};
-    HIPCHK(ctx, hipMemcpy(g.scratch.ptr, ctl0, 16, hipMemcpyHostToDevice));
+    // the control block and its epoch window (PngControl); the boundary
+    // granules start with tag 0, which no epoch is -- cleared and complete
+    // before the first launch, whichever stream that is on
+    if (int e = g.ctl.init(ctx)) return e;
     const size_t bbytes = std::max<size_t>(1, size_t(base)) * g.band_bytes * sizeof(uint64_t);
     HIPCHK(ctx, g.boundary.alloc(bbytes));
-    HIPCHK(ctx, hipMemset(g.boundary.ptr, 0, bbytes));
+    HIPCHK(ctx, hipMemsetAsync(g.boundary.ptr, 0, bbytes, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }
 
@@ -730,7 +811,8 @@ static int zpx_rgba_plan_create_impl(zpx_ctx *ctx, const zpx_image *imgs, uint8_
     for (int i = 0; i < n; i++) {
         const zpx_image &im = imgs[i];
         if (im.min_x != 0 || im.min_y != 0) return ZPX_E_UNSUPPORTED;
-        if (im.kind < ZPX_GRAY || im.kind > ZPX_PALETTED || !outs[i] || !im.pixels) return ZPX_E_INVALID_ARGUMENT;
+        if (im.kind < ZPX_GRAY || im.kind > ZPX_PALETTED || !outs[i] || !im.pixels || !palette_ok(im))
+            return ZPX_E_INVALID_ARGUMENT;
         const uint64_t w = uint64_t(im.max_x), h = uint64_t(im.max_y);
         if (w > 65535u * 1024u || h > 65535) return ZPX_E_UNSUPPORTED;
         by_kind[im.kind].push_back(rgba_job(dev_image_of(&im, im.pixels, im.palette), outs[i]));
@@ -794,21 +876,24 @@ extern "C" int zpx_plan_launch(zpx_plan *plan, void *stream)
         if (rc) return hip_fail(ctx, hipGetLastError(), "jpeg kernel launch");
     }
     for (auto &g : plan->png) {
+        // the control kernels of this group's launches: re-base the epoch
+        // (clearing the boundary) first if they would wrap its cycle
+        if (int e = g->ctl.prepare(ctx, g->nsched2 ? 2 : 1, g->boundary.ptr, g->boundary.bytes, st)) return e;
         // stream-layout frames: their band slabs first
         if (g->nslab_jobs && launch_png_slab(png_slab_chunk_bytes(g->depth), g->slab_jobs.as<DevSlabBand>(),
                                              g->nslab_jobs, g->slab_max_groups, st))
             return hip_fail(ctx, hipGetLastError(), "png slab kernel launch");
         const int rc = g->pair ? launch_png_pair(g->depth, g->trns, g->stream, g->passes.as<DevPngPass>(),
-                                                 g->sched.as<DevPngBand>(), g->nsched, g->scratch.as<uint32_t>(),
+                                                 g->sched.as<DevPngBand>(), g->nsched, g->ctl.words(),
                                                  g->boundary.as<uint64_t>(), g->band_bytes, st)
                                : launch_png_unfilter(g->depth, g->passes.as<DevPngPass>(), g->sched.as<DevPngBand>(),
-                                                     g->nsched, g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(),
+                                                     g->nsched, g->ctl.words(), g->boundary.as<uint64_t>(),
                                                      g->band_bytes, st);
         if (rc) return hip_fail(ctx, hipGetLastError(), "png kernel launch");
         // Adam7: pass 6 merges the staged passes once the first launch is done
         if (g->nsched2 && launch_png_pair_merge(g->depth, g->trns, g->stream, g->passes.as<DevPngPass>(),
                                                 g->sched.as<DevPngBand>() + g->nsched, g->nsched2,
-                                                g->scratch.as<uint32_t>(), g->boundary.as<uint64_t>(), g->band_bytes,
+                                                g->ctl.words(), g->boundary.as<uint64_t>(), g->band_bytes,
                                                 st))
             return hip_fail(ctx, hipGetLastError(), "png adam7 merge pass launch");
     }
@@ -833,7 +918,7 @@ static int zpx_plan_status_impl(zpx_plan *plan, void *stream)
     if (plan->status_host.bytes < n * 8 && !plan->status_host.alloc(n * 8, true)) return ZPX_E_OUT_OF_MEMORY;
     uint32_t *h = static_cast<uint32_t *>(plan->status_host.ptr);
     for (size_t i = 0; i < n; i++) {
-        uint32_t *ctl = plan->png[i]->scratch.as<uint32_t>();
+        uint32_t *ctl = plan->png[i]->ctl.words();
         HIPCHK(ctx, hipMemcpyAsync(h + 2 * i, ctl + 2, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(ctx, hipMemsetAsync(ctl + 2, 0, 8, st));
     }
@@ -1451,7 +1536,7 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
         filt.swap(slab);
         f.layout = ZPX_PNG_LAYOUT_SLAB;
     }
-    DevBuf din, dout, ctl, bound, dpass, dsched;
+    DevBuf din, dout, bound, dpass, dsched;
     HIPCHK(ctx, din.alloc(filt.size()));
     HIPCHK(ctx, hipMemcpy(din.ptr, filt.data(), filt.size(), hipMemcpyHostToDevice));
     HIPCHK(ctx, dout.alloc(size_t(W) * H * 4));
@@ -1465,9 +1550,8 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
     passes[0].band_base = 0;
     const DevPngBand only{0, 1}; // band 1 alone: band 0 never runs, so never publishes
     const uint32_t granules = static_cast<uint32_t>(png_band_granules(ZPX_PNG_TC8, rb));
-    HIPCHK(ctx, ctl.alloc(16));
-    const uint32_t ctl0[4] = {png_epoch_base(), 0, 0, 0};
-    HIPCHK(ctx, hipMemcpy(ctl.ptr, ctl0, 16, hipMemcpyHostToDevice));
+    PngControl ctl;
+    if (int e = ctl.init(ctx)) return e;
     HIPCHK(ctx, bound.alloc(size_t(2) * granules * sizeof(uint64_t)));
     HIPCHK(ctx, hipMemset(bound.ptr, 0, size_t(2) * granules * sizeof(uint64_t)));
     HIPCHK(ctx, dpass.alloc(sizeof(DevPngPass)));
@@ -1477,16 +1561,16 @@ static int png_stall_once(zpx_ctx *ctx, bool pair, uint32_t spin_limit, double &
     HIPCHK(ctx, hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = pair ? launch_png_pair(ZPX_PNG_TC8, false, false, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
-                                          ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream, spin_limit)
+                                          ctl.words(), bound.as<uint64_t>(), granules, ctx->stream, spin_limit)
                         : launch_png_unfilter(ZPX_PNG_TC8, dpass.as<DevPngPass>(), dsched.as<DevPngBand>(), 1,
-                                              ctl.as<uint32_t>(), bound.as<uint64_t>(), granules, ctx->stream,
+                                              ctl.words(), bound.as<uint64_t>(), granules, ctx->stream,
                                               spin_limit);
     if (rc)
         return hip_fail(ctx, hipGetLastError(), "png stall kernel launch");
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     uint32_t st[2] = {0, 0};
-    HIPCHK(ctx, hipMemcpy(st, ctl.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(st, ctl.words() + 2, 8, hipMemcpyDeviceToHost));
     timed_out = (st[0] | st[1]) != 0;
     return ZPX_OK;
 }
@@ -1514,10 +1598,10 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
 
 namespace zpx {
 namespace {
-// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab
-std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}};
-const char *const kOptNames[static_cast<int>(Opt::Count)] = {"jpeg_strip", "jpeg_sparse", "png_pair", "qoi_segment",
-                                                             "png_device_slab"};
+// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}};
+const char *const kOptNames[static_cast<int>(Opt::Count)] = {"jpeg_strip",      "jpeg_sparse",    "png_pair",
+                                                             "qoi_segment",     "png_device_slab", "png_epoch_cycle"};
 } // namespace
 int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
 } // namespace zpx
