@@ -639,7 +639,12 @@ int zpx_debug_shard_fake_comm(int on);
  *   "png_epoch_cycle" epochs a PNG control block cycles through before its
  *                 boundary buffer is cleared and the epoch re-based (>= 4;
  *                 default 0 = 2^20, the whole window; blocks created after
- *                 the call take it): a short cycle runs the wrap path. */
+ *                 the call take it): a short cycle runs the wrap path;
+ *   "shard_rccl_self" 1: zpx_batch_decode_sharded moves the results of a
+ *                 shard on device 0's GPU by grouped ncclSend / ncclRecv to
+ *                 rank 0 itself (RCCL; a one-rank communicator when every
+ *                 context shares the GPU) instead of a device copy
+ *                 (default 0). */
 int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the
  * ZPX_COEFFS_PIECES form the batch pipeline uploads and

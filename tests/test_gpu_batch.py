@@ -214,6 +214,46 @@ def test_batch_decode_sharded_fake_comm_send_recv(ndev):
         _lib.lib().zpx_debug_shard_fake_comm(prev)
 
 
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_batch_decode_sharded_real_rccl_self_send(ndev):
+    """configs[3]'s gather through the real RCCL on the one-GPU box (test
+    switch shard_rccl_self): every context shares device 0, so the
+    communicator set is one rank (ncclCommInitAll over device 0, from the
+    dlopen'd librccl.so.1) and each remote shard's results travel as grouped
+    ncclSend / ncclRecv to rank 0 itself on the gather stream.  Bit-exact
+    against the oracle on two calls, the second reusing the cached
+    communicator; closing the contexts destroys it (zpx_ctx_destroy ->
+    shard_release_comms), and a later call builds a new one."""
+    from zpix_amd import shard
+
+    bufs = mixed_buffers()[-9:]
+    dims = [batch._probe_dims(b) or (1, 1) for b in bufs]
+    prev = _lib.lib().zpx_debug_option(b"shard_rccl_self", 1)
+    try:
+        for life in range(2):
+            ctxs = [zpix_amd.Context(0) for _ in range(ndev)]
+            for call in range(2):
+                dst = [torch.full((h, w, 4), 0x5a, dtype=torch.uint8, device="cuda:0") for w, h in dims]
+                torch.cuda.synchronize()
+                statuses, st, gs = shard.decode_sharded(bufs, ctxs, dst, host_threads=2)
+                assert gs.ndev == ndev and gs.comm_ranks == 1
+                if call == 1:
+                    assert gs.comm_setup_s < 1e-3  # the cached communicator
+                moved = 0
+                for i, data in enumerate(bufs):
+                    want, status = oracle_rgba(data)
+                    assert statuses[i] == status, (life, call, i, statuses[i], status)
+                    if status == "Ok":
+                        assert np.array_equal(dst[i].cpu().numpy(), want), (life, call, i)
+                        if i % ndev:
+                            moved += dims[i][0] * dims[i][1] * 4
+                assert gs.gather_bytes == moved and moved > 0
+            for c in ctxs:
+                c.close()
+    finally:
+        _lib.lib().zpx_debug_option(b"shard_rccl_self", prev)
+
+
 def test_batch_decode_sharded_concurrent_calls_share_comms():
     """Two threads run sharded decodes at once, each on its own contexts but
     on the same device set, so both use the one cached communicator set: a

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -140,7 +141,12 @@ class Pipeline {
     std::vector<int> oom_items_; // items a worker could not even allocate for
     int tokens_ = 0;
     bool stop_ = false;
-    std::atomic<int> next_{0};
+    // dispatch order of the host stage (take_item): the most expensive
+    // untaken item of the look-ahead window [front_, front_ + 2 threads_)
+    std::vector<double> cost_;
+    std::vector<char> taken_;
+    int front_ = 0, ntaken_ = 0;
+    int take_item(int &remaining);
     double host_s_ = 0, host_jpeg_s_ = 0, host_png_s_ = 0;
     int jpeg_items_ = 0, png_items_ = 0;
     double h2d_bytes_ = 0, d2h_bytes_ = 0, pixels_ = 0;
@@ -168,11 +174,57 @@ Pipeline::~Pipeline()
     if (d2h_) (void)hipStreamDestroy(d2h_);
 }
 
+// Host cost estimate of an item (ns on the GPU boxes' Zen 5 cores, order
+// of magnitude only: it orders the dispatch, nothing else).  PNG: inflate,
+// ~2 ns per inflated byte (H x (1 + row bytes), from IHDR) + the CRC and
+// copy of the compressed bytes; JPEG: Huffman decoding, ~14 ns per
+// entropy-coded byte (the bench's 4K q75 frames: 2.8 MB in 39 ms, tc8 PNGs:
+// 50 MB inflated in 106 ms).  Anything else costs nothing on the host.
+static double host_cost_estimate(const uint8_t *buf, size_t len)
+{
+    if (zpx_png_probe_buffer(buf, len)) {
+        if (len < 29) return 0;
+        auto be32 = [&](size_t o) { return uint32_t(buf[o]) << 24 | uint32_t(buf[o + 1]) << 16 | uint32_t(buf[o + 2]) << 8 | buf[o + 3]; };
+        const double w = be32(16), h = be32(20);
+        static const int kChannels[7] = {1, 0, 3, 1, 2, 0, 4}; // by colour type
+        const int depth = buf[24], ct = buf[25] <= 6 ? buf[25] : 0;
+        const double bits = double(depth) * std::max(1, kChannels[ct]);
+        return 2.0 * h * (1.0 + std::ceil(w * bits / 8.0)) + 0.5 * double(len);
+    }
+    if (zpx_jpeg_probe_buffer(buf, len)) return 14.0 * double(len);
+    return 0;
+}
+
+// Next item for a worker: of the untaken items in the window [front_,
+// front_ + 2 threads_), the one of the largest host cost (the first of
+// equals), so the batch's long items -- a tc8 PNG's inflate is ~3x a JPEG's
+// Huffman decode -- do not start last and set the end of the host stage.
+// (Simulated over the bench's 64 alternating 4K JPEG / PNG items on 16
+// workers: 357 ms in item order, 290 with this window, the even split.)  An
+// item waits at most one window behind its turn, so prefix completion
+// (zpx_batch_wait_prefix) still follows item order.  -1 when none remain;
+// `remaining` = the untaken items before this one was taken.
+int Pipeline::take_item(int &remaining)
+{
+    std::lock_guard<std::mutex> lk(mu_);
+    while (front_ < n_ && taken_[front_]) front_++;
+    if (front_ >= n_) return -1;
+    const int end = std::min(n_, front_ + 2 * std::max(1, threads_));
+    int best = -1;
+    for (int i = front_; i < end; i++)
+        if (!taken_[i] && (best < 0 || cost_[i] > cost_[best])) best = i;
+    remaining = n_ - ntaken_;
+    taken_[best] = 1;
+    ntaken_++;
+    return best;
+}
+
 void Pipeline::worker()
 {
     for (;;) {
-        const int i = next_.fetch_add(1);
-        if (i >= n_) return;
+        int remaining = 0;
+        const int i = take_item(remaining);
+        if (i < 0) return;
         {
             std::unique_lock<std::mutex> lk(mu_);
             cv_token_.wait(lk, [&] { return tokens_ > 0 || stop_; });
@@ -192,7 +244,7 @@ void Pipeline::worker()
         // threads this item may use: one while enough items remain to keep
         // every worker busy; the batch's last items split the workers that
         // are about to go idle (parallel inflate, restart-interval Huffman)
-        const int sub = std::max(1, threads_ / std::max(1, n_ - i));
+        const int sub = std::max(1, threads_ / std::max(1, remaining));
         if (zpx_png_probe_buffer(it.buf, it.len)) {
             d->fmt = 2;
             d->status = png_parse(it.buf, it.len, d->ps, sub);
@@ -661,6 +713,9 @@ int Pipeline::run(zpx_batch_stats *stats)
         items_[i].format = zpx_png_probe_buffer(items_[i].buf, items_[i].len) ? 2
                            : zpx_jpeg_probe_buffer(items_[i].buf, items_[i].len) ? 1 : 0;
     }
+    cost_.resize(size_t(n_));
+    taken_.assign(size_t(n_), 0);
+    for (int i = 0; i < n_; i++) cost_[i] = host_cost_estimate(items_[i].buf, items_[i].len);
     if (int e = setup()) return e;
     try {
         for (int t = 0; t < std::min(threads_, std::max(n_, 1)); t++) workers_.emplace_back([this] { worker(); });

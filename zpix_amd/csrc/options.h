@@ -6,7 +6,7 @@
 
 namespace zpx {
 
-enum class Opt { JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, Count };
+enum class Opt { JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, Count };
 int opt(Opt o);
 
 } // namespace zpx

@@ -335,10 +335,18 @@ int sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n, const 
         if (k == static_cast<int>(devs.size())) devs.push_back(ctxs[r]->device);
         rank_of[r] = k;
     }
+    // test switch "shard_rccl_self": a shard on device 0's GPU sends its
+    // results over RCCL too -- grouped ncclSend / ncclRecv to itself on rank
+    // 0's communicator (a one-rank communicator when every shard shares the
+    // GPU) -- instead of a device copy, so the real library's loading, group
+    // semantics and stream ordering run on a one-GPU box
+    bool self_send = false;
+    if (!T.per_context && opt(Opt::ShardRcclSelf) != 0)
+        for (int r = 1; r < ndev; r++) self_send |= rank_of[r] == 0;
     const double tc = now_s();
     std::shared_ptr<CommSet> cset;
     std::unique_lock<std::mutex> in_use; // this call's turn on the communicator set
-    if (devs.size() > 1 && n > 1) { // (some item lives on a rank other than 0)
+    if ((devs.size() > 1 || self_send) && n > 1) { // (some item lives on a rank other than 0, or sends to itself)
         if (!T.ok) {
             root->last_error = "RCCL (librccl.so.1) could not be loaded for the gather";
             return ZPX_E_UNSUPPORTED;
@@ -437,7 +445,7 @@ int sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n, const 
             zpx_batch_item &it = items[s.ids[k]];
             const size_t b = result_bytes(li);
             if (t_first == 0) t_first = now_s();
-            if (rank_of[r] == 0) { // device 0's own GPU: a device copy
+            if (rank_of[r] == 0 && !self_send) { // device 0's own GPU: a device copy
                 CtxScope scope(root);
                 const hipError_t e = hipMemcpyAsync(it.dst, li.dst, b, hipMemcpyDeviceToDevice, gs[0].s);
                 if (e != hipSuccess) {
@@ -446,8 +454,11 @@ int sharded(zpx_ctx *const *ctxs, int ndev, zpx_batch_item *items, int n, const 
                     continue;
                 }
             } else {
+                // (a self send/recv pair: both on rank 0's communicator and
+                // gather stream, which RCCL turns into a local copy kernel)
+                const hipStream_t ss = rank_of[r] == 0 ? gs[0].s : gs[r].s;
                 NcclResult e = T.group_start();
-                if (!e) e = T.send(li.dst, b, kNcclUint8, 0, comms[rank_of[r]], gs[r].s);
+                if (!e) e = T.send(li.dst, b, kNcclUint8, 0, comms[rank_of[r]], ss);
                 if (!e) e = T.recv(it.dst, b, kNcclUint8, rank_of[r], comms[0], gs[0].s);
                 const NcclResult e2 = T.group_end();
                 if (!e) e = e2;
