@@ -39,7 +39,8 @@ def main():
         t0 = time.perf_counter()
         d = S.png_generic(7, size, size, depth, ct, interlace=il, filters=(1, 2, 3, 4))
         st = png.Stream(d)
-        pb = device.PngBatch([st], slots=[0] * 64)
+        # ZPX_PROBE_LAYOUT: "auto" (host-built slab where the pair kernel takes it) or "stream"
+        pb = device.PngBatch([st], slots=[0] * 64, layout=os.environ.get("ZPX_PROBE_LAYOUT", "auto"))
         ms = timed(pb)
         print(f"{name:14s} {ms:8.3f} ms/launch  {pb.bytes / ms / 1e6:8.1f} GB/s algorithmic  "
               f"(prep {time.perf_counter() - t0:.1f}s)", flush=True)
