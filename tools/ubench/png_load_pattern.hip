@@ -12,7 +12,7 @@
 // reads each band cooperatively: 8 lanes per row, 128 contiguous bytes, 8
 // rows per instruction, rows walked in 128-byte steps (the shape a
 // line-staged input would have).
-// Usage: png_load_pattern <mode 0|1> [waves per CU, mode 0; default 8]
+// Usage: png_load_pattern <mode 0|1|2|3|5> [waves per CU, modes 0/2/3/5; default 8]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -75,6 +75,42 @@ __global__ __launch_bounds__(64) void coop_loads(const unsigned char *__restrict
     if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) & mask) sink[blockIdx.x * 64 + lane] = acc[0];
 }
 
+// mode 3: the STREAM instance's loads (png_pair_kernels.hip, load_units):
+// per group of 8 12-byte chunks and per row half h (rows 2j + h), six
+// instructions whose lane-piece n = 64 i + lane is piece n % 6 of row
+// 2 (n / 6) + h's 96-byte window -- unaligned 16-byte loads, a row's window
+// on 6 consecutive lanes -- one group after the other.  mode 5: the same
+// instruction shape, but only group `first` of every row (each row's window
+// read once): the fetch granularity of this shape, by comparing FETCH_SIZE
+// with the 64-byte sectors and 128-byte lines the windows cover (printed).
+__global__ __launch_bounds__(64) void stream_units(const unsigned char *__restrict__ in, unsigned *__restrict__ sink,
+                                                   unsigned mask, int once)
+{
+    const int lane = threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+    for (int b = blockIdx.x; b < kImages * kBands; b += gridDim.x) {
+        const int img = b / kBands, band = b % kBands;
+        const unsigned char *band0 = in + size_t(img) * kImg + size_t(band) * 128 * kRow;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char *>(band0), 0, 0x7ffffff0, 0x00020000);
+        unsigned voff[2][6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const int n = 64 * i + lane;
+            voff[0][i] = unsigned(2 * (n / 6)) * unsigned(kRow) + 1u + 16u * unsigned(n % 6);
+            voff[1][i] = voff[0][i] + unsigned(kRow);
+        }
+        const int ng = once ? 1 : kW * 3 / 96;
+        for (int g = 0; g < ng; g++) {
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int i = 0; i < 6; i++)
+                    acc ^= __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff[h][i] + 96u * unsigned(g), 0, 0);
+        }
+    }
+    if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) & mask) sink[blockIdx.x * 64 + lane] = acc[0];
+}
+
 __global__ __launch_bounds__(256) void linear_loads(const u32x4 *__restrict__ in, size_t n, unsigned *__restrict__ sink,
                                                     unsigned mask)
 {
@@ -100,6 +136,8 @@ int main(int argc, char **argv)
         (void)hipEventRecord(e0);
         if (mode == 0) hipLaunchKernelGGL(band_loads, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
         else if (mode == 2) hipLaunchKernelGGL(coop_loads, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
+        else if (mode == 3 || mode == 5)
+            hipLaunchKernelGGL(stream_units, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u, mode == 5 ? 1 : 0);
         else hipLaunchKernelGGL(linear_loads, dim3(8192), dim3(256), 0, 0, reinterpret_cast<const u32x4 *>(in),
                                  kImg * kImages / 16, sink, 0u);
         (void)hipEventRecord(e1);
@@ -107,6 +145,19 @@ int main(int argc, char **argv)
         float ms = 0;
         (void)hipEventElapsedTime(&ms, e0, e1);
         if (ms < best) best = ms;
+    }
+    if (mode == 5) { // the sectors / lines the windows cover (the buffer's base is 256-byte aligned)
+        size_t sectors = 0, lines = 0, bytes = 0;
+        for (int b = 0; b < kImages * kBands; b++)
+            for (int r = 0; r < 128; r++) {
+                const size_t a = size_t(b / kBands) * kImg + size_t(b % kBands) * 128 * kRow + size_t(r) * kRow + 1;
+                sectors += (a + 95) / 64 - a / 64 + 1;
+                lines += (a + 95) / 128 - a / 128 + 1;
+                bytes += 96;
+            }
+        printf("mode 5: %.3f ms; windows %zu B, 64-B sectors %zu (%zu B), 128-B lines %zu (%zu B)\n", best, bytes,
+               sectors, sectors * 64, lines, lines * 128);
+        return 0;
     }
     printf("mode %d, %d waves/CU: %.3f ms, %zu true bytes, %.1f GB/s\n", mode, wpc, best, kImg * kImages,
            kImg * kImages / (best * 1e-3) / 1e9);
