@@ -12,7 +12,7 @@
 // reads each band cooperatively: 8 lanes per row, 128 contiguous bytes, 8
 // rows per instruction, rows walked in 128-byte steps (the shape a
 // line-staged input would have).
-// Usage: png_load_pattern <mode 0|1|2|3|5> [waves per CU, modes 0/2/3/5; default 8]
+// Usage: png_load_pattern <mode 0|1|2|3|5|6|7> [waves per CU, modes 0/2/3/5/6/7; default 8]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -83,8 +83,10 @@ __global__ __launch_bounds__(64) void coop_loads(const unsigned char *__restrict
 // instruction shape, but only group `first` of every row (each row's window
 // read once): the fetch granularity of this shape, by comparing FETCH_SIZE
 // with the 64-byte sectors and 128-byte lines the windows cover (printed).
+// mode 6 / 7: mode 3 with every offset rounded down to 16 / 4 bytes (the
+// same rows and lines per instruction, aligned lane accesses).
 __global__ __launch_bounds__(64) void stream_units(const unsigned char *__restrict__ in, unsigned *__restrict__ sink,
-                                                   unsigned mask, int once)
+                                                   unsigned mask, int once, unsigned align_mask)
 {
     const int lane = threadIdx.x;
     u32x4 acc = {0, 0, 0, 0};
@@ -96,8 +98,8 @@ __global__ __launch_bounds__(64) void stream_units(const unsigned char *__restri
 #pragma unroll
         for (int i = 0; i < 6; i++) {
             const int n = 64 * i + lane;
-            voff[0][i] = unsigned(2 * (n / 6)) * unsigned(kRow) + 1u + 16u * unsigned(n % 6);
-            voff[1][i] = voff[0][i] + unsigned(kRow);
+            voff[0][i] = (unsigned(2 * (n / 6)) * unsigned(kRow) + 1u + 16u * unsigned(n % 6)) & align_mask;
+            voff[1][i] = (voff[0][i] + unsigned(kRow)) & align_mask;
         }
         const int ng = once ? 1 : kW * 3 / 96;
         for (int g = 0; g < ng; g++) {
@@ -136,8 +138,9 @@ int main(int argc, char **argv)
         (void)hipEventRecord(e0);
         if (mode == 0) hipLaunchKernelGGL(band_loads, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
         else if (mode == 2) hipLaunchKernelGGL(coop_loads, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
-        else if (mode == 3 || mode == 5)
-            hipLaunchKernelGGL(stream_units, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u, mode == 5 ? 1 : 0);
+        else if (mode == 3 || mode == 5 || mode == 6 || mode == 7)
+            hipLaunchKernelGGL(stream_units, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u, mode == 5 ? 1 : 0,
+                               mode == 6 ? ~15u : mode == 7 ? ~3u : ~0u);
         else hipLaunchKernelGGL(linear_loads, dim3(8192), dim3(256), 0, 0, reinterpret_cast<const u32x4 *>(in),
                                  kImg * kImages / 16, sink, 0u);
         (void)hipEventRecord(e1);

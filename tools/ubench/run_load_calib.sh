@@ -10,11 +10,14 @@ OUT=$ROOTDIR/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B=$ROOTDIR/tools/ubench/png_load_pattern
-for m in 1 3 5 0; do timeout -k 5 60 "$B" $m 8 | tee -a "$OUT/calib.log"; done
+for m in 1 3 6 7 5 0; do timeout -k 5 60 "$B" $m 8 | tee -a "$OUT/calib.log"; done
 cd /tmp
-for m in 1 3 5; do
-  timeout -s KILL 60 rocprofv3 --kernel-trace --pmc FETCH_SIZE TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
-      -d "$OUT/m$m" -o run -- "$B" $m 8 > "$OUT/m$m.out" 2> "$OUT/m$m.err" || { echo "pmc mode $m failed"; tail -5 "$OUT/m$m.err"; exit 1; }
-  find "$OUT/m$m" -name '*counter_collection.csv' -exec cp {} "$OUT/m$m.csv" \;
+for m in 1 3 6 5; do
+  for p in "FETCH_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+    q=$(echo $p | cut -c1-5)
+    timeout -s KILL 60 rocprofv3 --kernel-trace --pmc $p --output-format csv \
+        -d "$OUT/m$m$q" -o run -- "$B" $m 8 > "$OUT/m$m$q.out" 2> "$OUT/m$m$q.err" || { echo "pmc mode $m $q failed"; tail -5 "$OUT/m$m$q.err"; exit 1; }
+    find "$OUT/m$m$q" -name '*counter_collection.csv' -exec cp {} "$OUT/m$m.$q.csv" \;
+  done
 done
 echo calib done
