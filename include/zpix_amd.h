@@ -644,7 +644,10 @@ int zpx_debug_shard_fake_comm(int on);
  *                 shard on device 0's GPU by grouped ncclSend / ncclRecv to
  *                 rank 0 itself (RCCL; a one-rank communicator when every
  *                 context shares the GPU) instead of a device copy
- *                 (default 0). */
+ *                 (default 0);
+ *   "batch_lookahead" 1: the batch pipeline's host workers take items in
+ *                 item order (default 0: the costliest of the next
+ *                 2 x host_threads items first). */
 int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the
  * ZPX_COEFFS_PIECES form the batch pipeline uploads and

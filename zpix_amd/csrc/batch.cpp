@@ -209,7 +209,9 @@ int Pipeline::take_item(int &remaining)
     std::lock_guard<std::mutex> lk(mu_);
     while (front_ < n_ && taken_[front_]) front_++;
     if (front_ >= n_) return -1;
-    const int end = std::min(n_, front_ + 2 * std::max(1, threads_));
+    // (test switch "batch_lookahead" = 1: item order)
+    const int win = opt(Opt::BatchLookahead) == 1 ? 1 : 2 * std::max(1, threads_);
+    const int end = std::min(n_, front_ + win);
     int best = -1;
     for (int i = front_; i < end; i++)
         if (!taken_[i] && (best < 0 || cost_[i] > cost_[best])) best = i;

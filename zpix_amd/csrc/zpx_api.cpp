@@ -1598,10 +1598,11 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
 
 namespace zpx {
 namespace {
-// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf
-std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}};
+// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}};
 const char *const kOptNames[static_cast<int>(Opt::Count)] = {
-    "jpeg_strip", "jpeg_sparse", "png_pair", "qoi_segment", "png_device_slab", "png_epoch_cycle", "shard_rccl_self"};
+    "jpeg_strip",      "jpeg_sparse",     "png_pair",       "qoi_segment",
+    "png_device_slab", "png_epoch_cycle", "shard_rccl_self", "batch_lookahead"};
 } // namespace
 int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
 } // namespace zpx
