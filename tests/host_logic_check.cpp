@@ -7,7 +7,7 @@
 //     staging areas Q2 / S4 / S5 (every even-row, even-column pixel written
 //     exactly once, where pass 6's merge looks it up), passes 6-7 writing
 //     the image, pass 6 pointing at its merge job, and
-//     png_plan_bands putting passes 6-7 (and only those) in the second
+//     png_plan_bands putting pass 6 (and only that) in the second
 //     launch's schedule;
 //   - dev_jpeg_frame: the quant-pair tables of the block kernel's row pass;
 //   - the PNG epoch windows and cycle (check_epoch_windows).
@@ -146,16 +146,17 @@ int main()
         std::vector<DevPngPass> p = passes;
         const PngBandPlan bp = png_plan_bands(ZPX_PNG_TCA16, true, p, rowbytes);
         CHECK(bp.sched.size() + bp.sched2.size() == bp.nbands);
-        // passes 6 and 7: 2048 rows each of the 4K image, 23 and 22 of the 77x45 one
-        CHECK(bp.sched2.size() == 2 * 16 + 2);
+        // pass 6: 2048 rows of the 4K image, 23 of the 77x45 one
+        CHECK(bp.sched2.size() == 16 + 1);
         for (const DevPngBand &b : bp.sched) CHECK(p[b.pass].merge == nullptr && !p[b.pass].launch2);
         std::map<uint32_t, uint32_t> next_band;
         for (size_t t = 0; t < bp.sched2.size(); t++) {
             const DevPngPass &d = p[bp.sched2[t].pass];
-            CHECK(d.launch2 && d.yf == 2 && ((d.xf == 2 && d.merge != nullptr) || (d.xf == 1 && d.merge == nullptr)));
+            CHECK(d.launch2 && d.yf == 2 && d.xf == 2 && d.merge != nullptr);
             CHECK(bp.sched2[t].band == next_band[bp.sched2[t].pass]++); // band order within a pass
-            if (t > 0) CHECK(p[bp.sched2[t - 1].pass].row_bytes >= d.row_bytes); // pass 7 (longest) first
         }
+        // pass 7 (the longest rows) leads the first launch's tickets
+        CHECK(!bp.sched.empty() && p[bp.sched[0].pass].xf == 1 && p[bp.sched[0].pass].yf == 2);
     }
 
     CHECK(st.jobs.size() == 2 && st.merge_pass.size() == 2);
@@ -212,7 +213,7 @@ int main()
         CHECK(p7.xo == 0 && p7.yo == 1 && p7.xf == 1 && p7.yf == 2 && p7.out == fake_out.data() && !p7.merge);
         const DevPngPass &p6 = passes[first_of[k] + 5];
         CHECK(p6.xo == 1 && p6.yo == 0 && p6.xf == 2 && p6.yf == 2 && p6.out == fake_out.data());
-        CHECK(p6.merge == jobs_dev.data() + k && p6.launch2 && p7.launch2);
+        CHECK(p6.merge == jobs_dev.data() + k && p6.launch2 && !p7.launch2);
     }
 
     // ---- quant-pair tables of dev_jpeg_frame

@@ -1,3 +1,6 @@
 set -eu -o pipefail
 mkdir -p gpurun_out/r05_e2e
-timeout -k 10 300 python -u tools/e2e_ab.py 3 16 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r05_e2e/ab.log
+for t in 16 15 14 12; do
+  echo "== threads $t" | tee -a gpurun_out/r05_e2e/ab3.log
+  timeout -k 10 300 python -u tools/e2e_ab.py 2 $t 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/r05_e2e/ab3.log
+done

@@ -64,7 +64,7 @@ struct DevPngPass {
     uint32_t band_base;      // index of this pass's first band in the progress table
     uint8_t trns[6];         // tRNS colour key (raw bytes)
     uint8_t use_trns;
-    uint8_t launch2; // paired-row kernel: the band runs in the group's second launch (Adam7 passes 6-7)
+    uint8_t launch2; // paired-row kernel: the band runs in the group's second launch (Adam7 pass 6)
     uint8_t slab;    // paired-row kernel: `filtered` is the frame's band slab (png_slab.cpp), not the stream
     uint32_t slab_band0; // slab: this pass's first band in the slab's band offset table
 };

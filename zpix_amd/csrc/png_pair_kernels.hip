@@ -420,7 +420,7 @@ void png_pair_kernel(const DevPngPass *__restrict__ passes, const DevPngBand *__
         const uint32_t rb = ps.row_bytes;
         // Adam7 pass 6 (the only strided pass this kernel takes), in the
         // instance of the group's second launch (MERGE): its registers stay
-        // out of the other instances; pass 7 shares that launch
+        // out of the other instances (pass 7 runs in the first launch)
         const bool merge = MERGE && ps.merge != nullptr;
         A7Src a7{};
         if (merge) {
