@@ -334,15 +334,17 @@ template <typename T> inline void copy_match(T *dst, size_t d, size_t n)
 
 // Output of one decode run: a fixed buffer (capacity = the bytes wanted) or
 // a growable one (the parallel path's speculative chunks).
+// `o` is the committed end (a block's start while its symbols decode).
 template <typename T> struct Out {
     T *p = nullptr;
     size_t o = 0, cap = 0;
     std::vector<T> *grow = nullptr;
-    bool room(size_t n)
+    // room for n elements from element `at` (a growable buffer grows; p may move)
+    bool room(size_t at, size_t n)
     {
-        if (o + n <= cap) return true;
+        if (at + n <= cap) return true;
         if (!grow) return false;
-        const size_t nc = std::max(2 * cap, o + n + (size_t(1) << 20));
+        const size_t nc = std::max(2 * cap, at + n + (size_t(1) << 20));
         grow->resize(nc);
         p = grow->data();
         cap = nc;
@@ -411,7 +413,10 @@ enum class Run { Want, Final, AtStop, Error };
 template <typename T>
 Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &overshot, size_t floor)
 {
-    static thread_local uint32_t lit[kLitEntries], dist[kDistEntries];
+    // the tables on the stack (48 KiB): a thread_local's address in this
+    // -fPIC library is a __tls_get_addr call, which gcc re-issued before
+    // every lookup of the symbol loop instead of keeping it in a register
+    uint32_t lit[kLitEntries], dist[kDistEntries];
     for (;;) {
         if (out.o >= want) return Run::Want;
         const uint64_t at = b.bitpos();
@@ -438,7 +443,7 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
             p += 4;
             if (p + len > b.len) return Run::Error;
             size_t n = len;
-            if (!out.room(n)) n = std::min<size_t>(n, out.cap - out.o);
+            if (!out.room(out.o, n)) n = std::min<size_t>(n, out.cap - out.o);
             n = std::min(n, want - out.o);
             for (size_t k = 0; k < n; k++) out.p[out.o + k] = b.in[p + k];
             out.o += n;
@@ -466,23 +471,30 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
         }
         pair_literals(lit, kLitBits, l, nl);
         if (b.overrun()) return Run::Error;
-        // ---- the block's symbols
-        T *o = out.p + out.o;
+        // ---- the block's symbols.  The loop keeps the bit reader, the
+        // tables and the output pointers in locals: `o`'s stores (bytes) may
+        // alias any memory, so members of b / out would be re-read around
+        // every symbol.
+        Bits bl = b;
+        const uint32_t *const lt = lit, *const dt = dist;
+        T *base = out.p, *o = base + out.o;
+        // the fast zone: real input bytes behind every bit and room for a
+        // whole match + a pair's second slot (258 + 8) -- no end checks
+        // per symbol; it holds while o <= fend
+        size_t lim = std::min(want, out.cap);
+        T *fend = base + (lim >= 266 ? lim - 266 : 0);
+        bool fast_ok = lim >= 266;
         for (;;) {
             uint32_t e;
-            size_t done = static_cast<size_t>(o - out.p);
-            if (b.pos + 32 <= b.len && done + 258 + 8 <= want && (done + 258 + 8 <= out.cap || out.room(1 << 16))) {
-                o = out.p + done; // the buffer may have moved
-                // fast zone: real input bytes behind every bit and room for a
-                // whole match -- no end checks per symbol
-                b.refill_fast();
-                e = decode(b, lit, kLitBits);
+            if (fast_ok && o <= fend && bl.pos + 32 <= bl.len) {
+                bl.refill_fast();
+                e = decode(bl, lt, kLitBits);
                 if (e & kLiteral) {
                     o = put_literals(o, e);
-                    e = decode(b, lit, kLitBits);
+                    e = decode(bl, lt, kLitBits);
                     if (e & kLiteral) {
                         o = put_literals(o, e);
-                        e = decode(b, lit, kLitBits);
+                        e = decode(bl, lt, kLitBits);
                         if (e & kLiteral) {
                             o = put_literals(o, e);
                             continue;
@@ -490,51 +502,88 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
                     }
                 }
                 if (e & (kEob | kInvalid)) {
-                    if (e & kInvalid) return Run::Error;
+                    if (e & kInvalid) {
+                        b = bl;
+                        return Run::Error;
+                    }
                     break;
                 }
                 // a length: its extra bits, then the distance (one refill covers
                 // extra <= 5 + distance code <= 15 + extra <= 13 bits)
-                b.refill_fast();
-                const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
-                const uint32_t de = decode(b, dist, kDistBits);
-                if (de & kInvalid) return Run::Error;
-                const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
-                if (d > size_t(o - out.p) + floor) return Run::Error; // before the start of the output
+                bl.refill_fast();
+                const uint32_t len = payload(e) + bl.take(static_cast<int>(extra_of(e)));
+                const uint32_t de = decode(bl, dt, kDistBits);
+                if (de & kInvalid) {
+                    b = bl;
+                    return Run::Error;
+                }
+                const uint32_t d = payload(de) + bl.take(static_cast<int>(extra_of(de)));
+                if (d > size_t(o - base) + floor) { // before the start of the output
+                    b = bl;
+                    return Run::Error;
+                }
                 copy_match(o, d, len);
                 o += len;
                 continue;
             }
+            const size_t done = static_cast<size_t>(o - base);
+            if (out.grow && bl.pos + 32 <= bl.len && done + 266 <= want && done + 266 > out.cap) {
+                // a growable buffer out of fast-zone room: grow it and go on fast
+                out.room(done, size_t(1) << 16);
+                base = out.p;
+                o = base + done;
+                lim = std::min(want, out.cap);
+                fend = base + (lim >= 266 ? lim - 266 : 0);
+                fast_ok = lim >= 266;
+                continue;
+            }
             // careful path near the end of the input or the output
-            o = out.p + done;
-            b.refill();
-            e = decode(b, lit, kLitBits);
-            if (b.overrun() || (e & kInvalid)) return Run::Error;
+            bl.refill();
+            e = decode(bl, lt, kLitBits);
+            if (bl.overrun() || (e & kInvalid)) {
+                b = bl;
+                return Run::Error;
+            }
             if (e & kLiteral) {
                 if (done >= want) break;
                 const size_t n = std::min<size_t>((e & kLiteral2) ? 2 : 1, want - done);
-                if (!out.room(n)) return Run::Error;
-                out.p[done] = static_cast<T>(payload(e) & 0xff);
-                if (n == 2) out.p[done + 1] = static_cast<T>(payload(e) >> 8);
-                o = out.p + done + n;
+                if (!out.room(done, n)) {
+                    b = bl;
+                    return Run::Error;
+                }
+                base = out.p;
+                base[done] = static_cast<T>(payload(e) & 0xff);
+                if (n == 2) base[done + 1] = static_cast<T>(payload(e) >> 8);
+                o = base + done + n;
                 continue;
             }
             if (e & kEob) break;
-            b.refill();
-            const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
-            b.refill();
-            const uint32_t de = decode(b, dist, kDistBits);
-            if (de & kInvalid) return Run::Error;
-            const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
-            if (b.overrun()) return Run::Error;
-            if (d > done + floor) return Run::Error;
+            bl.refill();
+            const uint32_t len = payload(e) + bl.take(static_cast<int>(extra_of(e)));
+            bl.refill();
+            const uint32_t de = decode(bl, dt, kDistBits);
+            if (de & kInvalid) {
+                b = bl;
+                return Run::Error;
+            }
+            const uint32_t d = payload(de) + bl.take(static_cast<int>(extra_of(de)));
+            if (bl.overrun() || d > done + floor) {
+                b = bl;
+                return Run::Error;
+            }
             size_t n = len < want - done ? len : want - done;
-            if (!out.room(n)) return Run::Error;
-            copy_match(out.p + done, d, n);
-            o = out.p + done + n;
+            if (!out.room(done, n)) {
+                b = bl;
+                return Run::Error;
+            }
+            base = out.p;
+            copy_match(base + done, d, n);
+            o = base + done + n;
             if (done + n >= want) break;
         }
-        out.o = static_cast<size_t>(o - out.p);
+        b = bl;
+        // (base == out.p: every growth above re-read it)
+        out.o = static_cast<size_t>(o - base);
         if (out.o >= want) return Run::Want;
         if (last) return Run::Final;
     }
