@@ -647,7 +647,10 @@ int zpx_debug_shard_fake_comm(int on);
  *                 (default 0);
  *   "batch_lookahead" 1: the batch pipeline's host workers take items in
  *                 item order (default 0: the costliest of the next
- *                 2 x host_threads items first). */
+ *                 2 x host_threads items first);
+ *   "inflate_pair" 0: a batch worker inflates one PNG at a time (default 1:
+ *                 two PNGs' inflates in one loop while the batch has more
+ *                 than 2 x host_threads items left to take). */
 int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the
  * ZPX_COEFFS_PIECES form the batch pipeline uploads and
@@ -660,6 +663,12 @@ int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, int32_t *gri
  * the first `want` bytes into out on `threads` threads, 0 when it declined;
  * threads = 1 runs the serial fast decoder instead. */
 int zpx_debug_inflate_parallel(const uint8_t *z, size_t len, uint8_t *out, size_t want, int threads);
+/* Test hook: the host stages of two PNGs as a batch worker runs them
+ * together (their inflates in one loop): status[k] is what zpx_png_inflate
+ * returns for buffer k, and *out_k its stream when that is ZPX_OK (free with
+ * zpx_png_stream_free), else NULL.  Returns ZPX_OK or an argument error. */
+int zpx_debug_png_inflate_pair(const uint8_t *buf0, size_t len0, const uint8_t *buf1, size_t len1,
+                               zpx_png_stream **out0, zpx_png_stream **out1, int *status);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,25 @@ int main(int argc, char **argv)
             }
         }
     }
+    // two streams in one loop (inflate_fast_pair): the stream with itself,
+    // whole and a third (their fast zones end at different points)
+    std::vector<uint8_t> out2(raw.size() + 64);
+    const size_t wants[3][2] = {{raw.size(), raw.size()}, {raw.size(), raw.size() / 3}, {raw.size() / 3, raw.size()}};
+    for (const auto &w : wants) {
+        memset(out.data(), 0, out.size());
+        memset(out2.data(), 0, out2.size());
+        const uint8_t *in[2] = {z.data(), z.data()};
+        const size_t in_len[2] = {z.size(), z.size()};
+        uint8_t *dst[2] = {out.data(), out2.data()};
+        size_t produced[2] = {0, 0};
+        bool ok[2] = {false, false};
+        zpx::inflate_fast_pair(in, in_len, dst, w, produced, ok);
+        if (!ok[0] || !ok[1] || produced[0] != w[0] || produced[1] != w[1] || memcmp(out.data(), raw.data(), w[0]) ||
+            memcmp(out2.data(), raw.data(), w[1])) {
+            fprintf(stderr, "pair decode differs (want %zu / %zu)\n", w[0], w[1]);
+            return 1;
+        }
+    }
     printf("ok\n");
     return 0;
 }

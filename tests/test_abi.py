@@ -338,6 +338,95 @@ def test_host_png_errors_match_oracle():
         assert got == want, (got, want)
 
 
+def _png_single(data):
+    """(status, frame fields, filtered bytes) of zpx_png_inflate."""
+    import ctypes as C
+
+    L = _lib.lib()
+    h = C.c_void_p()
+    rc = L.zpx_png_inflate(data, len(data), C.byref(h))
+    if rc:
+        return rc, None, None
+    try:
+        return 0, *_png_stream_view(h)
+    finally:
+        L.zpx_png_stream_free(h)
+
+
+def _png_stream_view(h):
+    import ctypes as C
+
+    L = _lib.lib()
+    f, n = _lib.zpx_png_frame(), C.c_size_t(0)
+    _lib.check(L.zpx_png_stream_frame(h, C.byref(f), C.byref(n)))
+    fields = (f.width, f.height, f.depth, f.interlace, f.use_transparent, bytes(f.transparent), f.out_stride, n.value)
+    ptr = L.zpx_png_stream_data(h)
+    return fields, bytes(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(n.value,)))
+
+
+def _png_pair_cases():
+    cases = [open(p, "rb").read() for p in PNGS]
+    base = S.png_generic(3, 37, 21, 8, 2)
+    raw = np.frombuffer(_idat_stream(base), np.uint8).copy().reshape(21, -1)
+    bad_filter = raw.copy()
+    bad_filter[3, 0] = 7
+    cases += [base[:20], base[:-5], S.encode_png(37, 21, 8, 2, bad_filter.tobytes()),
+              S.encode_png(37, 21, 8, 2, raw.tobytes()[: raw.size // 2])]
+    # an IDAT run, another chunk, a second IDAT run (the second one is the image)
+    z1, z2 = zlib.compress(raw.tobytes()[:100]), zlib.compress(raw.tobytes())
+    ch = lambda t, d: struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)  # noqa: E731
+    head = base[:33]
+    cases += [head + ch(b"IDAT", z1) + ch(b"tEXt", b"k\x00v") + ch(b"IDAT", z2) + ch(b"IEND", b""),
+              head + ch(b"IDAT", z2) + ch(b"tEXt", b"k\x00v") + ch(b"IDAT", z1) + ch(b"IEND", b"")]
+    # a bad CRC after the image data (the image's own error ranks first when it has one)
+    good = S.png_generic(5, 300, 200, 8, 2, interlace=1)
+    cases += [good[:-4] + b"\x00\x00\x00\x00", S.encode_png(37, 21, 8, 2, bad_filter.tobytes())[:-4] + b"\x00" * 4]
+    # larger streams: the fast zones of both run side by side
+    cases += [S.png_tc8_mixed(7, 700, 300), S.png_generic(8, 513, 257, 16, 6, interlace=1),
+              S.png_generic(9, 640, 480, 8, 0)]
+    rng = np.random.default_rng(11)
+    for _ in range(6):
+        d = bytearray(cases[-3])
+        d[rng.integers(40, len(d))] ^= 1 << int(rng.integers(0, 8))
+        cases.append(bytes(d))
+    # corrupted zlib data behind valid CRCs (the inflate's own errors)
+    _, f = S.png_filtered_tc8(4, 400, 160)
+    z = zlib.compress(f.tobytes())
+    head = S.encode_png(400, 160, 8, 2, b"")[:33]
+    for i in range(16):  # (half of them in the first block's header: code sets, invalid codes)
+        zz = bytearray(z)
+        zz[rng.integers(2, 40 if i % 2 else len(zz))] ^= 1 << int(rng.integers(0, 8))
+        cases.append(head + ch(b"IDAT", bytes(zz)) + ch(b"IEND", b""))
+    return cases
+
+
+def test_png_inflate_pair_matches_single():
+    """A batch worker's two-PNG host stage (png_parse_pair: the chunk walks
+    deferred past IDAT, both inflates in one loop) gives each image
+    zpx_png_inflate's status, frame and bytes: every fixture, truncated and
+    corrupted streams, a second IDAT run, a chunk error after the image."""
+    import ctypes as C
+
+    L = _lib.lib()
+    cases = _png_pair_cases()
+    single = [_png_single(d) for d in cases]
+    pairs = [(i, (i + 1) % len(cases)) for i in range(len(cases))] + [(i, i) for i in range(0, len(cases), 7)]
+    pairs += [(i, len(cases) - 1 - i) for i in range(len(cases) // 2)]
+    for a, b in pairs:
+        h0, h1, st = C.c_void_p(), C.c_void_p(), (C.c_int * 2)()
+        _lib.check(L.zpx_debug_png_inflate_pair(cases[a], len(cases[a]), cases[b], len(cases[b]), C.byref(h0),
+                                                C.byref(h1), st))
+        for k, (idx, h) in enumerate(((a, h0), (b, h1))):
+            want = single[idx]
+            assert st[k] == want[0], (a, b, k, _lib.error_name(st[k]), _lib.error_name(want[0]))
+            if want[0] == 0:
+                assert h.value
+                assert _png_stream_view(h) == want[1:], (a, b, k)
+                L.zpx_png_stream_free(h)
+            else:
+                assert not h.value
+
+
 # ---------------------------------------------------------------- decodeConfig
 def test_jpeg_decode_config_matches_decode():
     """jpeg.decodeConfig (decoder.zig:178-218): dims of every fixture equal the

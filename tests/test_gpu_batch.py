@@ -68,6 +68,22 @@ def test_batch_device_dst(threads, depth):
     check_results(bufs, res)
 
 
+@pytest.mark.parametrize("pair", [0, 1])
+def test_batch_inflate_pair_switch(pair):
+    """Workers inflating two PNGs in one loop ("inflate_pair", the default)
+    or one at a time give the oracle's results, with a token budget of two
+    (a pair takes both) and malformed PNGs among the pairs."""
+    L = _lib.lib()
+    prev = L.zpx_debug_option(b"inflate_pair", pair)
+    try:
+        bufs = mixed_buffers() + [S.png_tc8_mixed(20 + i, 257 + i, 129) for i in range(12)]
+        bufs += [S.png_tc8_mixed(40, 64, 64)[:-30], S.png_generic(41, 99, 77, 16, 2)]
+        res = batch.decode_rgba(bufs, host_threads=2, depth=2)
+        check_results(bufs, res)
+    finally:
+        L.zpx_debug_option(b"inflate_pair", prev)
+
+
 def test_batch_host_dst():
     bufs = mixed_buffers()
     res, st = batch.decode_rgba(bufs, on_host=True, host_threads=3, with_stats=True)

@@ -1,6 +1,6 @@
 """The fast host inflate (zpix_amd/csrc/inflate_fast.cpp) under the host
-sanitizers (g++ -fsanitize=address,undefined; host code only): serial and
-speculative parallel decodes of streams whose single DEFLATE blocks expand to
+sanitizers (g++ -fsanitize=address,undefined; host code only): serial,
+two-stream (inflate_fast_pair) and speculative parallel decodes of streams whose single DEFLATE blocks expand to
 more than a speculative chunk's first output buffer (4 MiB of symbols: long
 zero runs, 258-byte matches), so the chunk buffers must grow mid-block."""
 import os
@@ -10,6 +10,8 @@ import zlib
 
 import numpy as np
 import pytest
+
+from tools import synthetic as S
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GXX = shutil.which("g++")
@@ -21,7 +23,9 @@ def _streams():
     zeros = bytes(12 << 20)
     runs = noise(300_000) + zeros + noise(300_000) + zeros + noise(300_000)
     ramp = b"".join(bytes([i % 251]) * 70_000 + noise(2_000) for i in range(200))
-    return [("runs", runs, 6), ("runs9", runs, 9), ("ramp", ramp, 6)]
+    _, tc8 = S.png_filtered_tc8(3, 640, 400)
+    return [("runs", runs, 6), ("runs9", runs, 9), ("ramp", ramp, 6), ("tc8", tc8.tobytes(), 6),
+            ("stored", noise(200_000), 0)]
 
 
 @pytest.mark.skipif(GXX is None, reason="g++ not available")

@@ -164,7 +164,7 @@ EXPORTS = [
     "zpx_debug_jpeg_parallel_progressive",
     "zpx_bmp_decode", "zpx_bmp_load", "zpx_bmp_probe_buffer", "zpx_qoi_decode", "zpx_qoi_load",
     "zpx_qoi_probe_buffer", "zpx_qoi_encode", "zpx_qoi_encode_bound", "zpx_qoi_encode_device",
-    "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel", "zpx_batch_wait_prefix",
+    "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel", "zpx_debug_png_inflate_pair", "zpx_batch_wait_prefix",
     "zpx_debug_shard_fake_comm", "zpx_debug_option",
 ]
 
@@ -248,6 +248,8 @@ def lib():
         "zpx_qoi_encode_device": (i32, [vp, vp, C.POINTER(zpx_qoi_desc), vp, sz, vp, vp]),
         "zpx_debug_jpeg_sparse_grids": (C.c_int64, [C.c_char_p, sz, vp, sz]),
         "zpx_debug_inflate_parallel": (i32, [C.c_char_p, sz, vp, sz, i32]),
+        "zpx_debug_png_inflate_pair": (i32, [C.c_char_p, sz, C.c_char_p, sz, C.POINTER(vp), C.POINTER(vp),
+                                             C.POINTER(i32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -146,7 +146,10 @@ class Pipeline {
     std::vector<double> cost_;
     std::vector<char> taken_;
     int front_ = 0, ntaken_ = 0;
+    std::vector<char> png_; // the item is a PNG (zpx_png_probe_buffer)
     int take_item(int &remaining);
+    int take_png_partner();
+    void push_decoded(std::unique_ptr<Decoded> d, double dt);
     double host_s_ = 0, host_jpeg_s_ = 0, host_png_s_ = 0;
     int jpeg_items_ = 0, png_items_ = 0;
     double h2d_bytes_ = 0, d2h_bytes_ = 0, pixels_ = 0;
@@ -221,17 +224,89 @@ int Pipeline::take_item(int &remaining)
     return best;
 }
 
+// A second PNG for a worker that took a PNG while every worker has items
+// to spare (inflate_pair): of the untaken PNGs in take_item's window, the
+// one of the largest host cost; -1 when none.
+int Pipeline::take_png_partner()
+{
+    std::lock_guard<std::mutex> lk(mu_);
+    const int win = opt(Opt::BatchLookahead) == 1 ? 1 : 2 * std::max(1, threads_);
+    const int end = std::min(n_, front_ + win);
+    int best = -1;
+    for (int i = front_; i < end; i++)
+        if (!taken_[i] && png_[i] && (best < 0 || cost_[i] > cost_[best])) best = i;
+    if (best >= 0) {
+        taken_[best] = 1;
+        ntaken_++;
+    }
+    return best;
+}
+
+void Pipeline::push_decoded(std::unique_ptr<Decoded> d, double dt)
+{
+    ZPX_TRACE("worker: item %d fmt %d status %d decoded in %.3fs", d->item, d->fmt, d->status, dt);
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        host_s_ += dt;
+        if (d->fmt == 1) {
+            host_jpeg_s_ += dt;
+            jpeg_items_++;
+        } else if (d->fmt == 2) {
+            host_png_s_ += dt;
+            png_items_++;
+        }
+        ready_.push_back(std::move(d));
+    }
+    cv_ready_.notify_one();
+}
+
 void Pipeline::worker()
 {
     for (;;) {
         int remaining = 0;
         const int i = take_item(remaining);
         if (i < 0) return;
+        // threads this item may use: one while enough items remain to keep
+        // every worker busy; the batch's last items split the workers that
+        // are about to go idle (parallel inflate, restart-interval Huffman)
+        const int sub = std::max(1, threads_ / std::max(1, remaining));
+        // two PNGs at once while the batch keeps every worker busy: their
+        // inflates share one loop (png_parse_pair), 1.3x the work per CPU
+        // second of one stream's decode chain.  (Test switch "inflate_pair".)
+        const int j = png_[i] && sub == 1 && remaining > 2 * threads_ && depth_ >= 2 && opt(Opt::InflatePair)
+                          ? take_png_partner()
+                          : -1;
+        const int need = j >= 0 ? 2 : 1;
         {
             std::unique_lock<std::mutex> lk(mu_);
-            cv_token_.wait(lk, [&] { return tokens_ > 0 || stop_; });
+            cv_token_.wait(lk, [&] { return tokens_ >= need || stop_; });
             if (stop_) return;
-            tokens_--;
+            tokens_ -= need;
+        }
+        if (j >= 0) {
+            std::unique_ptr<Decoded> d0(new (std::nothrow) Decoded), d1(new (std::nothrow) Decoded);
+            if (!d0 || !d1) { // out of memory: report on the items, keep the pipeline going
+                std::lock_guard<std::mutex> lk(mu_);
+                oom_items_.push_back(i);
+                oom_items_.push_back(j);
+                cv_ready_.notify_one();
+                continue;
+            }
+            d0->item = i;
+            d1->item = j;
+            d0->fmt = d1->fmt = 2;
+            const double t0 = now_s();
+            const uint8_t *buf[2] = {items_[i].buf, items_[j].buf};
+            const size_t len[2] = {items_[i].len, items_[j].len};
+            PngStream *out[2] = {&d0->ps, &d1->ps};
+            int st[2];
+            png_parse_pair(buf, len, out, st);
+            d0->status = st[0];
+            d1->status = st[1];
+            const double dt = now_s() - t0;
+            push_decoded(std::move(d0), dt / 2);
+            push_decoded(std::move(d1), dt / 2);
+            continue;
         }
         std::unique_ptr<Decoded> d(new (std::nothrow) Decoded);
         if (!d) { // out of memory: report on the item, keep the pipeline going
@@ -243,11 +318,7 @@ void Pipeline::worker()
         d->item = i;
         const zpx_batch_item &it = items_[i];
         const double t0 = now_s();
-        // threads this item may use: one while enough items remain to keep
-        // every worker busy; the batch's last items split the workers that
-        // are about to go idle (parallel inflate, restart-interval Huffman)
-        const int sub = std::max(1, threads_ / std::max(1, remaining));
-        if (zpx_png_probe_buffer(it.buf, it.len)) {
+        if (png_[i]) {
             d->fmt = 2;
             d->status = png_parse(it.buf, it.len, d->ps, sub);
             // (the paired-row kernel's band slab is built on the device from
@@ -260,21 +331,7 @@ void Pipeline::worker()
         } else {
             d->status = ZPX_E_UNKNOWN_IMAGE_FORMAT;
         }
-        const double dt = now_s() - t0;
-        ZPX_TRACE("worker: item %d fmt %d status %d decoded in %.3fs", i, d->fmt, d->status, dt);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            host_s_ += dt;
-            if (d->fmt == 1) {
-                host_jpeg_s_ += dt;
-                jpeg_items_++;
-            } else if (d->fmt == 2) {
-                host_png_s_ += dt;
-                png_items_++;
-            }
-            ready_.push_back(std::move(d));
-        }
-        cv_ready_.notify_one();
+        push_decoded(std::move(d), now_s() - t0);
     }
 }
 
@@ -717,6 +774,8 @@ int Pipeline::run(zpx_batch_stats *stats)
     }
     cost_.resize(size_t(n_));
     taken_.assign(size_t(n_), 0);
+    png_.assign(size_t(n_), 0);
+    for (int i = 0; i < n_; i++) png_[i] = items_[i].format == 2;
     for (int i = 0; i < n_; i++) cost_[i] = host_cost_estimate(items_[i].buf, items_[i].len);
     if (int e = setup()) return e;
     try {

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -403,6 +404,117 @@ bool read_dynamic(Bits &b, uint32_t *lit, uint32_t *dist, uint8_t *lit_lens = nu
     return !b.overrun();
 }
 
+// A stored block (its 3 header bits consumed): the byte offset `at` of its
+// `len` data bytes in b.in; b moves past them.  False when it is irregular.
+bool stored_block(Bits &b, size_t &at, uint32_t &len)
+{
+    if (b.overrun()) return false;
+    b.drop((b.cnt - b.pad) & 7);
+    // re-sync the byte position to the bit buffer (whole real bytes still
+    // buffered go back to the input)
+    const size_t bytes_in_buf = static_cast<size_t>((b.cnt - b.pad) >> 3);
+    size_t p = b.pos - bytes_in_buf;
+    b.buf = 0;
+    b.cnt = 0;
+    b.pad = 0;
+    b.pos = p;
+    if (p + 4 > b.len) return false;
+    len = b.in[p] | uint32_t(b.in[p + 1]) << 8;
+    const uint32_t nlen = b.in[p + 2] | uint32_t(b.in[p + 3]) << 8;
+    if ((len ^ 0xffffu) != nlen) return false;
+    p += 4;
+    if (p + len > b.len) return false;
+    at = p;
+    b.pos = p + len;
+    return true;
+}
+
+// The decode tables of a fixed (type 1) or dynamic (type 2) block whose 3
+// header bits are consumed, literal pairs included.  False when irregular.
+bool block_tables(Bits &b, uint32_t type, uint32_t *lit, uint32_t *dist)
+{
+    uint8_t l[320];
+    int nl = 0;
+    if (type == 1) { // fixed codes
+        for (int i = 0; i < 144; i++) l[i] = 8;
+        for (int i = 144; i < 256; i++) l[i] = 9;
+        for (int i = 256; i < 280; i++) l[i] = 7;
+        for (int i = 280; i < 288; i++) l[i] = 8;
+        // zlib's fixed table has 288 literal/length symbols (286, 287 invalid when used)
+        if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen)) return false;
+        nl = 288;
+        uint8_t d[32];
+        for (int i = 0; i < 32; i++) d[i] = 5;
+        if (!build(dist, kDistEntries, d, 32, kDistBits, Kind::Dist)) return false;
+    } else if (type == 2) { // dynamic
+        if (!read_dynamic(b, lit, dist, l, &nl)) return false;
+    } else {
+        return false;
+    }
+    pair_literals(lit, kLitBits, l, nl);
+    return !b.overrun();
+}
+
+// One step of a block's symbols in the fast zone (real input bytes behind
+// every bit, room for a whole match + a pair's second slot): up to three
+// literal lookups, or one match.  0: go on, 1: the block ended, 2: an invalid
+// symbol or a distance before the output's start (`floor` elements before
+// base are readable).
+// The rest of a fast-zone step from its (k+1)-th lookup, whose entry is e
+// (k < 3 lookups done since the step's refill).
+template <typename T>
+inline int fast_step_from(Bits &b, T *&o, uint32_t e, int k, const uint32_t *lt, const uint32_t *dt, const T *base,
+                          size_t floor)
+{
+    while (e & kLiteral) {
+        o = put_literals(o, e);
+        if (++k == 3) return 0;
+        e = decode(b, lt, kLitBits);
+    }
+    if (e & (kEob | kInvalid)) return (e & kInvalid) ? 2 : 1;
+    // a length: its extra bits, then the distance (one refill covers extra
+    // <= 5 + distance code <= 15 + extra <= 13 bits)
+    b.refill_fast();
+    const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
+    const uint32_t de = decode(b, dt, kDistBits);
+    if (de & kInvalid) return 2;
+    const uint32_t d = payload(de) + b.take(static_cast<int>(extra_of(de)));
+    if (d > size_t(o - base) + floor) return 2;
+    copy_match(o, d, len);
+    o += len;
+    return 0;
+}
+
+template <typename T>
+inline int fast_step(Bits &b, T *&o, const uint32_t *lt, const uint32_t *dt, const T *base, size_t floor)
+{
+    b.refill_fast();
+    return fast_step_from(b, o, decode(b, lt, kLitBits), 0, lt, dt, base, floor);
+}
+
+// Steps of two streams a and b with their lookups interleaved (a's and b's
+// chains side by side while both decode literals): ra / rb as fast_step's.
+inline void fast_step2(Bits &a, uint8_t *&oa, const uint32_t *la, const uint32_t *da, const uint8_t *ba, int &ra,
+                       Bits &b, uint8_t *&ob, const uint32_t *lb, const uint32_t *db, const uint8_t *bb, int &rb)
+{
+    a.refill_fast();
+    b.refill_fast();
+    uint32_t ea = decode(a, la, kLitBits), eb = decode(b, lb, kLitBits);
+    int k = 0;
+    while (ea & eb & kLiteral) {
+        oa = put_literals(oa, ea);
+        ob = put_literals(ob, eb);
+        if (++k == 3) {
+            ra = rb = 0;
+            return;
+        }
+        ea = decode(a, la, kLitBits);
+        eb = decode(b, lb, kLitBits);
+    }
+    ra = fast_step_from(a, oa, ea, k, la, da, ba, 0);
+    rb = fast_step_from(b, ob, eb, k, lb, db, bb, 0);
+}
+
 enum class Run { Want, Final, AtStop, Error };
 
 // Decodes blocks from b's position into out until out.o reaches `want`
@@ -426,51 +538,18 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
         const bool last = b.take(1) != 0;
         const uint32_t type = b.take(2);
         if (type == 0) { // stored
-            if (b.overrun()) return Run::Error;
-            b.drop((b.cnt - b.pad) & 7);
-            // re-sync the byte position to the bit buffer (whole real bytes
-            // still buffered go back to the input)
-            const size_t bytes_in_buf = static_cast<size_t>((b.cnt - b.pad) >> 3);
-            size_t p = b.pos - bytes_in_buf;
-            b.buf = 0;
-            b.cnt = 0;
-            b.pad = 0;
-            b.pos = p;
-            if (p + 4 > b.len) return Run::Error;
-            const uint32_t len = b.in[p] | uint32_t(b.in[p + 1]) << 8;
-            const uint32_t nlen = b.in[p + 2] | uint32_t(b.in[p + 3]) << 8;
-            if ((len ^ 0xffffu) != nlen) return Run::Error;
-            p += 4;
-            if (p + len > b.len) return Run::Error;
+            size_t at;
+            uint32_t len;
+            if (!stored_block(b, at, len)) return Run::Error;
             size_t n = len;
             if (!out.room(out.o, n)) n = std::min<size_t>(n, out.cap - out.o);
             n = std::min(n, want - out.o);
-            for (size_t k = 0; k < n; k++) out.p[out.o + k] = b.in[p + k];
+            for (size_t k = 0; k < n; k++) out.p[out.o + k] = b.in[at + k];
             out.o += n;
-            b.pos = p + len;
             if (last) return out.o >= want ? Run::Want : Run::Final;
             continue;
         }
-        uint8_t l[320];
-        int nl = 0;
-        if (type == 1) { // fixed codes
-            for (int i = 0; i < 144; i++) l[i] = 8;
-            for (int i = 144; i < 256; i++) l[i] = 9;
-            for (int i = 256; i < 280; i++) l[i] = 7;
-            for (int i = 280; i < 288; i++) l[i] = 8;
-            // zlib's fixed table has 288 literal/length symbols (286, 287 invalid when used)
-            if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen)) return Run::Error;
-            nl = 288;
-            uint8_t d[32];
-            for (int i = 0; i < 32; i++) d[i] = 5;
-            if (!build(dist, kDistEntries, d, 32, kDistBits, Kind::Dist)) return Run::Error;
-        } else if (type == 2) { // dynamic
-            if (!read_dynamic(b, lit, dist, l, &nl)) return Run::Error;
-        } else {
-            return Run::Error;
-        }
-        pair_literals(lit, kLitBits, l, nl);
-        if (b.overrun()) return Run::Error;
+        if (!block_tables(b, type, lit, dist)) return Run::Error;
         // ---- the block's symbols.  The loop keeps the bit reader, the
         // tables and the output pointers in locals: `o`'s stores (bytes) may
         // alias any memory, so members of b / out would be re-read around
@@ -487,44 +566,13 @@ Run decode_blocks(Bits &b, Out<T> &out, size_t want, uint64_t stop, bool &oversh
         for (;;) {
             uint32_t e;
             if (fast_ok && o <= fend && bl.pos + 32 <= bl.len) {
-                bl.refill_fast();
-                e = decode(bl, lt, kLitBits);
-                if (e & kLiteral) {
-                    o = put_literals(o, e);
-                    e = decode(bl, lt, kLitBits);
-                    if (e & kLiteral) {
-                        o = put_literals(o, e);
-                        e = decode(bl, lt, kLitBits);
-                        if (e & kLiteral) {
-                            o = put_literals(o, e);
-                            continue;
-                        }
-                    }
-                }
-                if (e & (kEob | kInvalid)) {
-                    if (e & kInvalid) {
-                        b = bl;
-                        return Run::Error;
-                    }
-                    break;
-                }
-                // a length: its extra bits, then the distance (one refill covers
-                // extra <= 5 + distance code <= 15 + extra <= 13 bits)
-                bl.refill_fast();
-                const uint32_t len = payload(e) + bl.take(static_cast<int>(extra_of(e)));
-                const uint32_t de = decode(bl, dt, kDistBits);
-                if (de & kInvalid) {
+                const int r = fast_step(bl, o, lt, dt, base, floor);
+                if (r == 0) continue;
+                if (r == 2) {
                     b = bl;
                     return Run::Error;
                 }
-                const uint32_t d = payload(de) + bl.take(static_cast<int>(extra_of(de)));
-                if (d > size_t(o - base) + floor) { // before the start of the output
-                    b = bl;
-                    return Run::Error;
-                }
-                copy_match(o, d, len);
-                o += len;
-                continue;
+                break; // the block's end
             }
             const size_t done = static_cast<size_t>(o - base);
             if (out.grow && bl.pos + 32 <= bl.len && done + 266 <= want && done + 266 > out.cap) {
@@ -621,6 +669,152 @@ bool plausible_block(const uint8_t *in, size_t len, uint64_t bit)
     return read_dynamic(b, lit, dist);
 }
 
+
+// ---- Two streams in one loop (inflate_fast_pair).  A noisy stream's symbol
+// loop is one dependency chain -- table lookup, shift, the next lookup --
+// that leaves most of a core's issue slots idle; two independent streams
+// stepped in turn in one loop overlap their chains.
+struct PairDec {
+    Bits b;
+    uint8_t *p = nullptr;
+    size_t o = 0, want = 0;
+    bool last = false;
+    enum State { Header, Symbols, Done, Fail } st = Header;
+    uint32_t lit[kLitEntries], dist[kDistEntries];
+    bool fast() const { return want >= 266 && o <= want - 266 && b.pos + 32 <= b.len; }
+};
+
+// st Header: the next block's header -- a stored block is copied whole, a
+// Huffman block's tables are built (st Symbols) -- Done once `want` bytes
+// are out, Fail on anything irregular or a stream that ends short
+// (decode_blocks' rules with a fixed output)
+void pair_header(PairDec &d)
+{
+    Bits &b = d.b;
+    while (d.st == PairDec::Header) {
+        if (d.o >= d.want) {
+            d.st = PairDec::Done;
+            return;
+        }
+        if (d.last) {
+            d.st = PairDec::Fail;
+            return;
+        }
+        b.refill();
+        d.last = b.take(1) != 0;
+        const uint32_t type = b.take(2);
+        if (type == 0) {
+            size_t at;
+            uint32_t len;
+            if (!stored_block(b, at, len)) {
+                d.st = PairDec::Fail;
+                return;
+            }
+            const size_t n = std::min<size_t>(len, d.want - d.o);
+            memcpy(d.p + d.o, b.in + at, n);
+            d.o += n;
+            continue;
+        }
+        d.st = block_tables(b, type, d.lit, d.dist) ? PairDec::Symbols : PairDec::Fail;
+    }
+}
+
+// st Symbols outside the fast zone: the block's rest symbol by symbol with
+// every end check (decode_blocks' careful path); st Header at its end or
+// when the output is full, Fail on anything irregular
+void pair_careful(PairDec &d)
+{
+    Bits &b = d.b;
+    for (;;) {
+        const size_t done = d.o;
+        b.refill();
+        const uint32_t e = decode(b, d.lit, kLitBits);
+        if (b.overrun() || (e & kInvalid)) break;
+        if (e & kLiteral) {
+            if (done >= d.want) {
+                d.st = PairDec::Header;
+                return;
+            }
+            const size_t n = std::min<size_t>((e & kLiteral2) ? 2 : 1, d.want - done);
+            d.p[done] = static_cast<uint8_t>(payload(e) & 0xff);
+            if (n == 2) d.p[done + 1] = static_cast<uint8_t>(payload(e) >> 8);
+            d.o = done + n;
+            continue;
+        }
+        if (e & kEob) {
+            d.st = PairDec::Header;
+            return;
+        }
+        b.refill();
+        const uint32_t len = payload(e) + b.take(static_cast<int>(extra_of(e)));
+        b.refill();
+        const uint32_t de = decode(b, d.dist, kDistBits);
+        if (de & kInvalid) break;
+        const uint32_t dd = payload(de) + b.take(static_cast<int>(extra_of(de)));
+        if (b.overrun() || dd > done) break;
+        const size_t n = std::min<size_t>(len, d.want - done);
+        copy_match(d.p + done, dd, n);
+        d.o = done + n;
+        if (d.o >= d.want) {
+            d.st = PairDec::Header;
+            return;
+        }
+    }
+    d.st = PairDec::Fail;
+}
+
+// Headers and careful stretches until the stream is in a block's fast zone
+// (st Symbols with fast()), Done or Fail.
+void pair_settle(PairDec &d)
+{
+    for (;;) {
+        if (d.st == PairDec::Header) pair_header(d);
+        else if (d.st == PairDec::Symbols && !d.fast()) pair_careful(d);
+        else return;
+    }
+}
+
+// The fast zones of N streams (st Symbols, fast()), stepped in turn until
+// one leaves its zone or its block ends; their state is written back.
+template <int N>
+void pair_fast(PairDec *const *d)
+{
+    Bits b[N];
+    uint8_t *base[N], *o[N], *end[N];
+    const uint32_t *lt[N], *dt[N];
+    int r[N];
+#pragma GCC unroll 2
+    for (int k = 0; k < N; k++) {
+        b[k] = d[k]->b;
+        base[k] = d[k]->p;
+        o[k] = base[k] + d[k]->o;
+        end[k] = base[k] + (d[k]->want - 266);
+        lt[k] = d[k]->lit;
+        dt[k] = d[k]->dist;
+        r[k] = 0;
+    }
+    for (;;) {
+        bool go = true;
+#pragma GCC unroll 2
+        for (int k = 0; k < N; k++) go = go && o[k] <= end[k] && b[k].pos + 32 <= b[k].len;
+        if (!go) break;
+        if constexpr (N == 2) {
+            fast_step2(b[0], o[0], lt[0], dt[0], base[0], r[0], b[1], o[1], lt[1], dt[1], base[1], r[1]);
+            if (r[0] | r[1]) break;
+        } else {
+            r[0] = fast_step(b[0], o[0], lt[0], dt[0], base[0], 0);
+            if (r[0]) break;
+        }
+    }
+#pragma GCC unroll 2
+    for (int k = 0; k < N; k++) {
+        d[k]->b = b[k];
+        d[k]->o = static_cast<size_t>(o[k] - base[k]);
+        if (r[k] == 1) d[k]->st = PairDec::Header;
+        else if (r[k] == 2) d[k]->st = PairDec::Fail;
+    }
+}
+
 } // namespace
 
 bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced)
@@ -633,6 +827,36 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
     const Run r = decode_blocks(b, o, want, ~uint64_t(0), overshot, 0);
     *produced = o.o;
     return r == Run::Want; // anything short of the requested bytes: let zlib decide
+}
+
+void inflate_fast_pair(const uint8_t *const in[2], const size_t in_len[2], uint8_t *const out[2], const size_t want[2],
+                       size_t produced[2], bool ok[2])
+{
+    std::unique_ptr<PairDec> d0(new PairDec), d1(new PairDec);
+    PairDec *d[2] = {d0.get(), d1.get()};
+    for (int k = 0; k < 2; k++) {
+        produced[k] = 0;
+        if (!zlib_header_ok(in[k], in_len[k])) {
+            d[k]->st = PairDec::Fail;
+            continue;
+        }
+        d[k]->b = bits_at(in[k], in_len[k], 16);
+        d[k]->p = out[k];
+        d[k]->want = want[k];
+    }
+    for (;;) {
+        pair_settle(*d[0]);
+        pair_settle(*d[1]);
+        const bool s0 = d[0]->st == PairDec::Symbols, s1 = d[1]->st == PairDec::Symbols;
+        if (s0 && s1) pair_fast<2>(d);
+        else if (s0) pair_fast<1>(d);
+        else if (s1) pair_fast<1>(d + 1);
+        else break;
+    }
+    for (int k = 0; k < 2; k++) {
+        produced[k] = d[k]->o;
+        ok[k] = d[k]->st == PairDec::Done;
+    }
 }
 
 // Parallel inflate of one stream (the reference's single call

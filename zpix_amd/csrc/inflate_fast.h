@@ -12,4 +12,8 @@ bool inflate_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, s
 // The same contract, decoded by `threads` threads (speculative chunks; false
 // on anything irregular, the caller then runs the serial decoder).
 bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t want, size_t *produced, int threads);
+// Two streams decoded together on this thread (their decode chains overlap):
+// ok[k] and produced[k] are inflate_fast's result for stream k.
+void inflate_fast_pair(const uint8_t *const in[2], const size_t in_len[2], uint8_t *const out[2], const size_t want[2],
+                       size_t produced[2], bool ok[2]);
 }

@@ -79,6 +79,18 @@ class Parser {
   public:
     Parser(const uint8_t *p, size_t n, PngStream &o, int threads) : src_(p), len_(n), o_(o), threads_(threads) {}
     int run(bool header_only = false);
+    // Deferred inflate (png_parse_pair): the IDAT stage only sets the job up
+    // and the chunk walk goes on; complete() takes the inflated bytes'
+    // checks after the caller inflated them (inflate_fast_pair).
+    void defer() { defer_ = true; }
+    bool pending() const { return pending_; }
+    const std::vector<uint8_t> &job_z() const { return z_; }
+    uint8_t *job_dst() const { return static_cast<uint8_t *>(o_.data.ptr); }
+    size_t job_want() const { return o_.data_len; }
+    // the job's inflate result (ok: inflate_fast's), else its zlib fallback,
+    // then the row checks; `run_status` is run()'s, whose chunk errors
+    // after the IDAT rank behind the image's own
+    int complete(int run_status, bool ok, size_t produced);
 
   private:
     int read(uint8_t *p, size_t n)
@@ -118,7 +130,8 @@ class Parser {
     int plte(uint32_t len);
     int trns(uint32_t len);
     int idat(uint32_t first_len);
-    int decode_image(const std::vector<uint8_t> &z);
+    int prepare_image();
+    int inflate_image(bool fast_done, bool fast_ok, size_t fast_produced);
 
     const uint8_t *src_;
     size_t len_, pos_ = 0;
@@ -127,6 +140,8 @@ class Parser {
     bool have_image_ = false;
     PngStream &o_;
     int threads_ = 1; // inflate threads (inflate_parallel)
+    std::vector<uint8_t> z_; // the concatenated IDAT data (the zlib stream)
+    bool defer_ = false, pending_ = false;
 };
 
 int Parser::ihdr(uint32_t len)
@@ -226,9 +241,10 @@ int Parser::trns(uint32_t len)
     return verify();
 }
 
-int Parser::decode_image(const std::vector<uint8_t> &z)
+// The passes' geometry and the inflated stream's buffer (readImagePass
+// :655-673, :782-785).
+int Parser::prepare_image()
 {
-    // pass geometry (readImagePass :655-673, :782-785)
     const uint32_t bits = static_cast<uint32_t>(bits_of(o_.depth));
     o_.npasses = 0;
     size_t total = 0;
@@ -260,23 +276,34 @@ int Parser::decode_image(const std::vector<uint8_t> &z)
     o_.data_len = total;
     if (!o_.data.alloc(total + ZPX_PNG_INPUT_PAD, false)) return ZPX_E_OUT_OF_MEMORY;
     memset(static_cast<uint8_t *>(o_.data.ptr) + total, 0, ZPX_PNG_INPUT_PAD);
+    return 0;
+}
 
-    // inflate exactly the bytes the passes read (std.compress.flate .zlib):
-    // the fast decoder when the stream decodes cleanly, else system zlib from
-    // the start (whose error behaviour the rest of this function maps)
+// Inflates exactly the bytes the passes read (std.compress.flate .zlib) --
+// the fast decoder when the stream decodes cleanly (or its result, when the
+// caller ran it: fast_done), else system zlib from the start, whose error
+// behaviour the rest maps -- then the rows' checks and the output type.
+int Parser::inflate_image(bool fast_done, bool fast_ok, size_t fast_produced)
+{
+    const size_t total = o_.data_len;
     uint8_t *dst = static_cast<uint8_t *>(o_.data.ptr);
     size_t produced = 0;
     bool data_error = false;
-    // several threads for a large stream (speculative chunks, identical
-    // bytes), else / on anything irregular the serial fast decoder
-    const bool par = threads_ > 1 && total >= (size_t(4) << 20) &&
-                     inflate_parallel(z.data(), z.size(), dst, total, &produced, threads_);
-    if (!par && !inflate_fast(z.data(), z.size(), dst, total, &produced)) {
-        produced = 0;
-        if (int e = inflate_zlib(z, dst, total, produced, data_error)) return e;
+    bool ok;
+    if (fast_done) {
+        ok = fast_ok;
+        produced = fast_produced;
+    } else {
+        // several threads for a large stream (speculative chunks, identical
+        // bytes), else / on anything irregular the serial fast decoder
+        ok = threads_ > 1 && total >= (size_t(4) << 20) &&
+             inflate_parallel(z_.data(), z_.size(), dst, total, &produced, threads_);
+        if (!ok) ok = inflate_fast(z_.data(), z_.size(), dst, total, &produced);
     }
-
-
+    if (!ok) {
+        produced = 0;
+        if (int e = inflate_zlib(z_, dst, total, produced, data_error)) return e;
+    }
     // rows in order: short data -> EndOfStream / ReadFailed, bad filter ->
     // InvalidFilterType (readImagePass :800, :839-841)
     for (int p = 0; p < o_.npasses; p++) {
@@ -311,7 +338,12 @@ int Parser::decode_image(const std::vector<uint8_t> &z)
 
 int Parser::idat(uint32_t first_len)
 { // parseIdat :404-545
-    std::vector<uint8_t> all;
+    if (pending_) { // a second IDAT run (deferred): the first one's image is checked first, as undeferred
+        pending_ = false;
+        if (int e = inflate_image(false, false, 0)) return e;
+    }
+    std::vector<uint8_t> &all = z_;
+    all.clear();
     { // reserve the whole stream once: sum the run of IDAT chunk lengths
       // ahead (a read-only scan; the loop below does the checks)
         size_t total = first_len, p = pos_ + size_t(first_len) + 4;
@@ -355,7 +387,20 @@ int Parser::idat(uint32_t first_len)
         if (int e = verify()) return e;
     }
     if (all.empty()) return ZPX_E_EMPTY_IDAT_DATA;
-    return decode_image(all);
+    if (int e = prepare_image()) return e;
+    if (defer_) {
+        pending_ = true;
+        return 0;
+    }
+    return inflate_image(false, false, 0);
+}
+
+int Parser::complete(int run_status, bool ok, size_t produced)
+{
+    if (!pending_) return run_status; // stopped before its image (or no job)
+    pending_ = false;
+    const int e = inflate_image(true, ok, produced);
+    return e ? e : run_status;
 }
 
 int Parser::chunk()
@@ -412,7 +457,7 @@ int Parser::run(bool header_only)
     }
     while (stage_ != 5)
         if (int e = chunk()) return e;
-    if (!have_image_) return ZPX_E_INVALID_IMAGE_DIMENSIONS;
+    if (!have_image_ && !pending_) return ZPX_E_INVALID_IMAGE_DIMENSIONS;
     return 0;
 }
 
@@ -433,6 +478,38 @@ int png_parse(const uint8_t *buf, size_t len, PngStream &out, int threads)
         Parser p(buf, len, out, threads);
         return p.run();
     } catch (...) {
+        return ZPX_E_OUT_OF_MEMORY;
+    }
+}
+
+int png_parse_pair(const uint8_t *const buf[2], const size_t len[2], PngStream *const out[2], int status[2])
+{
+    try {
+        Parser a(buf[0], len[0], *out[0], 1), b(buf[1], len[1], *out[1], 1);
+        Parser *p[2] = {&a, &b};
+        int run[2];
+        for (int k = 0; k < 2; k++) {
+            p[k]->defer();
+            run[k] = p[k]->run();
+        }
+        bool ok[2] = {false, false};
+        size_t produced[2] = {0, 0};
+        if (a.pending() && b.pending()) {
+            const uint8_t *in[2] = {a.job_z().data(), b.job_z().data()};
+            const size_t in_len[2] = {a.job_z().size(), b.job_z().size()};
+            uint8_t *dst[2] = {a.job_dst(), b.job_dst()};
+            const size_t want[2] = {a.job_want(), b.job_want()};
+            inflate_fast_pair(in, in_len, dst, want, produced, ok);
+        } else {
+            for (int k = 0; k < 2; k++)
+                if (p[k]->pending())
+                    ok[k] = inflate_fast(p[k]->job_z().data(), p[k]->job_z().size(), p[k]->job_dst(), p[k]->job_want(),
+                                         &produced[k]);
+        }
+        for (int k = 0; k < 2; k++) status[k] = p[k]->complete(run[k], ok[k], produced[k]);
+        return 0;
+    } catch (...) {
+        status[0] = status[1] = ZPX_E_OUT_OF_MEMORY;
         return ZPX_E_OUT_OF_MEMORY;
     }
 }

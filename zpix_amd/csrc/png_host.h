@@ -48,6 +48,10 @@ int png_stream_build_slab(PngStream &ps, int threads = 1);
 // chunk-level error.
 // threads > 1: a large stream inflates on that many threads (inflate_parallel)
 int png_parse(const uint8_t *buf, size_t len, PngStream &out, int threads = 1);
+// Two PNGs' host stages on this thread, their inflates in one loop
+// (inflate_fast_pair: two decode chains overlap on a core): status[k] is
+// png_parse(buf[k], len[k], *out[k]).
+int png_parse_pair(const uint8_t *const buf[2], const size_t len[2], PngStream *const out[2], int status[2]);
 // default inflate threads of the single-image entry points: ZPX_INFLATE_THREADS,
 // else min(8, hardware threads)
 int png_inflate_threads();

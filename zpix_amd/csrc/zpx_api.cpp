@@ -1066,6 +1066,23 @@ extern "C" int zpx_png_inflate(const uint8_t *buf, size_t len, zpx_png_stream **
     return guarded([&] { return zpx_png_inflate_impl(buf, len, out); });
 }
 
+extern "C" int zpx_debug_png_inflate_pair(const uint8_t *buf0, size_t len0, const uint8_t *buf1, size_t len1,
+                                          zpx_png_stream **out0, zpx_png_stream **out1, int *status)
+{
+    return guarded([&]() -> int {
+        if (!out0 || !out1 || !status || (!buf0 && len0) || (!buf1 && len1)) return ZPX_E_INVALID_ARGUMENT;
+        *out0 = *out1 = nullptr;
+        std::unique_ptr<zpx_png_stream> s0(new zpx_png_stream), s1(new zpx_png_stream);
+        const uint8_t *buf[2] = {buf0, buf1};
+        const size_t len[2] = {len0, len1};
+        PngStream *ps[2] = {&s0->s, &s1->s};
+        if (int e = png_parse_pair(buf, len, ps, status)) return e;
+        if (status[0] == ZPX_OK) *out0 = s0.release();
+        if (status[1] == ZPX_OK) *out1 = s1.release();
+        return ZPX_OK;
+    });
+}
+
 extern "C" int zpx_png_stream_frame(const zpx_png_stream *ss, zpx_png_frame *f, size_t *filtered_len)
 {
     if (!ss || !f) return ZPX_E_INVALID_ARGUMENT;
@@ -1599,10 +1616,10 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
 namespace zpx {
 namespace {
 // JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead
-std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}};
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}};
 const char *const kOptNames[static_cast<int>(Opt::Count)] = {
-    "jpeg_strip",      "jpeg_sparse",     "png_pair",       "qoi_segment",
-    "png_device_slab", "png_epoch_cycle", "shard_rccl_self", "batch_lookahead"};
+    "jpeg_strip",      "jpeg_sparse",     "png_pair",        "qoi_segment",     "png_device_slab",
+    "png_epoch_cycle", "shard_rccl_self", "batch_lookahead", "inflate_pair"};
 } // namespace
 int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
 } // namespace zpx
