@@ -113,6 +113,37 @@ __global__ __launch_bounds__(64) void stream_units(const unsigned char *__restri
     if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) & mask) sink[blockIdx.x * 64 + lane] = acc[0];
 }
 
+// mode 8: two groups' windows of a row in one unit -- 192 contiguous bytes
+// a row on 12 consecutive lanes, ~5.3 rows an instruction -- every second
+// group, for row quarters (the shape of a 2-group stream unit).
+__global__ __launch_bounds__(64) void stream_units2(const unsigned char *__restrict__ in, unsigned *__restrict__ sink,
+                                                    unsigned mask)
+{
+    const int lane = threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+    for (int b = blockIdx.x; b < kImages * kBands; b += gridDim.x) {
+        const int img = b / kBands, band = b % kBands;
+        const unsigned char *band0 = in + size_t(img) * kImg + size_t(band) * 128 * kRow;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char *>(band0), 0, 0x7ffffff0, 0x00020000);
+        unsigned voff[4][6];
+#pragma unroll
+        for (int q = 0; q < 4; q++) // row quarter q: rows 4 r + q, r < 32
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                const int n = 64 * i + lane; // 384 lane-pieces: row n / 12, piece n % 12
+                voff[q][i] = unsigned(4 * (n / 12) + q) * unsigned(kRow) + 1u + 16u * unsigned(n % 12);
+            }
+        for (int g = 0; g < kW * 3 / 96; g += 2) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int i = 0; i < 6; i++)
+                    acc ^= __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff[q][i] + 96u * unsigned(g), 0, 0);
+        }
+    }
+    if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) & mask) sink[blockIdx.x * 64 + lane] = acc[0];
+}
+
 __global__ __launch_bounds__(256) void linear_loads(const u32x4 *__restrict__ in, size_t n, unsigned *__restrict__ sink,
                                                     unsigned mask)
 {
@@ -138,6 +169,7 @@ int main(int argc, char **argv)
         (void)hipEventRecord(e0);
         if (mode == 0) hipLaunchKernelGGL(band_loads, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
         else if (mode == 2) hipLaunchKernelGGL(coop_loads, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
+        else if (mode == 8) hipLaunchKernelGGL(stream_units2, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u);
         else if (mode == 3 || mode == 5 || mode == 6 || mode == 7)
             hipLaunchKernelGGL(stream_units, dim3(256 * wpc), dim3(64), 0, 0, in, sink, 0u, mode == 5 ? 1 : 0,
                                mode == 6 ? ~15u : mode == 7 ? ~3u : ~0u);

@@ -10,9 +10,9 @@ OUT=$ROOTDIR/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B=$ROOTDIR/tools/ubench/png_load_pattern
-for m in 1 3 6 7 5 0; do timeout -k 5 60 "$B" $m 8 | tee -a "$OUT/calib.log"; done
+for m in 1 3 8 6 7 5 0; do timeout -k 5 60 "$B" $m 8 | tee -a "$OUT/calib.log"; done
 cd /tmp
-for m in 1 3 6 5; do
+for m in 3 8; do
   for p in "FETCH_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
     q=$(echo $p | cut -c1-5)
     timeout -s KILL 60 rocprofv3 --kernel-trace --pmc $p --output-format csv \
