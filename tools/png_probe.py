@@ -40,10 +40,12 @@ def main():
         d = S.png_generic(7, size, size, depth, ct, interlace=il, filters=(1, 2, 3, 4))
         st = png.Stream(d)
         # ZPX_PROBE_LAYOUT: "auto" (host-built slab where the pair kernel takes it) or "stream"
-        pb = device.PngBatch([st], slots=[0] * 64, layout=os.environ.get("ZPX_PROBE_LAYOUT", "auto"))
+        # ZPX_PROBE_N: images per plan (default 64)
+        n = int(os.environ.get("ZPX_PROBE_N", "64"))
+        pb = device.PngBatch([st], slots=[0] * n, layout=os.environ.get("ZPX_PROBE_LAYOUT", "auto"))
         ms = timed(pb)
-        print(f"{name:14s} {ms:8.3f} ms/launch  {pb.bytes / ms / 1e6:8.1f} GB/s algorithmic  "
-              f"(prep {time.perf_counter() - t0:.1f}s)", flush=True)
+        print(f"{name:14s} {ms:8.3f} ms/launch  {ms * 64 / n:8.3f} ms per 64 images  "
+              f"{pb.bytes / ms / 1e6:8.1f} GB/s algorithmic  (prep {time.perf_counter() - t0:.1f}s)", flush=True)
         del pb
         torch.cuda.empty_cache()
 

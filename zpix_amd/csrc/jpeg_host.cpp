@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <condition_variable>
 #include <memory>
+#include <type_traits>
 #include <cstring>
 #include <thread>
 #include <map>
@@ -644,7 +645,7 @@ class Decoder {
         size_t pos;
         int unread;
         explicit FastBits(Decoder &dd) : d(dd), src(dd.src_), ba(dd.ba_), bn(dd.bn_), pos(dd.pos_), unread(dd.unread_) {}
-        void sync()
+        __attribute__((always_inline)) void sync()
         {
             d.ba_ = ba;
             d.bn_ = bn;
@@ -652,7 +653,7 @@ class Decoder {
             d.pos_ = pos;
             d.unread_ = unread;
         }
-        void load()
+        __attribute__((always_inline)) void load()
         {
             ba = d.ba_;
             bn = d.bn_;
@@ -660,7 +661,7 @@ class Decoder {
             unread = d.unread_;
         }
         // stuffed() + one step of ensure(): false (nothing read) at a marker
-        inline bool fill()
+        __attribute__((always_inline)) bool fill()
         {
             const uint8_t x = src[pos];
             if (x != 0xff) {
@@ -675,7 +676,7 @@ class Decoder {
             bn += 8;
             return true;
         }
-        inline int huffman(const Huff &h, uint8_t &out)
+        __attribute__((always_inline)) int huffman(const Huff &h, uint8_t &out)
         {
             if (h.num_codes != 0 && (bn >= 8 || fill())) {
                 const uint16_t lv = h.lut[(ba >> (bn - 8)) & 0xff];
@@ -690,7 +691,7 @@ class Decoder {
             load();
             return e;
         }
-        inline int receive_extend(uint8_t t, int32_t &out)
+        __attribute__((always_inline)) int receive_extend(uint8_t t, int32_t &out)
         {
             while (bn < static_cast<int32_t>(t)) {
                 if (!fill()) {
@@ -703,11 +704,12 @@ class Decoder {
             bn -= t;
             const int32_t thr = int32_t(1) << t;
             int32_t v = static_cast<int32_t>((ba >> bn) & static_cast<uint32_t>(thr - 1));
-            if (v < (thr >> 1)) v += static_cast<int32_t>(0xffffffffu << t) + 1;
+            // (branch-free: the sign of a coefficient is a coin toss)
+            v += ((v - (thr >> 1)) >> 31) & (static_cast<int32_t>(0xffffffffu << t) + 1);
             out = v;
             return 0;
         }
-        inline int bit(bool &out)
+        __attribute__((always_inline)) int bit(bool &out)
         {
             if (bn == 0 && !fill()) {
                 sync();
@@ -719,7 +721,7 @@ class Decoder {
             bn--;
             return 0;
         }
-        inline int bits(int32_t n, uint32_t &out)
+        __attribute__((always_inline)) int bits(int32_t n, uint32_t &out)
         {
             while (bn < n) {
                 if (!fill()) {
@@ -736,9 +738,20 @@ class Decoder {
             return 0;
         }
     };
+    // (inlined into mcu(): the reader and nnz then live in registers; called
+    // out of line, FastBits' fields stayed in memory, written and re-read
+    // around the block's byte / int stores, and receive_extend was a call)
     template <class R>
-    int first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac, int32_t &dcv, int32_t *b, uint8_t *nzpos,
-                    int &nnz);
+    __attribute__((always_inline)) int first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
+                                                   int32_t &dcv, int32_t *b, uint8_t *nzpos, int &nnz);
+    // first_block + PieceSink::put in one pass (the batch path's baseline
+    // scans): the block decodes straight into zig-zag order -- the pieces'
+    // own -- in zz (zero on entry and on return), and its pieces are written
+    // from there, with no natural-order block or position list in between
+    template <class R>
+    __attribute__((always_inline)) int first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
+                                                          int32_t &dcv, JpegPieces &p, int ci, size_t blk,
+                                                          int32_t *zz);
     template <class Sink>
     int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
             Sink &sink);
@@ -1220,6 +1233,7 @@ template <class R>
 int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac, int32_t &dcv, int32_t *b,
                          uint8_t *nzpos, int &nnz)
 {
+    const int32_t ze = sc.ze, al = sc.al; // (locals: the byte stores below may alias sc)
     int32_t zig = sc.zs;
     if (zig == 0) {
         zig++;
@@ -1229,23 +1243,23 @@ int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
         int32_t delta;
         ZTRY(r.receive_extend(t, delta));
         dcv += delta;
-        b[0] = dcv << sc.al;
+        b[0] = dcv << al;
         nzpos[nnz++] = 0;
     }
-    if (zig <= sc.ze && eob_run_ > 0) {
+    if (zig <= ze && eob_run_ > 0) {
         eob_run_--;
         return 0;
     }
-    for (; zig <= sc.ze; zig++) {
+    for (; zig <= ze; zig++) {
         uint8_t value;
         ZTRY(r.huffman(hac, value));
         const uint8_t v0r = value >> 4, v1 = value & 0x0f;
         if (v1 != 0) {
             zig += v0r;
-            if (zig > sc.ze) break;
+            if (zig > ze) break;
             int32_t ac;
             ZTRY(r.receive_extend(v1, ac));
-            b[kUnzig[zig]] = ac << sc.al;
+            b[kUnzig[zig]] = ac << al;
             nzpos[nnz++] = kUnzig[zig];
         } else {
             if (v0r != 0x0f) {
@@ -1262,6 +1276,96 @@ int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
         }
     }
     return 0;
+}
+
+template <class R>
+int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huff &hac, int32_t &dcv, JpegPieces &p,
+                                int ci, size_t blk, int32_t *zz)
+{
+    const int32_t ze = sc.ze, al = sc.al;
+    int32_t zig = sc.zs;
+    int last = -1; // the last coefficient written, zig-zag order
+    uint32_t m = 0; // the largest magnitude (INT32_MIN's: 2^31)
+    auto mag = [](int32_t v) { return v < 0 ? 0u - static_cast<uint32_t>(v) : static_cast<uint32_t>(v); };
+    if (zig == 0) {
+        zig++;
+        uint8_t t;
+        ZTRY(r.huffman(hdc, t));
+        if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+        int32_t delta;
+        ZTRY(r.receive_extend(t, delta));
+        dcv += delta;
+        const int32_t v = dcv << al;
+        zz[0] = v;
+        last = 0;
+        m = mag(v);
+    }
+    if (zig <= ze && eob_run_ > 0) {
+        eob_run_--;
+    } else {
+        for (; zig <= ze; zig++) {
+            uint8_t value;
+            ZTRY(r.huffman(hac, value));
+            const uint8_t v0r = value >> 4, v1 = value & 0x0f;
+            if (v1 != 0) {
+                zig += v0r;
+                if (zig > ze) break;
+                int32_t ac;
+                ZTRY(r.receive_extend(v1, ac));
+                const int32_t v = ac << al;
+                zz[zig] = v;
+                last = zig;
+                m = std::max(m, mag(v));
+            } else {
+                if (v0r != 0x0f) {
+                    eob_run_ = static_cast<uint16_t>(1u << v0r);
+                    if (v0r != 0) {
+                        uint32_t x;
+                        ZTRY(r.bits(v0r, x));
+                        eob_run_ |= static_cast<uint16_t>(x);
+                    }
+                    eob_run_--;
+                    break;
+                }
+                zig += 0x0f;
+            }
+        }
+    }
+    // PieceSink::put's rules on the zig-zag block (every AC entry is nonzero)
+    int rc = 0;
+    const uint32_t mm = std::max(m, static_cast<uint32_t>(p.max_abs[ci]));
+    if (mm > 32767) {
+        rc = kSparseAbort;
+    } else {
+        p.max_abs[ci] = static_cast<int32_t>(mm);
+        if (p.bits == 8 && mm > 127 && !p.widen()) rc = kSparseAbort;
+    }
+    if (rc == 0) {
+        uint32_t &ix = p.index_of(ci)[blk];
+        if (last < 0 || (last == 0 && zz[0] == 0)) {
+            ix = 0;
+        } else {
+            const int eob = last + 1;
+            uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + p.npieces * 16;
+            size_t np;
+            if (p.bits == 8) {
+                np = static_cast<size_t>((eob + 15) >> 4);
+                for (size_t k = 0; k < np; k++)
+                    for (int j = 0; j < 16; j++) reinterpret_cast<int8_t *>(d)[16 * k + j] = static_cast<int8_t>(zz[16 * k + j]);
+            } else {
+                np = static_cast<size_t>((eob + 7) >> 3);
+                for (size_t k = 0; k < np; k++)
+                    for (int j = 0; j < 8; j++) {
+                        const int16_t v = static_cast<int16_t>(zz[8 * k + j]);
+                        memcpy(d + 16 * k + 2 * j, &v, 2);
+                    }
+            }
+            ix = static_cast<uint32_t>(p.npieces << 4 | np);
+            p.npieces += np;
+        }
+    }
+    for (int i = 0; i <= last; i++) zz[i] = 0;
+    return rc;
 }
 
 template <class Sink>
@@ -1293,6 +1397,21 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
                 // the reader in and out per block cost more than it saved)
                 ZTRY(prog_block_member(sc, ci, blk, hdc, hac, dc));
                 continue;
+            }
+            if constexpr (std::is_same<Sink, PieceSink>::value) {
+                if (sc.ah == 0) { // (b: the zig-zag block, zero between blocks)
+                    int e;
+                    if (len_ - pos_ >= kFastSlack) {
+                        FastBits fb(*this);
+                        e = first_block_pieces(fb, sc, hdc, hac, dc[ci], sink.p, ci, blk, b);
+                        fb.sync();
+                    } else {
+                        MemberBits mb{*this};
+                        e = first_block_pieces(mb, sc, hdc, hac, dc[ci], sink.p, ci, blk, b);
+                    }
+                    if (e) return e;
+                    continue;
+                }
             }
             int nnz = 0;
             if (sc.ah != 0) {
