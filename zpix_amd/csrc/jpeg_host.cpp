@@ -544,7 +544,7 @@ class Decoder {
         bm_ >>= t;
         int32_t thr = int32_t(1) << t;
         int32_t v = static_cast<int32_t>((ba_ >> bn_) & static_cast<uint32_t>(thr - 1));
-        if (v < (thr >> 1)) v += static_cast<int32_t>(0xffffffffu << t) + 1;
+        v += ((v - (thr >> 1)) >> 31) & (static_cast<int32_t>(0xffffffffu << t) + 1); // (branch-free)
         out = v;
         return 0;
     }
