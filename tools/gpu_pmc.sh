@@ -16,8 +16,11 @@ pass() {
   timeout -s KILL 150 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \
       python3 "$ROOTDIR/bench.py" $ARGS > "$OUT/$name.json" 2> "$OUT/$name.err" || { echo "pass $name failed rc=$?"; tail -5 "$OUT/$name.err"; exit 1; }
 }
+# ZPX_PMC_SQ=0: the traffic passes only (FETCH_SIZE, WRITE_SIZE)
+if [ "${ZPX_PMC_SQ:-1}" != 0 ]; then
 pass sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 pass sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE
+fi
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 for extra in "$@"; do pass "x_$(echo $extra | tr ',' '_')" $(echo $extra | tr ',' ' '); done
