@@ -646,8 +646,8 @@ int zpx_debug_shard_fake_comm(int on);
  *                 context shares the GPU) instead of a device copy
  *                 (default 0);
  *   "batch_lookahead" 1: the batch pipeline's host workers take items in
- *                 item order (default 0: the costliest of the next
- *                 2 x host_threads items first);
+ *                 item order; k >= 2: the costliest of the next k x host_threads
+ *                 items first (default 0: k = 4);
  *   "inflate_pair" 0: a batch worker inflates one PNG at a time (default 1:
  *                 two PNGs' inflates in one loop while the batch has more
  *                 than 2 x host_threads items left to take). */

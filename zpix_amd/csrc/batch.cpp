@@ -53,18 +53,19 @@ bool trace_on()
     static const bool on = getenv("ZPX_BATCH_TRACE") != nullptr;
     return on;
 }
-#define ZPX_TRACE(...)                                                                                     \
-    do {                                                                                                   \
-        if (trace_on()) {                                                                                  \
-            fprintf(stderr, "[zpx batch] " __VA_ARGS__);                                                    \
-            fputc('\n', stderr);                                                                           \
-        }                                                                                                  \
-    } while (0)
-
 double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+// (trace lines carry a steady-clock time in ms, for timelines)
+#define ZPX_TRACE(...)                                                                                     \
+    do {                                                                                                   \
+        if (trace_on()) {                                                                                  \
+            fprintf(stderr, "[zpx batch %.3f] ", now_s() * 1e3);                                            \
+            fprintf(stderr, __VA_ARGS__);                                                                   \
+            fputc('\n', stderr);                                                                           \
+        }                                                                                                  \
+    } while (0)
 
 struct Decoded {
     int item = -1;
@@ -82,6 +83,7 @@ struct Slot {
     hipEvent_t ev_in = nullptr, ev_kernel = nullptr, ev_done = nullptr;
     std::unique_ptr<Decoded> dec;
     bool busy = false;
+    int last_fmt = 0; // format of the slot's last item (its buffers' sizes follow it)
     bool check_png = false;
     bool failed = false; // the image failed after its slot was bound (status already set)
     DevPiecesExpand expand[4]; // a pieces frame the block kernels do not take: its expand jobs (issue_jpeg)
@@ -149,6 +151,31 @@ class Pipeline {
     std::vector<char> png_; // the item is a PNG (zpx_png_probe_buffer)
     int take_item(int &remaining);
     int take_png_partner();
+    // the dispatch window (take_item): 4 x threads items; test switch
+    // "batch_lookahead" 1: item order, k >= 2: k x threads
+    int lookahead_window() const
+    {
+        const int o = opt(Opt::BatchLookahead);
+        return o == 1 ? 1 : (o >= 2 ? o : 4) * std::max(1, threads_);
+    }
+    // A slot buffer at least n bytes large.  A buffer too small is replaced,
+    // and the old one kept until the pipeline ends: hipFree waits for the
+    // whole device, and freeing in the dispatch loop stalled it behind
+    // every queued copy and kernel (a JPEG slot taking a PNG: 20-80 ms).
+    hipError_t grow(DevBuf &b, size_t n)
+    {
+        if (b.ptr && b.bytes >= n) return hipSuccess;
+        if (b.ptr) {
+            retired_.push_back(b.ptr);
+            b.ptr = nullptr;
+            b.bytes = 0;
+        }
+        const double t = now_s();
+        const hipError_t e = b.alloc(n);
+        ZPX_TRACE("grow: %zu bytes in %.2f ms", n, (now_s() - t) * 1e3);
+        return e;
+    }
+    std::vector<void *> retired_; // replaced slot buffers, freed by ~Pipeline
     void push_decoded(std::unique_ptr<Decoded> d, double dt);
     double host_s_ = 0, host_jpeg_s_ = 0, host_png_s_ = 0;
     int jpeg_items_ = 0, png_items_ = 0;
@@ -168,6 +195,7 @@ Pipeline::~Pipeline()
     (void)hipStreamSynchronize(ctx_->stream);
     if (h2d_) (void)hipStreamSynchronize(h2d_);
     if (d2h_) (void)hipStreamSynchronize(d2h_);
+    for (void *p : retired_) (void)hipFree(p);
     for (auto &s : slots_) {
         if (s->ev_in) (void)hipEventDestroy(s->ev_in);
         if (s->ev_kernel) (void)hipEventDestroy(s->ev_kernel);
@@ -198,13 +226,43 @@ static double host_cost_estimate(const uint8_t *buf, size_t len)
     return 0;
 }
 
+// The inflated stream's bytes of a PNG from its IHDR (every pass's rows x
+// (1 + row bytes), readImagePass's layout, + ZPX_PNG_INPUT_PAD), 0 when the
+// header does not parse -- the size of its upload buffer.
+static size_t png_stream_bytes(const uint8_t *buf, size_t len)
+{
+    if (!zpx_png_probe_buffer(buf, len) || len < 29) return 0;
+    auto be32 = [&](size_t o) { return uint32_t(buf[o]) << 24 | uint32_t(buf[o + 1]) << 16 | uint32_t(buf[o + 2]) << 8 | buf[o + 3]; };
+    const uint64_t w = be32(16), h = be32(20);
+    static const int kChannels[7] = {1, 0, 3, 1, 2, 0, 4}; // by colour type
+    const int depth = buf[24], ct = buf[25] <= 6 ? buf[25] : 0;
+    const uint64_t bits = uint64_t(depth) * uint64_t(std::max(1, kChannels[ct]));
+    if (w == 0 || h == 0 || w > (1u << 20) || h > (1u << 20) || depth > 16) return 0;
+    uint64_t total = 0;
+    if (buf[28] == 1) { // Adam7: (x0, y0, dx, dy) per pass
+        static const int kP[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                                     {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+        for (const auto &p : kP) {
+            const uint64_t pw = w > uint64_t(p[0]) ? (w - p[0] + p[2] - 1) / p[2] : 0;
+            const uint64_t ph = h > uint64_t(p[1]) ? (h - p[1] + p[3] - 1) / p[3] : 0;
+            if (pw && ph) total += ph * (1 + (pw * bits + 7) / 8);
+        }
+    } else {
+        total = h * (1 + (w * bits + 7) / 8);
+    }
+    return static_cast<size_t>(total) + ZPX_PNG_INPUT_PAD;
+}
+
 // Next item for a worker: of the untaken items in the window [front_,
-// front_ + 2 threads_), the one of the largest host cost (the first of
+// front_ + 4 threads_), the one of the largest host cost (the first of
 // equals), so the batch's long items -- a tc8 PNG's inflate is ~3x a JPEG's
-// Huffman decode -- do not start last and set the end of the host stage.
-// (Simulated over the bench's 64 alternating 4K JPEG / PNG items on 16
-// workers: 357 ms in item order, 290 with this window, the even split.)  An
-// item waits at most one window behind its turn, so prefix completion
+// Huffman decode, a PNG pair ~5x -- do not start last and set the end of
+// the host stage.  Measured on the bench's 64 alternating 4K JPEG / PNG
+// items, 16 workers (tools/e2e_ab.py, batch_lookahead 0 vs 4): a window of
+// 2 threads items let only half the PNGs start (and pair) in the first wave,
+// and the pairs taken later ended the batch ~50 ms after the rest --
+// 3,560-3,640 MPix/s against 4,340-4,460 with 4 threads.  An item waits at
+// most one window behind its turn, so prefix completion
 // (zpx_batch_wait_prefix) still follows item order.  -1 when none remain;
 // `remaining` = the untaken items before this one was taken.
 int Pipeline::take_item(int &remaining)
@@ -213,7 +271,7 @@ int Pipeline::take_item(int &remaining)
     while (front_ < n_ && taken_[front_]) front_++;
     if (front_ >= n_) return -1;
     // (test switch "batch_lookahead" = 1: item order)
-    const int win = opt(Opt::BatchLookahead) == 1 ? 1 : 2 * std::max(1, threads_);
+    const int win = lookahead_window();
     const int end = std::min(n_, front_ + win);
     int best = -1;
     for (int i = front_; i < end; i++)
@@ -226,15 +284,18 @@ int Pipeline::take_item(int &remaining)
 
 // A second PNG for a worker that took a PNG while every worker has items
 // to spare (inflate_pair): of the untaken PNGs in take_item's window, the
-// one of the largest host cost; -1 when none.
+// one of the largest host cost, else the next untaken PNG past the window
+// (taking an item early delays no prefix); -1 when none.
 int Pipeline::take_png_partner()
 {
     std::lock_guard<std::mutex> lk(mu_);
-    const int win = opt(Opt::BatchLookahead) == 1 ? 1 : 2 * std::max(1, threads_);
+    const int win = lookahead_window();
     const int end = std::min(n_, front_ + win);
     int best = -1;
     for (int i = front_; i < end; i++)
         if (!taken_[i] && png_[i] && (best < 0 || cost_[i] > cost_[best])) best = i;
+    for (int i = end; best < 0 && i < n_; i++)
+        if (!taken_[i] && png_[i]) best = i;
     if (best >= 0) {
         taken_[best] = 1;
         ntaken_++;
@@ -277,12 +338,14 @@ void Pipeline::worker()
                           ? take_png_partner()
                           : -1;
         const int need = j >= 0 ? 2 : 1;
+        ZPX_TRACE("worker: took item %d%s%d (remaining %d)", i, j >= 0 ? " + " : "", j, remaining);
         {
             std::unique_lock<std::mutex> lk(mu_);
             cv_token_.wait(lk, [&] { return tokens_ >= need || stop_; });
             if (stop_) return;
             tokens_ -= need;
         }
+        ZPX_TRACE("worker: tokens for item %d", i);
         if (j >= 0) {
             std::unique_ptr<Decoded> d0(new (std::nothrow) Decoded), d1(new (std::nothrow) Decoded);
             if (!d0 || !d1) { // out of memory: report on the items, keep the pipeline going
@@ -360,6 +423,17 @@ int Pipeline::setup()
         if (!s->hstatus.alloc(16, true)) return ZPX_E_OUT_OF_MEMORY;
         slots_.push_back(std::move(s));
     }
+    // every slot's input buffer sized for the batch's largest PNG stream up
+    // front (IHDR), when that takes at most a quarter of the free device
+    // memory: a device allocation in the dispatch loop waits behind the
+    // workers' pinned-memory allocations (hipMalloc of 50 MB: 20-65 ms in a
+    // traced 4K batch, the dispatch of every later item held up with it)
+    size_t max_in = 0;
+    for (int i = 0; i < n_; i++)
+        if (png_[i]) max_in = std::max(max_in, png_stream_bytes(items_[i].buf, items_[i].len));
+    size_t free_b = 0, total_b = 0;
+    if (max_in && hipMemGetInfo(&free_b, &total_b) == hipSuccess && max_in * slots_.size() <= free_b / 4)
+        for (auto &s : slots_) HIPCHK(ctx_, grow(s->din, max_in));
     HIPCHK(ctx_, hipStreamSynchronize(ctx_->stream));
     return ZPX_OK;
 }
@@ -395,7 +469,7 @@ int Pipeline::upload_pieces(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f, bo
     const JpegPieces &p = jc.pieces;
     size_t ib = 0;
     for (int c = 0; c < jc.n_comp; c++) ib += align_up(p.blocks[c] * sizeof(uint32_t));
-    HIPCHK(ctx_, s.din.reserve(ib + p.data_bytes()));
+    HIPCHK(ctx_, grow(s.din, ib + p.data_bytes()));
     uint8_t *base = s.din.as<uint8_t>();
     const uint32_t *dix[4] = {};
     size_t off = 0;
@@ -420,7 +494,7 @@ int Pipeline::upload_pieces(Slot &s, const JpegCoeffs &jc, zpx_jpeg_frame &f, bo
         gbytes[c] = p.blocks[c] * 64 * (f.coeff_bits / 8);
         total += align_up(gbytes[c]);
     }
-    HIPCHK(ctx_, s.dgrid.reserve(total));
+    HIPCHK(ctx_, grow(s.dgrid, total));
     off = 0;
     for (int c = 0; c < jc.n_comp; c++) {
         DevPiecesExpand &j = s.expand[s.nexpand++];
@@ -468,7 +542,7 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
     } else {
         size_t total = 0;
         for (int c = 0; c < 4; c++) total += f.coeffs[c] ? align_up(cb[c]) : 0;
-        HIPCHK(ctx_, s.din.reserve(total));
+        HIPCHK(ctx_, grow(s.din, total));
         size_t off = 0;
         for (int c = 0; c < 4; c++) {
             if (!f.coeffs[c]) continue;
@@ -485,7 +559,7 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
         // the jobs go up behind the frame descriptor's place in the staging
         // (the descriptor copy below must not overwrite them in flight)
         const size_t jo = align_up(sizeof(DevJpegFrame));
-        HIPCHK(ctx_, s.ddesc.reserve(jo + sizeof(s.expand)));
+        HIPCHK(ctx_, grow(s.ddesc, jo + sizeof(s.expand)));
         if (!host_reserve(s.hdesc, jo + sizeof(s.expand))) return ZPX_E_OUT_OF_MEMORY;
         memcpy(static_cast<uint8_t *>(s.hdesc.ptr) + jo, s.expand, sizeof(s.expand));
         HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.as<uint8_t>() + jo, static_cast<uint8_t *>(s.hdesc.ptr) + jo,
@@ -501,7 +575,7 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
         const bool direct = !on_host_ && stride == size_t(W) * 4;
         uint8_t *out = it.dst;
         if (!direct) {
-            HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+            HIPCHK(ctx_, grow(s.dout, size_t(W) * H * 4));
             out = s.dout.as<uint8_t>();
         }
         if (int e = jpeg_planes_to_rgba(ctx_, d.jc, f, s.dimg, s.ddesc, s.hdesc, out, ctx_->stream)) {
@@ -523,7 +597,7 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
         out = it.dst;
         f.rgba_stride = stride;
     } else {
-        HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+        HIPCHK(ctx_, grow(s.dout, size_t(W) * H * 4));
         out = s.dout.as<uint8_t>();
         f.rgba_stride = size_t(W) * 4;
     }
@@ -531,7 +605,7 @@ int Pipeline::issue_jpeg(Slot &s, bool &sync_done)
     const DevJpegFrame df = dev_jpeg_frame(f);
     if (!host_reserve(s.hdesc, sizeof(df))) return ZPX_E_OUT_OF_MEMORY;
     memcpy(s.hdesc.ptr, &df, sizeof(df));
-    HIPCHK(ctx_, s.ddesc.reserve(sizeof(df)));
+    HIPCHK(ctx_, grow(s.ddesc, sizeof(df)));
     HIPCHK(ctx_, hipMemcpyAsync(s.ddesc.ptr, s.hdesc.ptr, sizeof(df), hipMemcpyHostToDevice, ctx_->stream));
     if (int rc = launch_jpeg_rgba_frame(f, s.ddesc.as<DevJpegFrame>(), ctx_->stream))
         return rc == -2 ? ZPX_E_UNSUPPORTED : hip_fail(ctx_, hipGetLastError(), "batch: jpeg kernel");
@@ -556,8 +630,10 @@ int Pipeline::issue_png(Slot &s)
     const bool pair = png_use_pair(ps.depth, ps.interlace, ps.use_transparent, W,
                                    ps.kind == ZPX_RGBA ? stride : size_t(W) * ps.out_bpp);
     const size_t in_len = ps.data_len + ZPX_PNG_INPUT_PAD;
-    HIPCHK(ctx_, s.din.reserve(in_len));
+    HIPCHK(ctx_, grow(s.din, in_len));
+    const double th = now_s();
     HIPCHK(ctx_, hipMemcpyAsync(s.din.ptr, ps.data.ptr, in_len, hipMemcpyHostToDevice, h2d_));
+    ZPX_TRACE("png: item %d H2D issue %.2f ms (pinned %d)", d.item, (now_s() - th) * 1e3, ps.data.pinned ? 1 : 0);
     h2d_bytes_ += double(ps.data_len);
     HIPCHK(ctx_, hipEventRecord(s.ev_in, h2d_));
     HIPCHK(ctx_, hipStreamWaitEvent(ctx_->stream, s.ev_in, 0));
@@ -572,13 +648,13 @@ int Pipeline::issue_png(Slot &s)
             img_out = it.dst;
             img_stride = stride;
         } else {
-            HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+            HIPCHK(ctx_, grow(s.dout, size_t(W) * H * 4));
             img_out = s.dout.as<uint8_t>();
             img_stride = size_t(W) * 4;
         }
     } else {
         img_stride = size_t(W) * ps.out_bpp;
-        HIPCHK(ctx_, s.dimg.reserve(img_stride * H));
+        HIPCHK(ctx_, grow(s.dimg, img_stride * H));
         img_out = s.dimg.as<uint8_t>();
     }
     zpx_png_frame f;
@@ -600,7 +676,7 @@ int Pipeline::issue_png(Slot &s)
     const bool dev_slab = pair && opt(Opt::PngDeviceSlab);
     if (dev_slab) {
         const size_t slab_b = png_dev_slab_layout(f, slab_off);
-        HIPCHK(ctx_, s.dslab.reserve(slab_b));
+        HIPCHK(ctx_, grow(s.dslab, slab_b));
         png_dev_slab_jobs(f, slab_off, s.din.as<uint8_t>(), in_len, s.dslab.as<uint8_t>(), sjobs, slab_groups);
         f.filtered = s.dslab.as<uint8_t>();
         f.layout = ZPX_PNG_LAYOUT_SLAB;
@@ -612,7 +688,7 @@ int Pipeline::issue_png(Slot &s)
     Adam7Stage a7;
     if (pair && ps.interlace) {
         png_adam7_stage(f, static_cast<int>(ps.out_bpp), passes, 0, a7);
-        HIPCHK(ctx_, s.dstage.reserve(a7.bytes));
+        HIPCHK(ctx_, grow(s.dstage, a7.bytes));
     }
     const PngBandPlan bp = png_plan_bands(ps.depth, pair, passes, rowbytes);
     const uint32_t granules = bp.granules;
@@ -627,7 +703,7 @@ int Pipeline::issue_png(Slot &s)
     const size_t table_b = align_up(slab_off.size() * sizeof(uint64_t));
     const size_t sjobs_b = sjobs.size() * sizeof(DevSlabBand);
     const size_t desc_b = pass_b + sched_b + pal_b + merge_b + table_b + sjobs_b;
-    HIPCHK(ctx_, s.ddesc.reserve(desc_b));
+    HIPCHK(ctx_, grow(s.ddesc, desc_b));
     uint8_t *dd = s.ddesc.as<uint8_t>();
     if (!a7.jobs.empty())
         png_adam7_rebase(passes, a7, s.dstage.as<uint8_t>(),
@@ -654,7 +730,7 @@ int Pipeline::issue_png(Slot &s)
     }
     const size_t bound_b = std::max<size_t>(1, base) * granules * sizeof(uint64_t);
     if (s.dbound.bytes < bound_b) { // fresh granules carry tag 0, older than any epoch
-        HIPCHK(ctx_, s.dbound.alloc(bound_b));
+        HIPCHK(ctx_, grow(s.dbound, bound_b));
         HIPCHK(ctx_, hipMemsetAsync(s.dbound.ptr, 0, bound_b, ctx_->stream));
     }
     ZPX_TRACE("png: item %d %ux%u depth %d interlace %d passes %zu bands %u+%u granules %u", d.item, W, H, ps.depth,
@@ -704,7 +780,7 @@ int Pipeline::issue_png(Slot &s)
     if (direct) {
         rgba = it.dst;
     } else {
-        HIPCHK(ctx_, s.dout.reserve(size_t(W) * H * 4));
+        HIPCHK(ctx_, grow(s.dout, size_t(W) * H * 4));
         rgba = s.dout.as<uint8_t>();
     }
     if (launch_rgba_pixels(m, rgba, ctx_->stream)) return hip_fail(ctx_, hipGetLastError(), "batch: rgba kernel");
@@ -814,15 +890,19 @@ int Pipeline::run(zpx_batch_stats *stats)
                 give_token();
                 finished(d->item);
             } else {
+                // a free slot, one whose last item had this item's format if
+                // any: its grow-only device buffers then fit without a new
+                // allocation (hipFree / hipMalloc wait for the device: a PNG
+                // bound to a slot that held JPEGs stalled this loop -- and so
+                // every later item's dispatch -- for 20-80 ms)
                 Slot *free_slot = nullptr;
                 for (auto &s : slots_)
-                    if (!s->busy) {
+                    if (!s->busy && (!free_slot || (s->last_fmt == d->fmt && free_slot->last_fmt != d->fmt)))
                         free_slot = s.get();
-                        break;
-                    }
                 // a worker holds a token for every decoded item, and there are
                 // as many tokens as slots, so a free slot always exists here
                 Slot &s = *free_slot;
+                s.last_fmt = d->fmt;
                 s.dec = std::move(d);
                 s.busy = true;
                 bool sync_done = false;
