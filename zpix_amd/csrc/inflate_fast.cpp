@@ -24,6 +24,8 @@
 #include <atomic>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <utility>
 #include <thread>
 #include <vector>
 
@@ -335,11 +337,60 @@ template <typename T> inline void copy_match(T *dst, size_t d, size_t n)
 
 // Output of one decode run: a fixed buffer (capacity = the bytes wanted) or
 // a growable one (the parallel path's speculative chunks).
+// A vector whose resize() leaves new elements uninitialised (the decoder
+// writes every element it keeps)
+template <class T> struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    template <class U> void construct(U *p) noexcept { ::new (static_cast<void *>(p)) U; }
+    template <class U, class... A> void construct(U *p, A &&...a)
+    {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <typename T> using RawVec = std::vector<T, NoInitAlloc<T>>;
+
+// The speculative chunks' symbol buffers, recycled: 8 MB a chunk, zeroed and
+// page-faulted in on every call when they were fresh vectors (at most
+// 1 GiB held)
+class SymPool {
+  public:
+    RawVec<uint16_t> take()
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (free_.empty()) return {};
+        RawVec<uint16_t> v = std::move(free_.back());
+        free_.pop_back();
+        held_ -= v.capacity() * 2;
+        return v;
+    }
+    void give(RawVec<uint16_t> &&v)
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (v.capacity() == 0 || held_ + v.capacity() * 2 > (size_t(1) << 30)) return;
+        held_ += v.capacity() * 2;
+        free_.push_back(std::move(v));
+    }
+
+  private:
+    std::mutex mu_;
+    std::vector<RawVec<uint16_t>> free_;
+    size_t held_ = 0;
+};
+SymPool &sym_pool()
+{
+    static SymPool *p = new SymPool; // (intentionally leaked)
+    return *p;
+}
+
 // `o` is the committed end (a block's start while its symbols decode).
 template <typename T> struct Out {
     T *p = nullptr;
     size_t o = 0, cap = 0;
-    std::vector<T> *grow = nullptr;
+    RawVec<T> *grow = nullptr;
     // room for n elements from element `at` (a growable buffer grows; p may move)
     bool room(size_t at, size_t n)
     {
@@ -921,7 +972,10 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
     if (!run_pool(1, T, [&](int i) { if (i) search(i); })) return false; // (cand[0] is the stream start)
     // 2. speculative decode, chunk i from cand[i] to the next candidate it lands on
     struct Chunk {
-        std::vector<uint16_t> sym;
+        RawVec<uint16_t> sym = sym_pool().take();
+        ~Chunk() { sym_pool().give(std::move(sym)); }
+        Chunk() = default;
+        Chunk(Chunk &&) = default;
         size_t n = 0;       // output elements (without the window)
         int next = -1;      // index of the candidate it landed on (T = the stream end)
         bool ok = false;
