@@ -101,7 +101,8 @@ inline uint32_t reverse(uint32_t code, int len)
 // code: we reject it and let zlib handle that stream).  Runs once per
 // dynamic block (~3,000 per 4K image), so it avoids per-call clears: the
 // subtable-size scratch is kept zero between calls.
-bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind)
+// (rev_out: the symbols' bit-reversed codes, for pair_literals; 320 entries)
+bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind, uint16_t *rev_out = nullptr)
 {
     uint16_t count[16] = {};
     for (int i = 0; i < n; i++) count[lens[i]]++;
@@ -119,7 +120,8 @@ bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind
         code = static_cast<uint16_t>((code + count[l - 1]) << 1);
         next[l] = code;
     }
-    uint16_t rev[320];
+    uint16_t rev_local[320];
+    uint16_t *const rev = rev_out ? rev_out : rev_local;
     static thread_local uint8_t sub_bits[1 << 12]; // zero between calls
     uint16_t longp[320];
     int nlong = 0;
@@ -190,7 +192,7 @@ bool build(uint32_t *t, int cap, const uint8_t *lens, int n, int root, Kind kind
 // first literal of l1 bits walks just the prefix of budget <= root - l1.
 // (Walking every entry of every short literal, with its data-dependent
 // branch, cost ~16k cycles a block -- a tenth of a noisy 4K image's decode.)
-void pair_literals(uint32_t *t, int root, const uint8_t *lens, int n)
+void pair_literals(uint32_t *t, int root, const uint8_t *lens, int n, const uint16_t *rev)
 {
     int minlen = 16;
     for (int s = 0; s < 256 && s < n; s++)
@@ -224,19 +226,10 @@ void pair_literals(uint32_t *t, int root, const uint8_t *lens, int n)
         }
     // (start[k] now ends budget k's run: the candidates of budget <= b are
     // cand[0 .. start[b]))
-    uint16_t count[16] = {}, next[16];
-    for (int s = 0; s < n; s++) count[lens[s]]++;
-    count[0] = 0;
-    uint16_t code = 0;
-    for (int l = 1; l < 16; l++) {
-        code = static_cast<uint16_t>((code + count[l - 1]) << 1);
-        next[l] = code;
-    }
     for (int s = 0; s < 256 && s < n; s++) {
         const int l1 = lens[s];
-        if (!l1) continue;
-        const uint32_t r1 = reverse(next[l1]++, l1);
-        if (l1 > maxb) continue;
+        if (!l1 || l1 > maxb) continue;
+        const uint32_t r1 = rev[s]; // (the root's canonical code, from build())
         const int end = start[root - l1];
         const uint32_t add = uint32_t(s) << 16 | uint32_t(l1);
         for (int i = 0; i < end; i++) t[r1 | static_cast<uint32_t>(cand[i]) << l1] = sec[i] + add;
@@ -406,7 +399,8 @@ template <typename T> struct Out {
 
 // The dynamic block header (RFC 1951 3.2.7) after BTYPE: both tables.
 // (lit_lens: the literal/length code lengths, for pair_literals; may be null)
-bool read_dynamic(Bits &b, uint32_t *lit, uint32_t *dist, uint8_t *lit_lens = nullptr, int *nlit = nullptr)
+bool read_dynamic(Bits &b, uint32_t *lit, uint32_t *dist, uint8_t *lit_lens = nullptr, int *nlit = nullptr,
+                  uint16_t *lit_rev = nullptr)
 {
     b.refill();
     const int hlit = static_cast<int>(b.take(5)) + 257;
@@ -446,7 +440,7 @@ bool read_dynamic(Bits &b, uint32_t *lit, uint32_t *dist, uint8_t *lit_lens = nu
         }
     }
     if (lens[256] == 0) return false; // no end-of-block code
-    if (!build(lit, kLitEntries, lens, hlit, kLitBits, Kind::LitLen)) return false;
+    if (!build(lit, kLitEntries, lens, hlit, kLitBits, Kind::LitLen, lit_rev)) return false;
     if (lit_lens) {
         memcpy(lit_lens, lens, static_cast<size_t>(hlit));
         *nlit = hlit;
@@ -484,6 +478,7 @@ bool stored_block(Bits &b, size_t &at, uint32_t &len)
 // header bits are consumed, literal pairs included.  False when irregular.
 bool block_tables(Bits &b, uint32_t type, uint32_t *lit, uint32_t *dist)
 {
+    uint16_t rev[320];
     uint8_t l[320];
     int nl = 0;
     if (type == 1) { // fixed codes
@@ -492,17 +487,17 @@ bool block_tables(Bits &b, uint32_t type, uint32_t *lit, uint32_t *dist)
         for (int i = 256; i < 280; i++) l[i] = 7;
         for (int i = 280; i < 288; i++) l[i] = 8;
         // zlib's fixed table has 288 literal/length symbols (286, 287 invalid when used)
-        if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen)) return false;
+        if (!build(lit, kLitEntries, l, 288, kLitBits, Kind::LitLen, rev)) return false;
         nl = 288;
         uint8_t d[32];
         for (int i = 0; i < 32; i++) d[i] = 5;
         if (!build(dist, kDistEntries, d, 32, kDistBits, Kind::Dist)) return false;
     } else if (type == 2) { // dynamic
-        if (!read_dynamic(b, lit, dist, l, &nl)) return false;
+        if (!read_dynamic(b, lit, dist, l, &nl, rev)) return false;
     } else {
         return false;
     }
-    pair_literals(lit, kLitBits, l, nl);
+    pair_literals(lit, kLitBits, l, nl, rev);
     return !b.overrun();
 }
 
