@@ -620,15 +620,22 @@ class Decoder {
         }
     };
     // Bit readers of a first scan's block (first_block).  MemberBits is the
-    // Decoder's own: huffman / receive_extend / bits above.  FastBits runs
-    // the same operations, byte for byte and bit for bit, on register copies
-    // of (ba_, bn_, pos_, unread_) -- bm_ is always 1 << (bn_ - 1) -- while
-    // at least kFastSlack input bytes remain, so no read reaches the end;
-    // an operation whose byte reads would meet a marker (0xFF not followed by
-    // 0x00), or a code longer than the 8-bit table, is handed to the member
-    // function with the state written back, and the copies reloaded after it.
-    // (The members, updated through `this` beside the int32 block stores,
-    // were reloaded and stored around every symbol.)
+    // Decoder's own: huffman / receive_extend / bits above, the reference's
+    // lazy byte-at-a-time reads (ensureNBits / readByteStuffedByte).
+    // FastBits decodes from a 64-bit look-ahead of the stream instead -- the
+    // member's buffered bits, then plain bytes up to the next 0xFF -- and
+    // tracks what the member would have read: C bits consumed and H, the
+    // furthest bit any operation needed (ensure(n) = C + n); the member's
+    // reads being lazy and whole bytes, it would hold (H - bn0) / 8 bytes
+    // more, rounded up, so sync() rebuilds (ba_, bn_, bm_, pos_, unread_)
+    // exactly.  An operation whose bits reach a 0xFF byte (a stuffed byte or
+    // a marker), or a code the member would finish bit by bit, syncs, runs
+    // the member function and reloads, so its outcome -- value or error -- is
+    // the member's.  Used while kFastSlack input bytes remain (no read
+    // reaches the end); the pieces path keeps one for a whole MCU
+    // (mcu_pieces).  (The members, updated through `this` beside the int32
+    // block stores, were reloaded and stored around every symbol; the
+    // byte-at-a-time copy of them branched on every byte.)
     static constexpr size_t kFastSlack = 2048; // > any block's entropy-coded bytes (64 x 27 bits, stuffed x2)
     struct MemberBits {
         Decoder &d;
@@ -640,107 +647,140 @@ class Decoder {
     struct FastBits {
         Decoder &d;
         const uint8_t *src;
-        uint32_t ba;
-        int32_t bn;
-        size_t pos;
-        int unread;
-        explicit FastBits(Decoder &dd) : d(dd), src(dd.src_), ba(dd.ba_), bn(dd.bn_), pos(dd.pos_), unread(dd.unread_) {}
+        uint64_t acc = 0;
+        int avail = 0;
+        size_t q = 0;
+        uint32_t ba0 = 0;
+        int32_t bn0 = 0, C = 0, H = 0;
+        size_t pos0 = 0;
+        size_t unread0 = 0;
+        explicit FastBits(Decoder &dd) : d(dd), src(dd.src_) { load(); }
         __attribute__((always_inline)) void sync()
         {
+            const int32_t k = H > bn0 ? (H - bn0 + 7) >> 3 : 0;
+            uint32_t ba = ba0;
+            if (k >= 4) {
+                ba = uint32_t(src[pos0 + k - 4]) << 24 | uint32_t(src[pos0 + k - 3]) << 16 |
+                     uint32_t(src[pos0 + k - 2]) << 8 | src[pos0 + k - 1];
+            } else {
+                for (int32_t i = 0; i < k; i++) ba = (ba << 8) | src[pos0 + static_cast<size_t>(i)];
+            }
             d.ba_ = ba;
-            d.bn_ = bn;
-            d.bm_ = bn > 0 ? 1u << (bn - 1) : 0u;
-            d.pos_ = pos;
-            d.unread_ = unread;
+            d.bn_ = bn0 + 8 * k - C;
+            d.bm_ = d.bn_ > 0 ? 1u << (d.bn_ - 1) : 0u;
+            d.pos_ = pos0 + static_cast<size_t>(k);
+            d.unread_ = k > 0 ? 1 : unread0;
         }
         __attribute__((always_inline)) void load()
         {
-            ba = d.ba_;
-            bn = d.bn_;
-            pos = d.pos_;
-            unread = d.unread_;
+            ba0 = d.ba_;
+            bn0 = d.bn_;
+            pos0 = d.pos_;
+            unread0 = d.unread_;
+            C = H = 0;
+            acc = bn0 > 0 ? uint64_t(ba0 & (bn0 >= 32 ? ~0u : (1u << bn0) - 1)) << (64 - bn0) : 0;
+            avail = bn0;
+            q = pos0;
+            refill();
         }
-        // stuffed() + one step of ensure(): false (nothing read) at a marker
-        __attribute__((always_inline)) bool fill()
+        __attribute__((always_inline)) void refill()
         {
-            const uint8_t x = src[pos];
-            if (x != 0xff) {
-                pos += 1;
-                unread = 1;
-            } else {
-                if (src[pos + 1] != 0x00) return false;
-                pos += 2;
-                unread = 2;
+            uint64_t le;
+            memcpy(&le, src + q, 8);
+            const uint64_t x = ~le;
+            const uint64_t z = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+            const int plain = z ? __builtin_ctzll(z) >> 3 : 8;
+            const int nb = std::min((64 - avail) >> 3, plain);
+            if (nb > 0) {
+                acc |= (__builtin_bswap64(le) >> (64 - 8 * nb)) << (64 - avail - 8 * nb);
+                avail += 8 * nb;
+                q += static_cast<size_t>(nb);
             }
-            ba = (ba << 8) | x;
-            bn += 8;
+        }
+        __attribute__((always_inline)) bool need(int n)
+        {
+            if (avail < n) refill();
+            if (avail < n) return false;
+            H = std::max(H, C + n);
             return true;
         }
-        __attribute__((always_inline)) int huffman(const Huff &h, uint8_t &out)
+        __attribute__((always_inline)) void consume(int n)
         {
-            if (h.num_codes != 0 && (bn >= 8 || fill())) {
-                const uint16_t lv = h.lut[(ba >> (bn - 8)) & 0xff];
-                if (lv != 0) {
-                    bn -= static_cast<int32_t>(lv & 0xff) - 1;
-                    out = static_cast<uint8_t>(lv >> 8);
-                    return 0;
-                }
-            }
+            C += n;
+            acc = n < 64 ? acc << n : 0;
+            avail -= n;
+        }
+        __attribute__((always_inline)) int slow_huffman(const Huff &h, uint8_t &out)
+        {
             sync();
             const int e = d.huffman(h, out);
             load();
             return e;
         }
-        __attribute__((always_inline)) int receive_extend(uint8_t t, int32_t &out)
+        __attribute__((always_inline)) int huffman(const Huff &h, uint8_t &out)
         {
-            while (bn < static_cast<int32_t>(t)) {
-                if (!fill()) {
-                    sync();
-                    const int e = d.receive_extend(t, out);
-                    load();
-                    return e;
+            if (h.num_codes == 0 || !need(8)) return slow_huffman(h, out);
+            const uint16_t lv = h.lut[acc >> 56];
+            if (lv != 0) {
+                consume(static_cast<int>(lv & 0xff) - 1);
+                out = static_cast<uint8_t>(lv >> 8);
+                return 0;
+            }
+            const int32_t k = (H - bn0 + 7) >> 3;
+            const int held = bn0 + 8 * k - C;
+            if (avail < 16) refill();
+            for (int i = 8; i < 16 && i < held && i < avail; i++) {
+                const int32_t code = static_cast<int32_t>(acc >> (63 - i));
+                if (code <= h.max_codes[i]) {
+                    const int32_t idx = h.vals_indices[i] + code - h.min_codes[i];
+                    if (idx < 0 || idx > 255) break;
+                    consume(i + 1);
+                    out = h.vals[idx];
+                    return 0;
                 }
             }
-            bn -= t;
+            return slow_huffman(h, out);
+        }
+        __attribute__((always_inline)) int receive_extend(uint8_t t, int32_t &out)
+        {
+            if (!need(t)) {
+                sync();
+                const int e = d.receive_extend(t, out);
+                load();
+                return e;
+            }
             const int32_t thr = int32_t(1) << t;
-            int32_t v = static_cast<int32_t>((ba >> bn) & static_cast<uint32_t>(thr - 1));
-            // (branch-free: the sign of a coefficient is a coin toss)
+            int32_t v = t ? static_cast<int32_t>(acc >> (64 - t)) : 0;
+            consume(t);
             v += ((v - (thr >> 1)) >> 31) & (static_cast<int32_t>(0xffffffffu << t) + 1);
             out = v;
             return 0;
         }
         __attribute__((always_inline)) int bit(bool &out)
         {
-            if (bn == 0 && !fill()) {
+            if (!need(1)) {
                 sync();
                 const int e = d.bit(out);
                 load();
                 return e;
             }
-            out = ((ba >> (bn - 1)) & 1u) != 0;
-            bn--;
+            out = (acc >> 63) != 0;
+            consume(1);
             return 0;
         }
         __attribute__((always_inline)) int bits(int32_t n, uint32_t &out)
         {
-            while (bn < n) {
-                if (!fill()) {
-                    sync();
-                    const int e = d.bits(n, out);
-                    load();
-                    return e;
-                }
+            if (n > 32 || !need(n)) {
+                sync();
+                const int e = d.bits(n, out);
+                load();
+                return e;
             }
-            uint32_t r = ba >> (bn - n);
-            r &= n >= 32 ? 0xffffffffu : ((1u << n) - 1);
-            bn -= n;
-            out = r;
+            out = n ? static_cast<uint32_t>(acc >> (64 - n)) : 0u;
+            consume(n);
             return 0;
         }
     };
-    // (inlined into mcu(): the reader and nnz then live in registers; called
-    // out of line, FastBits' fields stayed in memory, written and re-read
-    // around the block's byte / int stores, and receive_extend was a call)
     template <class R>
     __attribute__((always_inline)) int first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
                                                    int32_t &dcv, int32_t *b, uint8_t *nzpos, int &nnz);
@@ -755,6 +795,12 @@ class Decoder {
     template <class Sink>
     int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
             Sink &sink);
+    // an interleaved baseline MCU into pieces (first_block_pieces per block)
+    // on one register reader for the whole MCU
+    int mcu_pieces(const Scan &sc, int32_t my, int32_t mx, int32_t *dc, int32_t *zz, JpegPieces &p);
+    template <class R>
+    __attribute__((always_inline)) int mcu_pieces_with(R &r, const Scan &sc, int32_t my, int32_t mx, int32_t *dc,
+                                                       int32_t *zz, JpegPieces &p);
     // one block of a progressive scan, touching only the scan's band
     template <class R>
     int prog_block(R &r, const Scan &sc, int ci, size_t blk, const Huff &hdc, const Huff &hac, int32_t *dc);
@@ -1368,10 +1414,44 @@ int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huf
     return rc;
 }
 
+template <class R>
+int Decoder::mcu_pieces_with(R &r, const Scan &sc, int32_t my, int32_t mx, int32_t *dc, int32_t *zz, JpegPieces &p)
+{
+    const int32_t mxx = sc.mxx;
+    for (int k = 0; k < sc.ns; k++) {
+        const int ci = sc.c[k].id;
+        const int32_t hi = o_.comp[ci].h, vi = o_.comp[ci].v;
+        const Huff &hdc = huff_[0][sc.c[k].td];
+        const Huff &hac = huff_[1][sc.c[k].ta];
+        for (int32_t j = 0; j < hi * vi; j++) {
+            const int32_t bx = hi * mx + j % hi, by = vi * my + j / hi;
+            ZTRY(first_block_pieces(r, sc, hdc, hac, dc[ci], p, ci, size_t(by) * size_t(mxx * hi) + size_t(bx), zz));
+        }
+    }
+    return 0;
+}
+
+int Decoder::mcu_pieces(const Scan &sc, int32_t my, int32_t mx, int32_t *dc, int32_t *zz, JpegPieces &p)
+{
+    constexpr size_t kMcuSlack = 8192; // > an MCU's entropy-coded bytes (<= 10 blocks x 216, stuffed x2)
+    if (len_ - pos_ >= kMcuSlack) {
+        FastBits fb(*this);
+        const int e = mcu_pieces_with(fb, sc, my, mx, dc, zz, p);
+        fb.sync();
+        return e;
+    }
+    MemberBits mb{*this};
+    return mcu_pieces_with(mb, sc, my, mx, dc, zz, p);
+}
+
 template <class Sink>
 int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b,
                  uint8_t *nzpos, Sink &sink)
 {
+    if constexpr (std::is_same<Sink, PieceSink>::value) {
+        // (b: the zig-zag block, zero between blocks)
+        if (!sc.prog && sc.ah == 0 && sc.ns != 1) return mcu_pieces(sc, my, mx, dc, b, sink.p);
+    }
     const int32_t mxx = sc.mxx;
     for (int k = 0; k < sc.ns; k++) {
         const int ci = sc.c[k].id;
