@@ -28,5 +28,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     || { echo "rocprof failed rc=$?"; tail -30 "$OUT/prof_bench.err"; exit 1; }
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 find "$OUT/prof" -name '*kernel_trace.csv' -exec python3 "$ROOTDIR/tools/trace_stats.py" {} \; > "$OUT/kernel_by_launch.csv"
-cut -c1-200 "$OUT/kernel_by_launch.csv" | head -8
+cut -c1-200 "$OUT/kernel_by_launch.csv" | sed -n 1,8p
 echo gpu_round done
