@@ -205,27 +205,6 @@ Pipeline::~Pipeline()
     if (d2h_) (void)hipStreamDestroy(d2h_);
 }
 
-// Host cost estimate of an item (ns on the GPU boxes' Zen 5 cores, order
-// of magnitude only: it orders the dispatch, nothing else).  PNG: inflate,
-// ~2 ns per inflated byte (H x (1 + row bytes), from IHDR) + the CRC and
-// copy of the compressed bytes; JPEG: Huffman decoding, ~14 ns per
-// entropy-coded byte (the bench's 4K q75 frames: 2.8 MB in 39 ms, tc8 PNGs:
-// 50 MB inflated in 106 ms).  Anything else costs nothing on the host.
-static double host_cost_estimate(const uint8_t *buf, size_t len)
-{
-    if (zpx_png_probe_buffer(buf, len)) {
-        if (len < 29) return 0;
-        auto be32 = [&](size_t o) { return uint32_t(buf[o]) << 24 | uint32_t(buf[o + 1]) << 16 | uint32_t(buf[o + 2]) << 8 | buf[o + 3]; };
-        const double w = be32(16), h = be32(20);
-        static const int kChannels[7] = {1, 0, 3, 1, 2, 0, 4}; // by colour type
-        const int depth = buf[24], ct = buf[25] <= 6 ? buf[25] : 0;
-        const double bits = double(depth) * std::max(1, kChannels[ct]);
-        return 2.0 * h * (1.0 + std::ceil(w * bits / 8.0)) + 0.5 * double(len);
-    }
-    if (zpx_jpeg_probe_buffer(buf, len)) return 14.0 * double(len);
-    return 0;
-}
-
 // The inflated stream's bytes of a PNG from its IHDR (every pass's rows x
 // (1 + row bytes), readImagePass's layout, + ZPX_PNG_INPUT_PAD), 0 when the
 // header does not parse -- the size of its upload buffer.
@@ -251,6 +230,19 @@ static size_t png_stream_bytes(const uint8_t *buf, size_t len)
         total = h * (1 + (w * bits + 7) / 8);
     }
     return static_cast<size_t>(total) + ZPX_PNG_INPUT_PAD;
+}
+
+// Host cost estimate of an item (ns on the GPU boxes' Zen 5 cores, order
+// of magnitude only: it orders the dispatch, nothing else).  PNG: inflate,
+// ~2 ns per inflated byte (png_stream_bytes, from IHDR) + the CRC and
+// copy of the compressed bytes; JPEG: Huffman decoding, ~14 ns per
+// entropy-coded byte (the bench's 4K q75 frames: 2.8 MB in 39 ms, tc8 PNGs:
+// 50 MB inflated in 106 ms).  Anything else costs nothing on the host.
+static double host_cost_estimate(const uint8_t *buf, size_t len)
+{
+    if (zpx_png_probe_buffer(buf, len)) return 2.0 * double(png_stream_bytes(buf, len)) + 0.5 * double(len);
+    if (zpx_jpeg_probe_buffer(buf, len)) return 14.0 * double(len);
+    return 0;
 }
 
 // Next item for a worker: of the untaken items in the window [front_,
