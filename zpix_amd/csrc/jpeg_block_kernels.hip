@@ -86,6 +86,16 @@ constexpr int block_waves_per_eu()
                               : (!ZZ && H0 == 1 && V0 == 1 && HC == 1 && VC == 1 ? ZPX_JPEG_W444 : kWavesPerEu8);
 }
 constexpr int kStoreAux = 2; // nt
+// low-frequency chroma blocks (lf_high): 0 off, 1 the 4x4 test, 2 the 3x3
+// test and then the 4x4 one; ZPX_JPEGB_LF_INLANE: also 4:4:4's in-lane
+// chroma passes
+#ifndef ZPX_JPEGB_LF
+#define ZPX_JPEGB_LF 1
+#endif
+#ifndef ZPX_JPEGB_LF_INLANE
+#define ZPX_JPEGB_LF_INLANE 0
+#endif
+constexpr int kJpegLf = ZPX_JPEGB_LF;
 
 // Samples stay in the signed domain (sample - 128, the IDCT's clamp range
 // before its level shift): the +128 costs nothing folded into the colour
@@ -240,18 +250,63 @@ __device__ __forceinline__ void load_raw(const uint8_t *img, int j, u32x4 raw[Co
         raw[pc] = *reinterpret_cast<const u32x4 *>(img + 16 * CoefImage<CoefT>::slot(j, pc));
 }
 
+// Low-frequency blocks.  A block whose coefficients outside the top-left
+// NxN (N = 4 or 3) are all zero (at q75 every chroma block of the 4:2:0 bench frames, and
+// about half the 64-block chroma passes of 4:4:4 ones) has all-zero rows 4-7
+// after the row pass -- the reference's row pass maps a zero row to zeros
+// (idct.zig:84-97 and the full path agree there) -- so those rows are not
+// transformed, and the row pass of the others and the column pass run with
+// their inputs N-7 known zero, which hipcc folds (x + 0, 0 * c: the same
+// wrap-around values).  The test is per
+// wave (a uniform branch): lf_high() ORs the lane's coefficient words under a
+// mask of the positions outside 4x4 in the storage order (natural, or
+// zig-zag for ZPX_COEFFS_PIECES blocks).
+template <typename CoefT, bool ZZ, int N>
+struct LfMask {
+    static constexpr int NW = 16 * static_cast<int>(sizeof(CoefT)); // words per block
+    uint32_t m[NW];
+    constexpr LfMask() : m{}
+    {
+        constexpr int per = 4 / static_cast<int>(sizeof(CoefT)); // coefficients per word
+        for (int i = 0; i < 64; i++) {
+            int nat = i;
+            if (ZZ)
+                for (int k = 0; k < 64; k++)
+                    if (kZigOf[k] == i) nat = k;
+            if (nat / 8 >= N || nat % 8 >= N)
+                m[i / per] |= (sizeof(CoefT) == 1 ? 0xffu : 0xffffu) << (8 * static_cast<int>(sizeof(CoefT)) * (i % per));
+        }
+    }
+};
+template <typename CoefT, bool ZZ, int N>
+__device__ __forceinline__ uint32_t lf_high(const u32x4 raw[CoefImage<CoefT>::P])
+{
+    constexpr LfMask<CoefT, ZZ, N> M{};
+    uint32_t acc = 0;
+#pragma unroll
+    for (int w = 0; w < LfMask<CoefT, ZZ, N>::NW; w++) {
+        const uint32_t v = raw[w >> 2][w & 3];
+        if (M.m[w] == 0xffffffffu) acc |= v;
+        else if (M.m[w] != 0u) acc |= v & M.m[w];
+    }
+    return acc;
+}
+
 // Dequant + row pass (idct.zig:79-145) + column pass with clamp, as
 // idct_block, from the raw block and the component's quant-pair table.
-template <typename CoefT, bool ZZ = false, typename QRow>
+// N < 8: the block is low-frequency, its coefficients outside NxN zero (see
+// lf_high).
+template <typename CoefT, bool ZZ = false, int N = 8, typename QRow>
 __device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT>::P], QRow &&qrow, int32_t s[64])
 {
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
+    for (int r = 0; r < N; r++) { // (rows N-7 are zeros, never read)
         const u32x4 p = qrow(r, ZZ ? row_coef_pairs_zz<CoefT>(raw, r) : row_coef_pairs<CoefT>(raw, r));
         const uint32_t p17 = p[0], p53 = p[1], p26 = p[2], p04 = p[3];
         int32_t x4 = dot2<W1, W7>(p17), x5 = dot2<W7, -W1>(p17);
-        int32_t x6 = dot2<W5, W3>(p53), x7 = dot2<W3, -W5>(p53);
-        int32_t x8 = dot2<2048, 2048>(p04, 128), x0 = dot2<2048, -2048>(p04, 128);
+        int32_t x6 = N <= 3 ? 0 : dot2<W5, W3>(p53), x7 = N <= 3 ? 0 : dot2<W3, -W5>(p53);
+        // (N <= 4: coefficient 4 is zero, so x0 = x8; N <= 3: 3 and 5 too)
+        int32_t x8 = dot2<2048, 2048>(p04, 128), x0 = N <= 4 ? x8 : dot2<2048, -2048>(p04, 128);
         int32_t x2 = dot2<W6, -W2>(p26), x3 = dot2<W2, W6>(p26);
         int32_t x1 = x4 + x6;
         x4 -= x6;
@@ -279,7 +334,7 @@ __device__ __forceinline__ void idct_block_pairs(const u32x4 raw[CoefImage<CoefT
     for (int c = 0; c < 8; c++) {
         int32_t t[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) t[i] = s[8 * i + c];
+        for (int i = 0; i < 8; i++) t[i] = i >= N ? 0 : s[8 * i + c];
         idct_col_clamp<true, true>(t);
 #pragma unroll
         for (int i = 0; i < 8; i++) s[8 * i + c] = t[i];
@@ -672,7 +727,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 typedef const __attribute__((address_space(4))) u32x4 *cq;
                 const uint64_t q0 = ts.qp + 128 * c0, q2 = ts.qp + 256;
                 // dequantized pairs of row r: coefficient pairs c x the row's quant pairs
-                idct_block_pairs<CoefT, ZZ>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
+                auto qrow = [&](int r, u32x4 c) __attribute__((always_inline)) {
                     const u32x4 a = *reinterpret_cast<cq>(q0 + 16 * r);
                     if constexpr (kind(p) == 1 && kCb > 0 && kCb < 64) {
                         const u32x4 b = *reinterpret_cast<cq>(q2 + 16 * r);
@@ -689,7 +744,40 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                         (void)q2;
                         return u32x4{pk_mul16(c[0], a[0]), pk_mul16(c[1], a[1]), pk_mul16(c[2], a[2]), pk_mul16(c[3], a[3])};
                     }
-                }, s);
+                };
+                // an in-lane chroma block's samples leave the transform's
+                // registers inside each branch below (16 packed dwords live
+                // across the merge instead of 64 values: 4:4:4 int8 spilled
+                // otherwise)
+                auto inlane_out = [&]() __attribute__((always_inline)) {
+                    if constexpr (kind(p) >= 2) {
+                        // chroma block kept in this lane: 8 rows x 8 bytes
+                        const bool present = ts.g[kind(p) - 1] != nullptr;
+                        uint32_t *dst = kind(p) == 2 ? cbr : crr;
+#pragma unroll
+                        for (int r = 0; r < 8; r++) {
+                            dst[2 * r] = present ? pack4(s + 8 * r) : kBias4;
+                            dst[2 * r + 1] = present ? pack4(s + 8 * r + 4) : kBias4;
+                        }
+                    }
+                };
+                // chroma passes: low-frequency blocks (every lane's) take the
+                // short transform (lf_high)
+                if constexpr (kJpegLf > 0 && (kind(p) == 1 || (ZPX_JPEGB_LF_INLANE && kind(p) >= 2))) {
+                    if (kJpegLf >= 2 && __builtin_amdgcn_ballot_w64(lf_high<CoefT, ZZ, 3>(raw) != 0u) == 0) {
+                        idct_block_pairs<CoefT, ZZ, 3>(raw, qrow, s);
+                        inlane_out();
+                    } else if (__builtin_amdgcn_ballot_w64(lf_high<CoefT, ZZ, 4>(raw) != 0u) == 0) {
+                        idct_block_pairs<CoefT, ZZ, 4>(raw, qrow, s);
+                        inlane_out();
+                    } else {
+                        idct_block_pairs<CoefT, ZZ, 8>(raw, qrow, s);
+                        inlane_out();
+                    }
+                } else {
+                    idct_block_pairs<CoefT, ZZ>(raw, qrow, s);
+                    inlane_out();
+                }
             }
 
             if constexpr (kind(p) == 1) {
@@ -705,14 +793,6 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 }
                 if constexpr (p == CP - 1) wave_lds_order(); // tile complete before the luma passes
             } else if constexpr (kind(p) >= 2) {
-                // chroma block kept in this lane: 8 rows x 8 bytes
-                const bool present = ts.g[kind(p) - 1] != nullptr;
-                uint32_t *dst = kind(p) == 2 ? cbr : crr;
-#pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    dst[2 * r] = present ? pack4(s + 8 * r) : kBias4;
-                    dst[2 * r + 1] = present ? pack4(s + 8 * r + 4) : kBias4;
-                }
             } else {
                 // luma block -> 8 rows of 8 RGBA pixels
                 constexpr int yr = yrow(p);
@@ -819,8 +899,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
         if (!more) break;
         if constexpr (CP > 0) wave_lds_order(); // the tile's reads precede the next task's writes
         if constexpr (ZZ)
-#pragma unroll
-            for (int q = 0; q < NP; q++) ixc[q] = ixn[q];
+            static_for<NP>([&](auto Q) __attribute__((always_inline)) { ixc[decltype(Q)::value] = ixn[decltype(Q)::value]; });
         task = tn;
         f = fn;
         my = myn;
