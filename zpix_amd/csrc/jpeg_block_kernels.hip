@@ -939,6 +939,10 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
 #endif
 constexpr int kPlaneWavesPerEu = ZPX_PLANE_WPE; // <= 128 VGPRs: 16 waves per CU
 constexpr int kPlaneStoreAux = ZPX_PLANE_ST;
+#ifndef ZPX_PLANE_LF
+#define ZPX_PLANE_LF 1
+#endif
+constexpr bool kPlaneLf = ZPX_PLANE_LF != 0; // low-frequency tasks (lf_high)
 
 template <typename CoefT, bool ZZ = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kPlaneWavesPerEu)))
@@ -1080,10 +1084,16 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
         }
         int32_t s[64];
         typedef const __attribute__((address_space(4))) u32x4 *cq;
-        idct_block_pairs<CoefT, ZZ>(raw, [&](int r, u32x4 c) __attribute__((always_inline)) {
+        auto qrow = [&](int r, u32x4 c) __attribute__((always_inline)) {
             const u32x4 a = *reinterpret_cast<cq>(k.qp + 16 * r);
             return u32x4{pk_mul16(c[0], a[0]), pk_mul16(c[1], a[1]), pk_mul16(c[2], a[2]), pk_mul16(c[3], a[3])};
-        }, s);
+        };
+        // a task whose 64 blocks are all low-frequency (chroma, mostly)
+        // takes the short transform (lf_high)
+        if (kPlaneLf && __builtin_amdgcn_ballot_w64(lf_high<CoefT, ZZ, 4>(raw) != 0u) == 0)
+            idct_block_pairs<CoefT, ZZ, 4>(raw, qrow, s);
+        else
+            idct_block_pairs<CoefT, ZZ>(raw, qrow, s);
         const int bx = k.bx0 + lane;
         bool live = k.ok && bx < k.gw;
         if (k.rule == ZPX_BLOCKS_PROGRESSIVE) live = live && bx * k.hh < k.width && k.by * k.vv < k.height;
