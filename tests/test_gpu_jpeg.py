@@ -207,6 +207,49 @@ def _planar_random_case(rng, coeff_bits, scale, narrow, rule, h, v, mxx, myy, wi
         assert np.array_equal(got[c], want[c]), c
 
 
+@pytest.mark.parametrize("coeff_bits", [8, 16])
+def test_planar_kernel_low_frequency_tasks(coeff_bits):
+    """The low-frequency path: a task whose 64 blocks are all
+    zero outside the top-left 4x4 takes the short transform, any other the
+    full one.  Every block here is low-frequency except one outlier per task
+    at one of the 48 positions outside 4x4 (all 48 covered, per component),
+    plus all-low-frequency tasks: a mask that missed a position would send
+    its task down the short path and differ from the oracle."""
+    rng = np.random.default_rng(77 + coeff_bits)
+    mxx, myy = 70, 3
+    h, v, width, height = [2, 1, 1], [2, 1, 1], mxx * 16, myy * 16
+    outside = [r * 8 + c for r in range(8) for c in range(8) if r >= 4 or c >= 4]
+    lim = 16384 // 255
+    for rnd in range(8):
+        grids, qz = [], []
+        for c in range(3):
+            gw, gh = mxx * h[c], myy * v[c]
+            g = rng.integers(-lim, lim + 1, (gh, gw, 8, 8))
+            g[:, :, 4:, :] = 0
+            g[:, :, :, 4:] = 0
+            # one outlier in every other 64-block task; positions walk `outside`
+            tasks = [(by, x0) for by in range(gh) for x0 in range(0, gw, 64)]
+            for t, (by, x0) in enumerate(tasks):
+                if (t + rnd) % 2:
+                    continue
+                k = outside[(rnd * len(tasks) + t) % len(outside)]
+                bx = x0 + int(rng.integers(0, min(64, gw - x0)))
+                g[by, bx, k // 8, k % 8] = int(rng.integers(1, lim + 1)) * (1 if rng.random() < 0.5 else -1)
+            grids.append(g.reshape(gh * gw, 64).astype(np.int32))
+            qz.append(rng.integers(1, 256, 64).astype(np.int32))
+        qnat = []
+        for c in range(3):
+            n = np.zeros(64, np.int32)
+            n[UNZIG] = qz[c]
+            qnat.append(n)
+        got = _run_planar_grids(grids, qnat, h, v, mxx, myy, width, height, 0, coeff_bits, 1)
+        want = [np.zeros_like(p) for p in got]
+        strides = [mxx * h[c] * 8 for c in range(3)]
+        O.reconstruct_grids(3, width, height, h, v, mxx, myy, grids, qz, False, want, strides)
+        for c in range(3):
+            assert np.array_equal(got[c], want[c]), (rnd, c)
+
+
 def test_jpeg_batch_4k_fused_matches_oracle():
     """The bench workload (4096^2 4:2:0, q75) for one frame, slot-replicated."""
     data = S.jpeg_420(0, 4096, 4096)
