@@ -251,16 +251,16 @@ __device__ __forceinline__ void load_raw(const uint8_t *img, int j, u32x4 raw[Co
 }
 
 // Low-frequency blocks.  A block whose coefficients outside the top-left
-// NxN (N = 4 or 3) are all zero (at q75 every chroma block of the 4:2:0 bench frames, and
-// about half the 64-block chroma passes of 4:4:4 ones) has all-zero rows 4-7
-// after the row pass -- the reference's row pass maps a zero row to zeros
-// (idct.zig:84-97 and the full path agree there) -- so those rows are not
-// transformed, and the row pass of the others and the column pass run with
-// their inputs N-7 known zero, which hipcc folds (x + 0, 0 * c: the same
-// wrap-around values).  The test is per
-// wave (a uniform branch): lf_high() ORs the lane's coefficient words under a
-// mask of the positions outside 4x4 in the storage order (natural, or
-// zig-zag for ZPX_COEFFS_PIECES blocks).
+// NxN (N = 4 or 3) are all zero (at q75 every chroma block of the 4:2:0
+// bench frames, and about half the 64-block chroma passes of 4:4:4 ones)
+// has all-zero rows N-7 after the row pass -- the reference's row pass maps
+// a zero row to zeros (idct.zig:84-97 and the full path agree there) -- so
+// those rows are not transformed, and the row pass of the others and the
+// column pass run with their inputs N-7 known zero, which hipcc folds
+// (x + 0, 0 * c: the same wrap-around values).  The test is per wave (a
+// uniform branch): lf_high() ORs the lane's coefficient words under a mask
+// of the positions outside NxN in the storage order (natural, or zig-zag
+// for ZPX_COEFFS_PIECES blocks).
 template <typename CoefT, bool ZZ, int N>
 struct LfMask {
     static constexpr int NW = 16 * static_cast<int>(sizeof(CoefT)); // words per block
