@@ -764,10 +764,15 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                 // chroma passes: low-frequency blocks (every lane's) take the
                 // short transform (lf_high)
                 if constexpr (kJpegLf > 0 && (kind(p) == 1 || (ZPX_JPEGB_LF_INLANE && kind(p) >= 2))) {
-                    if (kJpegLf >= 2 && __builtin_amdgcn_ballot_w64(lf_high<CoefT, ZZ, 3>(raw) != 0u) == 0) {
+                    // (a chroma pass's lanes past the task's chroma blocks --
+                    // 4:1:1 / 4:1:0: lanes 32-63 -- read the descriptor array
+                    // and never reach the output: left out of the test)
+                    constexpr bool kPartial = kind(p) == 1 && (p + 1) * 64 > NCB;
+                    const bool real = !kPartial || p * 64 + lane < NCB;
+                    if (kJpegLf >= 2 && __builtin_amdgcn_ballot_w64(real && lf_high<CoefT, ZZ, 3>(raw) != 0u) == 0) {
                         idct_block_pairs<CoefT, ZZ, 3>(raw, qrow, s);
                         inlane_out();
-                    } else if (__builtin_amdgcn_ballot_w64(lf_high<CoefT, ZZ, 4>(raw) != 0u) == 0) {
+                    } else if (__builtin_amdgcn_ballot_w64(real && lf_high<CoefT, ZZ, 4>(raw) != 0u) == 0) {
                         idct_block_pairs<CoefT, ZZ, 4>(raw, qrow, s);
                         inlane_out();
                     } else {
