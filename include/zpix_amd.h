@@ -650,7 +650,11 @@ int zpx_debug_shard_fake_comm(int on);
  *                 items first (default 0: k = 4);
  *   "inflate_pair" 0: a batch worker inflates one PNG at a time (default 1:
  *                 two PNGs' inflates in one loop while the batch has more
- *                 than 2 x host_threads items left to take). */
+ *                 than 2 x host_threads items left to take);
+ *   "batch_makespan" 0: a batch worker pairs two PNGs whenever the batch
+ *                 has items to spare (default 1: only while the pair's
+ *                 estimated host time fits the batch's projected remaining
+ *                 time per worker, so late PNGs run alone). */
 int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the
  * ZPX_COEFFS_PIECES form the batch pipeline uploads and

@@ -111,7 +111,7 @@ class Pipeline {
     int run(zpx_batch_stats *stats);
 
   private:
-    void worker();
+    void worker(int w);
     int setup();
     int issue(Slot &s, bool &sync_done);
     int issue_jpeg(Slot &s, bool &sync_done);
@@ -144,13 +144,17 @@ class Pipeline {
     int tokens_ = 0;
     bool stop_ = false;
     // dispatch order of the host stage (take_item): the most expensive
-    // untaken item of the look-ahead window [front_, front_ + 2 threads_)
+    // untaken item of the look-ahead window [front_, front_ + 4 threads_)
     std::vector<double> cost_;
     std::vector<char> taken_;
     int front_ = 0, ntaken_ = 0;
+    double untaken_cost_ = 0; // sum of cost_ over the untaken items
+    // per worker, the virtual time (in host_cost_estimate's units) its
+    // current item ends at: the schedule take_item plans the pairs on
+    std::vector<double> vbusy_;
     std::vector<char> png_; // the item is a PNG (zpx_png_probe_buffer)
-    int take_item(int &remaining);
-    int take_png_partner();
+    int take_item(int w, int &remaining, int &partner);
+    int png_partner(double max_cost); // (mu_ held)
     // the dispatch window (take_item): 4 x threads items; test switch
     // "batch_lookahead" 1: item order, k >= 2: k x threads
     int lookahead_window() const
@@ -245,7 +249,7 @@ static double host_cost_estimate(const uint8_t *buf, size_t len)
     return 0;
 }
 
-// Next item for a worker: of the untaken items in the window [front_,
+// Next item for worker w: of the untaken items in the window [front_,
 // front_ + 4 threads_), the one of the largest host cost (the first of
 // equals), so the batch's long items -- a tc8 PNG's inflate is ~3x a JPEG's
 // Huffman decode, a PNG pair ~5x -- do not start last and set the end of
@@ -257,9 +261,25 @@ static double host_cost_estimate(const uint8_t *buf, size_t len)
 // most one window behind its turn, so prefix completion
 // (zpx_batch_wait_prefix) still follows item order.  -1 when none remain;
 // `remaining` = the untaken items before this one was taken.
-int Pipeline::take_item(int &remaining)
+//
+// `partner`: a second PNG whose inflate shares the worker's loop
+// (png_parse_pair: two streams' decode chains overlap, ~1.3x the work per
+// CPU second), or -1.  Only while every worker has items to spare, and only
+// while the pair -- which ends later than either PNG alone would, after
+// ~(c_i + c_j) / kPairGain -- fits the batch's projected remaining time per
+// worker: the untaken items' costs plus what the other workers' current
+// items have left, over the workers, on a virtual clock in cost units
+// (vbusy_: each worker's current item ends at its start + its cost).  So
+// once the first wave of pairs is under way, the PNGs left run one at a
+// time beside the JPEGs instead of ending the batch as a late pair (14 or
+// 15 workers on the bench's 32 PNG + 32 JPEG batch: the 2-4 PNGs left after
+// the first wave ran as one or two pairs ~120 ms after every other item was
+// done).  Test switch "batch_makespan" 0: pair whenever items are to spare.
+int Pipeline::take_item(int w, int &remaining, int &partner)
 {
+    constexpr double kPairGain = 1.3;
     std::lock_guard<std::mutex> lk(mu_);
+    partner = -1;
     while (front_ < n_ && taken_[front_]) front_++;
     if (front_ >= n_) return -1;
     // (test switch "batch_lookahead" = 1: item order)
@@ -269,28 +289,42 @@ int Pipeline::take_item(int &remaining)
     for (int i = front_; i < end; i++)
         if (!taken_[i] && (best < 0 || cost_[i] > cost_[best])) best = i;
     remaining = n_ - ntaken_;
+    const double vt = vbusy_[size_t(w)];
+    double busy = 0; // the other workers' current items, what is left of them at vt
+    for (size_t o = 0; o < vbusy_.size(); o++)
+        if (o != size_t(w)) busy += std::max(0.0, vbusy_[o] - vt);
+    const double horizon = (busy + untaken_cost_) / std::max(1, threads_);
     taken_[best] = 1;
     ntaken_++;
+    untaken_cost_ -= cost_[best];
+    double d = cost_[best];
+    const int sub = std::max(1, threads_ / std::max(1, remaining)); // (as worker())
+    if (png_[best] && sub == 1 && remaining > 2 * threads_ && depth_ >= 2 && opt(Opt::InflatePair)) {
+        const double max_partner = opt(Opt::BatchMakespan) ? kPairGain * horizon - cost_[best] : 1e300;
+        if (max_partner > 0) partner = png_partner(max_partner);
+        if (partner >= 0) d = (cost_[best] + cost_[partner]) / kPairGain;
+    }
+    vbusy_[size_t(w)] = vt + d;
     return best;
 }
 
-// A second PNG for a worker that took a PNG while every worker has items
-// to spare (inflate_pair): of the untaken PNGs in take_item's window, the
-// one of the largest host cost, else the next untaken PNG past the window
-// (taking an item early delays no prefix); -1 when none.
-int Pipeline::take_png_partner()
+// A second PNG for a pair (take_item): of the untaken PNGs in the window,
+// the one of the largest host cost, else the next untaken PNG past the
+// window (taking an item early delays no prefix) -- in both cases one whose
+// cost is at most max_cost; -1 when none.  (mu_ held)
+int Pipeline::png_partner(double max_cost)
 {
-    std::lock_guard<std::mutex> lk(mu_);
     const int win = lookahead_window();
     const int end = std::min(n_, front_ + win);
     int best = -1;
     for (int i = front_; i < end; i++)
-        if (!taken_[i] && png_[i] && (best < 0 || cost_[i] > cost_[best])) best = i;
+        if (!taken_[i] && png_[i] && cost_[i] <= max_cost && (best < 0 || cost_[i] > cost_[best])) best = i;
     for (int i = end; best < 0 && i < n_; i++)
-        if (!taken_[i] && png_[i]) best = i;
+        if (!taken_[i] && png_[i] && cost_[i] <= max_cost) best = i;
     if (best >= 0) {
         taken_[best] = 1;
         ntaken_++;
+        untaken_cost_ -= cost_[best];
     }
     return best;
 }
@@ -313,22 +347,17 @@ void Pipeline::push_decoded(std::unique_ptr<Decoded> d, double dt)
     cv_ready_.notify_one();
 }
 
-void Pipeline::worker()
+void Pipeline::worker(int w)
 {
     for (;;) {
-        int remaining = 0;
-        const int i = take_item(remaining);
+        int remaining = 0, j = -1;
+        const int i = take_item(w, remaining, j);
         if (i < 0) return;
         // threads this item may use: one while enough items remain to keep
         // every worker busy; the batch's last items split the workers that
-        // are about to go idle (parallel inflate, restart-interval Huffman)
+        // are about to go idle (parallel inflate, restart-interval Huffman).
+        // j: a second PNG inflated in the same loop (take_item)
         const int sub = std::max(1, threads_ / std::max(1, remaining));
-        // two PNGs at once while the batch keeps every worker busy: their
-        // inflates share one loop (png_parse_pair), 1.3x the work per CPU
-        // second of one stream's decode chain.  (Test switch "inflate_pair".)
-        const int j = png_[i] && sub == 1 && remaining > 2 * threads_ && depth_ >= 2 && opt(Opt::InflatePair)
-                          ? take_png_partner()
-                          : -1;
         const int need = j >= 0 ? 2 : 1;
         ZPX_TRACE("worker: took item %d%s%d (remaining %d)", i, j >= 0 ? " + " : "", j, remaining);
         {
@@ -396,7 +425,10 @@ void Pipeline::give_token()
         std::lock_guard<std::mutex> lk(mu_);
         tokens_++;
     }
-    cv_token_.notify_one();
+    // (notify_all: a worker holding a PNG pair waits for two tokens; woken
+    // alone on one token it would sleep again while a one-token waiter
+    // stayed asleep behind the free token)
+    cv_token_.notify_all();
 }
 
 int Pipeline::setup()
@@ -845,9 +877,12 @@ int Pipeline::run(zpx_batch_stats *stats)
     png_.assign(size_t(n_), 0);
     for (int i = 0; i < n_; i++) png_[i] = items_[i].format == 2;
     for (int i = 0; i < n_; i++) cost_[i] = host_cost_estimate(items_[i].buf, items_[i].len);
+    untaken_cost_ = 0;
+    for (int i = 0; i < n_; i++) untaken_cost_ += cost_[i];
+    vbusy_.assign(size_t(std::max(1, std::min(threads_, std::max(n_, 1)))), 0.0);
     if (int e = setup()) return e;
     try {
-        for (int t = 0; t < std::min(threads_, std::max(n_, 1)); t++) workers_.emplace_back([this] { worker(); });
+        for (int t = 0; t < std::min(threads_, std::max(n_, 1)); t++) workers_.emplace_back([this, t] { worker(t); });
     } catch (...) {
         return ZPX_E_OUT_OF_MEMORY;
     }

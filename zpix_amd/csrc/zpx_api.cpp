@@ -1615,11 +1615,12 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
 
 namespace zpx {
 namespace {
-// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead
-std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}};
+// JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead,
+// InflatePair, BatchMakespan
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}};
 const char *const kOptNames[static_cast<int>(Opt::Count)] = {
     "jpeg_strip",      "jpeg_sparse",     "png_pair",        "qoi_segment",     "png_device_slab",
-    "png_epoch_cycle", "shard_rccl_self", "batch_lookahead", "inflate_pair"};
+    "png_epoch_cycle", "shard_rccl_self", "batch_lookahead", "inflate_pair",    "batch_makespan"};
 } // namespace
 int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
 } // namespace zpx
