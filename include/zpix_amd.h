@@ -145,6 +145,12 @@ enum zpx_status {
 const char *zpx_error_name(int code);
 /* ZPX_ABI_VERSION of the library's build. */
 int zpx_abi_version(void);
+/* Releases the host stages' recycled buffers -- the PNG IDAT buffers and the
+ * parallel inflate's symbol buffers, which a batch of large PNGs leaves
+ * pooled (up to ~2 x host threads and 64 buffers, 2 GiB and 1 GiB at most)
+ * for the next batch to reuse with their pages -- and returns the bytes
+ * released.  Safe at any time; buffers in use are not touched. */
+size_t zpx_host_pools_trim(void);
 /* Detail message of the last failure on this context (never NULL). */
 const char *zpx_last_error(const zpx_ctx *ctx);
 

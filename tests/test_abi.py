@@ -791,3 +791,25 @@ def test_host_entropy_progressive_parallel_matches_oracle():
         for c in range(oc.n_comp):
             if oc.grids[c] is not None:
                 assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32)), (it, c)
+
+
+def test_host_pools_trim():
+    """zpx_host_pools_trim releases the host stages' recycled buffers: after
+    a PNG parse the IDAT buffer is pooled (reused by the next parse with its
+    pages), after a parallel inflate the symbol buffers; a trim returns
+    their bytes, a second trim 0, and decoding afterwards is unchanged."""
+    L = _lib.lib()
+    L.zpx_host_pools_trim()
+    data = S.png_tc8_mixed(3, 300, 200)
+    rc, frame, got = _png_single(data)
+    assert rc == 0
+    assert L.zpx_host_pools_trim() > 0
+    assert L.zpx_host_pools_trim() == 0
+    rng = np.random.default_rng(5)
+    raw = (128 + rng.normal(0, 12, 3_000_000)).clip(0, 255).astype(np.uint8).tobytes()
+    z = _zstream(raw, 6, 0)
+    out = np.zeros(len(raw) + 64, np.uint8)
+    if _lib.lib().zpx_debug_inflate_parallel(z, len(z), out.ctypes.data, len(raw), 4):
+        assert out[:len(raw)].tobytes() == raw
+        assert L.zpx_host_pools_trim() > 0
+    assert _png_single(data) == (rc, frame, got)

@@ -68,20 +68,26 @@ def test_batch_device_dst(threads, depth):
     check_results(bufs, res)
 
 
-@pytest.mark.parametrize("pair", [0, 1])
-def test_batch_inflate_pair_switch(pair):
+@pytest.mark.parametrize("pair,makespan", [(0, 1), (1, 1), (1, 0)])
+def test_batch_inflate_pair_switch(pair, makespan):
     """Workers inflating two PNGs in one loop ("inflate_pair", the default)
     or one at a time give the oracle's results, with a token budget of two
-    (a pair takes both) and malformed PNGs among the pairs."""
+    (a pair takes both) and malformed PNGs among the pairs; with the pairs
+    planned against the batch's remaining time ("batch_makespan", the
+    default: PNGs of very different sizes, so late ones run alone) or formed
+    whenever items are to spare."""
     L = _lib.lib()
     prev = L.zpx_debug_option(b"inflate_pair", pair)
+    prev_m = L.zpx_debug_option(b"batch_makespan", makespan)
     try:
         bufs = mixed_buffers() + [S.png_tc8_mixed(20 + i, 257 + i, 129) for i in range(12)]
         bufs += [S.png_tc8_mixed(40, 64, 64)[:-30], S.png_generic(41, 99, 77, 16, 2)]
-        res = batch.decode_rgba(bufs, host_threads=2, depth=2)
+        bufs += [S.png_tc8_mixed(60 + i, 700 if i % 3 == 0 else 90, 300) for i in range(9)]
+        res = batch.decode_rgba(bufs, host_threads=3, depth=3)
         check_results(bufs, res)
     finally:
         L.zpx_debug_option(b"inflate_pair", prev)
+        L.zpx_debug_option(b"batch_makespan", prev_m)
 
 
 def test_batch_host_dst():

@@ -348,7 +348,8 @@ template <typename T> using RawVec = std::vector<T, NoInitAlloc<T>>;
 
 // The speculative chunks' symbol buffers, recycled: 8 MB a chunk, zeroed and
 // page-faulted in on every call when they were fresh vectors (at most
-// 1 GiB held)
+// 1 GiB and 64 buffers held -- the chunks of 8 concurrent 8-thread
+// inflates; inflate_pool_trim releases them)
 class SymPool {
   public:
     RawVec<uint16_t> take()
@@ -362,10 +363,20 @@ class SymPool {
     }
     void give(RawVec<uint16_t> &&v)
     {
+        RawVec<uint16_t> keep = std::move(v); // (freed on return unless pooled)
         std::lock_guard<std::mutex> lk(mu_);
-        if (v.capacity() == 0 || held_ + v.capacity() * 2 > (size_t(1) << 30)) return;
-        held_ += v.capacity() * 2;
-        free_.push_back(std::move(v));
+        if (keep.capacity() == 0 || held_ + keep.capacity() * 2 > (size_t(1) << 30) || free_.size() >= 64) return;
+        held_ += keep.capacity() * 2;
+        free_.push_back(std::move(keep));
+    }
+    size_t trim()
+    {
+        std::vector<RawVec<uint16_t>> gone;
+        std::lock_guard<std::mutex> lk(mu_);
+        const size_t n = held_;
+        gone.swap(free_);
+        held_ = 0;
+        return n;
     }
 
   private:
@@ -1086,5 +1097,7 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
     *produced = want;
     return true;
 }
+
+size_t inflate_pool_trim() { return sym_pool().trim(); }
 
 } // namespace zpx

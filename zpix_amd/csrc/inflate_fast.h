@@ -16,4 +16,6 @@ bool inflate_parallel(const uint8_t *in, size_t in_len, uint8_t *out, size_t wan
 // ok[k] and produced[k] are inflate_fast's result for stream k.
 void inflate_fast_pair(const uint8_t *const in[2], const size_t in_len[2], uint8_t *const out[2], const size_t want[2],
                        size_t produced[2], bool ok[2]);
+// Releases inflate_parallel's recycled symbol buffers; the bytes released.
+size_t inflate_pool_trim();
 }

@@ -79,7 +79,10 @@ int inflate_zlib(const std::vector<uint8_t> &z, uint8_t *dst, size_t total, size
 // Reused buffers for the concatenated IDAT data: a fresh 40 MB vector per
 // 4K image cost a page fault per 4 KiB page on its first touch (the IDAT
 // copy ran at 1.5 GB/s into fresh pages, ~25 ms of a ~220 ms parse here);
-// recycled ones keep their pages.  Bounded: at most kZPoolBytes held.
+// recycled ones keep their pages.  Bounded: at most kZPoolBytes held, and
+// at most as many buffers as the batch pipeline's parsers can have in use
+// at once (two per host worker, min(16, budget) workers: host_cpus.h) -- the
+// working set of the busiest batch, which zpx_host_pools_trim() releases.
 class ZPool {
   public:
     std::vector<uint8_t> take()
@@ -93,11 +96,22 @@ class ZPool {
     }
     void give(std::vector<uint8_t> &&v)
     {
-        v.clear();
+        static const size_t kMaxFree = 2 * size_t(std::min(16, host_cpu_budget())) + 2;
+        std::vector<uint8_t> keep = std::move(v); // (freed on return unless pooled)
+        keep.clear();
         std::lock_guard<std::mutex> lk(mu_);
-        if (v.capacity() == 0 || held_ + v.capacity() > kZPoolBytes) return;
-        held_ += v.capacity();
-        free_.push_back(std::move(v));
+        if (keep.capacity() == 0 || held_ + keep.capacity() > kZPoolBytes || free_.size() >= kMaxFree) return;
+        held_ += keep.capacity();
+        free_.push_back(std::move(keep));
+    }
+    size_t trim() // the bytes released
+    {
+        std::vector<std::vector<uint8_t>> gone;
+        std::lock_guard<std::mutex> lk(mu_);
+        const size_t n = held_;
+        gone.swap(free_);
+        held_ = 0;
+        return n;
     }
 
   private:
@@ -503,6 +517,8 @@ int Parser::run(bool header_only)
 }
 
 } // namespace
+
+size_t png_pool_trim() { return zpool().trim() + inflate_pool_trim(); }
 
 int png_inflate_threads()
 {

@@ -55,6 +55,9 @@ int png_parse_pair(const uint8_t *const buf[2], const size_t len[2], PngStream *
 // default inflate threads of the single-image entry points: ZPX_INFLATE_THREADS,
 // else min(8, hardware threads)
 int png_inflate_threads();
+// Releases the host stages' recycled buffers (the IDAT pool here, the
+// parallel inflate's symbol pool): the bytes released (zpx_host_pools_trim)
+size_t png_pool_trim();
 
 // Signature + IHDR only (dimensions of the image png.decode would return).
 int png_decode_config(const uint8_t *buf, size_t len, uint32_t &w, uint32_t &h);

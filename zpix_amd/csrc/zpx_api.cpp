@@ -36,6 +36,7 @@ static const char *const kErrorNames[] = {
 };
 
 extern "C" int zpx_abi_version(void) { return ZPX_ABI_VERSION; }
+extern "C" size_t zpx_host_pools_trim(void) { return zpx::png_pool_trim(); }
 
 extern "C" const char *zpx_error_name(int code)
 {
