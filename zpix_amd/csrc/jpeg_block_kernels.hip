@@ -947,6 +947,9 @@ constexpr int kPlaneStoreAux = ZPX_PLANE_ST;
 #ifndef ZPX_PLANE_LF
 #define ZPX_PLANE_LF 1
 #endif
+#ifndef ZPX_PLANE_ZZ_NT
+#define ZPX_PLANE_ZZ_NT 0
+#endif
 constexpr bool kPlaneLf = ZPX_PLANE_LF != 0; // low-frequency tasks (lf_high)
 
 template <typename CoefT, bool ZZ = false>
@@ -1034,7 +1037,7 @@ void jpeg_plane_block_kernel(const DevJpegFrame *__restrict__ frames, PlaneTaskG
             // (cached, not non-temporal: the lines a task fetches also hold
             // the pieces of the MCU row's other blocks, which its
             // neighbouring tasks read soon after)
-            glds16<false>(pz + static_cast<size_t>(piece) * 16, cimg + 1024 * i);
+            glds16<ZPX_PLANE_ZZ_NT != 0>(pz + static_cast<size_t>(piece) * 16, cimg + 1024 * i);
         }
     };
     int task;
@@ -1244,7 +1247,10 @@ int launch_jpeg_plane_block(const DevJpegFrame *d_frames, int n_frames, const Jp
 #ifndef ZPX_PLANE_WPCU16
 #define ZPX_PLANE_WPCU16 8
 #endif
-    const int resident = coeff_bits == 8 ? (pieces ? resident8z : resident8)
+#ifndef ZPX_PLANE_WPCU8Z
+#define ZPX_PLANE_WPCU8Z 64
+#endif
+    const int resident = coeff_bits == 8 ? (pieces ? std::min(resident8z, device_cu_count() * ZPX_PLANE_WPCU8Z) : resident8)
                                          : std::min(pieces ? resident16z : resident16, device_cu_count() * ZPX_PLANE_WPCU16);
     const int grid = total < resident ? static_cast<int>(total) : resident;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(64), 0, stream, d_frames, geo);

@@ -308,26 +308,55 @@ bool JpegPieces::widen()
     uint8_t *o = static_cast<uint8_t *>(nd.ptr);
     const int8_t *src = static_cast<const int8_t *>(data.ptr);
     memset(o, 0, 16);
-    size_t n = 1;
-    uint32_t *ix = static_cast<uint32_t *>(index.ptr);
-    size_t total = 0;
-    for (int c = 0; c < 4; c++) total = std::max(total, first[c] + blocks[c]);
-    for (size_t k = 0; k < total; k++) {
-        if (ix[k] == 0) continue;
-        const int8_t *v = src + size_t(ix[k] >> 4) * 16;
-        int eob = static_cast<int>(ix[k] & 15) * 16;
-        while (eob > 0 && v[eob - 1] == 0) eob--;
-        const size_t np = static_cast<size_t>((eob + 7) / 8);
-        if (n + np > cap) return false;
-        int16_t *d = reinterpret_cast<int16_t *>(o + n * 16);
-        for (size_t z = 0; z < np * 8; z++) d[z] = static_cast<int16_t>(z < size_t(eob) ? v[z] : 0);
-        ix[k] = np ? static_cast<uint32_t>(n << 4 | np) : 0u;
-        n += np;
+    size_t nx[kMaxStreams];
+    for (int s = 0; s < nstreams; s++) nx[s] = base[s];
+    for (int c = 0; c < 4; c++) {
+        if (blocks[c] == 0) continue;
+        uint32_t *ix = index_of(c);
+        for (size_t k = 0; k < blocks[c]; k++) {
+            if (ix[k] == 0) continue;
+            const int8_t *v8 = src + size_t(ix[k] >> 4) * 16;
+            int eob = static_cast<int>(ix[k] & 15) * 16;
+            while (eob > 0 && v8[eob - 1] == 0) eob--;
+            const size_t np = static_cast<size_t>((eob + 7) / 8);
+            size_t &n = nx[stream_of(c, k)];
+            if (n + np > cap) return false;
+            int16_t *d = reinterpret_cast<int16_t *>(o + n * 16);
+            for (size_t z = 0; z < np * 8; z++) d[z] = static_cast<int16_t>(z < size_t(eob) ? v8[z] : 0);
+            ix[k] = np ? static_cast<uint32_t>(n << 4 | np) : 0u;
+            n += np;
+        }
     }
     data = static_cast<HostBuf &&>(nd);
-    npieces = n;
+    for (int s = 0; s < nstreams; s++) next[s] = nx[s];
     bits = 16;
     return true;
+}
+
+void JpegPieces::compact()
+{
+    uint8_t *d = static_cast<uint8_t *>(data.ptr);
+    size_t at = 1, shift[kMaxStreams];
+    for (int s = 0; s < nstreams; s++) {
+        const size_t n = next[s] - base[s];
+        shift[s] = base[s] - at;
+        if (shift[s] && n) memmove(d + at * 16, d + base[s] * 16, n * 16);
+        base[s] = at;
+        next[s] = at + n;
+        at += n;
+    }
+    for (int c = 0; c < 4; c++) {
+        if (blocks[c] == 0) continue;
+        uint32_t *ix = index_of(c);
+        const size_t rows = blocks[c] / gw[c];
+        for (size_t by = 0; by < rows; by++) {
+            const uint32_t d = static_cast<uint32_t>(shift[s0[c] + static_cast<int>(by % size_t(v[c]))] << 4);
+            uint32_t *row = ix + by * gw[c];
+            if (d)
+                for (size_t k = 0; k < gw[c]; k++) row[k] -= row[k] ? d : 0u;
+        }
+    }
+    npieces = at;
 }
 
 // ---------------------------------------------------------------- decoder
@@ -591,7 +620,8 @@ class Decoder {
                 return 0;
             }
             const int eob = kZigOf.z[pos[n - 1]] + 1;
-            uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + p.npieces * 16;
+            size_t &cur = p.next[p.stream_of(ci, blk)];
+            uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + cur * 16;
             size_t np;
             if (p.bits == 8) { // (the whole 64-byte block cleared: the data has that slack)
                 np = static_cast<size_t>((eob + 15) >> 4);
@@ -605,8 +635,8 @@ class Decoder {
                     memcpy(d + 2 * kZigOf.z[pos[i]], &v, 2);
                 }
             }
-            ix = static_cast<uint32_t>(p.npieces << 4 | np);
-            p.npieces += np;
+            ix = static_cast<uint32_t>(cur << 4 | np);
+            cur += np;
             return 0;
         }
     };
@@ -790,7 +820,7 @@ class Decoder {
     // from there, with no natural-order block or position list in between
     template <class R>
     __attribute__((always_inline)) int first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
-                                                          int32_t &dcv, JpegPieces &p, int ci, size_t blk,
+                                                          int32_t &dcv, JpegPieces &p, int ci, size_t blk, int yy,
                                                           int32_t *zz);
     template <class Sink>
     int mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, int32_t *dc, int32_t *b, uint8_t *nzpos,
@@ -1162,11 +1192,22 @@ int Decoder::sos(int32_t n)
         // (+8 pieces: a block's writes clear its whole dense extent)
         if (!pc.index.alloc(nblocks * sizeof(uint32_t), true) || !pc.data.alloc((cap + 8) * 16, false))
             return ZPX_E_OUT_OF_MEMORY;
-        size_t first = 0;
+        size_t first = 0, sb = 1;
+        pc.nstreams = 0;
         for (int c = 0; c < o_.n_comp; c++) {
             pc.first[c] = first;
             pc.blocks[c] = size_t(mxx) * size_t(myy) * size_t(o_.comp[c].h * o_.comp[c].v);
             first += pc.blocks[c];
+            // streams of the component: its block rows mod v (JpegPieces),
+            // each with room for 8 pieces (int16) per block
+            pc.s0[c] = pc.nstreams;
+            pc.v[c] = o_.comp[c].v;
+            pc.gw[c] = size_t(mxx) * size_t(o_.comp[c].h);
+            for (int yy = 0; yy < pc.v[c]; yy++) {
+                pc.base[pc.nstreams] = pc.next[pc.nstreams] = sb;
+                sb += 8 * (pc.blocks[c] / size_t(pc.v[c]));
+                pc.nstreams++;
+            }
         }
         memset(pc.data.ptr, 0, 16); // piece 0
         pc.cap = cap;
@@ -1326,7 +1367,7 @@ int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
 
 template <class R>
 int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huff &hac, int32_t &dcv, JpegPieces &p,
-                                int ci, size_t blk, int32_t *zz)
+                                int ci, size_t blk, int yy, int32_t *zz)
 {
     const int32_t ze = sc.ze, al = sc.al;
     int32_t zig = sc.zs;
@@ -1392,7 +1433,8 @@ int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huf
             ix = 0;
         } else {
             const int eob = last + 1;
-            uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + p.npieces * 16;
+            size_t &cur = p.next[p.s0[ci] + yy];
+            uint8_t *d = static_cast<uint8_t *>(p.data.ptr) + cur * 16;
             size_t np;
             if (p.bits == 8) {
                 np = static_cast<size_t>((eob + 15) >> 4);
@@ -1406,8 +1448,8 @@ int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huf
                         memcpy(d + 16 * k + 2 * j, &v, 2);
                     }
             }
-            ix = static_cast<uint32_t>(p.npieces << 4 | np);
-            p.npieces += np;
+            ix = static_cast<uint32_t>(cur << 4 | np);
+            cur += np;
         }
     }
     for (int i = 0; i <= last; i++) zz[i] = 0;
@@ -1425,7 +1467,8 @@ int Decoder::mcu_pieces_with(R &r, const Scan &sc, int32_t my, int32_t mx, int32
         const Huff &hac = huff_[1][sc.c[k].ta];
         for (int32_t j = 0; j < hi * vi; j++) {
             const int32_t bx = hi * mx + j % hi, by = vi * my + j / hi;
-            ZTRY(first_block_pieces(r, sc, hdc, hac, dc[ci], p, ci, size_t(by) * size_t(mxx * hi) + size_t(bx), zz));
+            // (the block's stream: its block row mod v = j / hi, JpegPieces)
+            ZTRY(first_block_pieces(r, sc, hdc, hac, dc[ci], p, ci, size_t(by) * size_t(mxx * hi) + size_t(bx), j / hi, zz));
         }
     }
     return 0;
@@ -1483,11 +1526,11 @@ int Decoder::mcu(const Scan &sc, int32_t my, int32_t mx, int32_t &block_count, i
                     int e;
                     if (len_ - pos_ >= kFastSlack) {
                         FastBits fb(*this);
-                        e = first_block_pieces(fb, sc, hdc, hac, dc[ci], sink.p, ci, blk, b);
+                        e = first_block_pieces(fb, sc, hdc, hac, dc[ci], sink.p, ci, blk, by % vi, b);
                         fb.sync();
                     } else {
                         MemberBits mb{*this};
-                        e = first_block_pieces(mb, sc, hdc, hac, dc[ci], sink.p, ci, blk, b);
+                        e = first_block_pieces(mb, sc, hdc, hac, dc[ci], sink.p, ci, blk, by % vi, b);
                     }
                     if (e) return e;
                     continue;
@@ -2047,7 +2090,10 @@ int jpeg_entropy_decode(const uint8_t *buf, size_t len, JpegCoeffs &out, int thr
             e = d.run();
         }
         if (e) return e;
-        if (out.pieces.valid) return ZPX_OK;
+        if (out.pieces.valid) {
+            out.pieces.compact();
+            return ZPX_OK;
+        }
         // one width per frame (the kernels take one coefficient type per frame)
         int bits = 8;
         for (int i = 0; i < 4; i++)

@@ -103,17 +103,35 @@ class CoeffGrid {
 // grids expanded from them on the device (launch_jpeg_pieces_expand).
 // The width starts at int8 and is widened (every piece so far copied) the
 // first time a value does not fit.
+//
+// Pieces are stored per block row class: stream (c, yy) holds the pieces of
+// component c's blocks in block rows by with by mod v_c == yy, in grid order
+// (for 4:2:0: Y's even block rows, Y's odd block rows, Cb, Cr).  So the 64
+// blocks a kernel task reads from one block row of one component have their
+// pieces in one contiguous span, as a dense grid's 64 blocks are -- not
+// spread over the MCU row between the other rows' and components' pieces,
+// as decode order leaves them.  While decoding, stream s fills its own
+// region [base[s], base[s] + 8 x its blocks) of the allocation; compact()
+// closes the gaps once the scan is done (a memmove of the streams after the
+// first and one pass over the index words).
 struct JpegPieces {
+    static constexpr int kMaxStreams = 16;
     bool valid = false;
     int bits = 8;                 // 8 or 16: the values of every piece
     HostBuf data;                 // npieces x 16 bytes
     HostBuf index;                // u32 per block: component c's blocks from first[c]
     size_t first[4] = {0, 0, 0, 0}, blocks[4] = {0, 0, 0, 0};
-    size_t npieces = 0, cap = 0;  // pieces written / allocated
+    size_t npieces = 0, cap = 0;  // pieces (after compact()) / allocated
     int32_t max_abs[4] = {0, 0, 0, 0};
+    // streams: component c's are s0[c] .. s0[c] + v[c] - 1 (block row mod v[c])
+    int nstreams = 0, s0[4] = {0, 0, 0, 0}, v[4] = {1, 1, 1, 1};
+    size_t gw[4] = {1, 1, 1, 1};  // component c's grid width in blocks
+    size_t base[kMaxStreams] = {}, next[kMaxStreams] = {};
+    int stream_of(int c, size_t blk) const { return s0[c] + static_cast<int>((blk / gw[c]) % size_t(v[c])); }
     size_t data_bytes() const { return npieces * 16; }
     uint32_t *index_of(int c) const { return static_cast<uint32_t *>(index.ptr) + first[c]; }
     bool widen(); // int8 -> int16 pieces
+    void compact(); // the streams back to back from piece 1; sets npieces
 };
 
 struct JpegCoeffs {

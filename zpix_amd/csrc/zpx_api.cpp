@@ -1669,6 +1669,9 @@ extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, i
                                         35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                         58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
         const int per = p.bits == 8 ? 16 : 8;
+        // every piece but piece 0 belongs to exactly one block (the streams
+        // compacted back to back, JpegPieces::compact)
+        std::vector<uint8_t> owner(p.npieces, 0);
         int32_t *o = grids;
         for (int ci = 0; ci < c.n_comp; ci++) {
             const uint32_t *ix = p.index_of(ci);
@@ -1680,6 +1683,8 @@ extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, i
                     continue;
                 }
                 if (first == 0 || first + np > p.npieces || np * static_cast<uint32_t>(per) > uint32_t(64 + per - 1)) return -int64_t(ZPX_E_PANIC);
+                for (uint32_t q = 0; q < np; q++)
+                    if (owner[first + q]++) return -int64_t(ZPX_E_PANIC);
                 for (uint32_t z = 0; z < np * per && z < 64; z++) {
                     int32_t v;
                     if (p.bits == 8) {
@@ -1693,6 +1698,8 @@ extern "C" int64_t zpx_debug_jpeg_sparse_grids(const uint8_t *buf, size_t len, i
                 }
             }
         }
+        for (size_t q = 1; q < p.npieces; q++)
+            if (!owner[q]) return -int64_t(ZPX_E_PANIC);
         return int64_t(blocks);
     });
 }
