@@ -603,10 +603,9 @@ def test_bmp_header_errors_match_oracle():
         assert _lib.error_name(code) == e.value.name, data[:32]
 
 
-def _sparse_grids(data: bytes):
+def _sparse_grids(data: bytes, cap: int = 1 << 22):
     import ctypes as C
 
-    cap = 1 << 22
     out = np.zeros(cap, np.int32)
     n = _lib.lib().zpx_debug_jpeg_sparse_grids(data, len(data), out.ctypes.data, cap)
     return n, out
@@ -813,3 +812,31 @@ def test_host_pools_trim():
         assert out[:len(raw)].tobytes() == raw
         assert L.zpx_host_pools_trim() > 0
     assert _png_single(data) == (rc, frame, got)
+
+
+def test_jpeg_pieces_fixture_geometries():
+    """Pieces of every baseline interleaved fixture, whatever its sampling
+    (4:1:0, 4:1:1, 4:4:0, 2x2 luma with 1x2 chroma, ...): the per (component,
+    block row mod v) streams (JpegPieces) compacted back to back -- every
+    piece owned by exactly one block, checked by the hook -- expand to the
+    oracle's coefficient grids."""
+    import glob
+
+    seen = 0
+    for path in sorted(glob.glob(golden("testdata", "*.jp*g"))):
+        data = open(path, "rb").read()
+        try:
+            c = O.jpeg_coefficients(data)
+        except O.OracleError:
+            continue
+        n, flat = _sparse_grids(data, 1 << 24)
+        if n <= 0:  # grids, not pieces (progressive, one component, restart-parallel...)
+            continue
+        seen += 1
+        off = 0
+        for i, g in enumerate(c.grids):
+            g = np.asarray(g, np.int32).reshape(-1)
+            assert np.array_equal(flat[off:off + g.size], g), (path, i)
+            off += g.size
+        assert n * 64 == off, path
+    assert seen >= 10
