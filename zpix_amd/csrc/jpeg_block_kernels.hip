@@ -96,6 +96,9 @@ constexpr int kStoreAux = 2; // nt
 #define ZPX_JPEGB_LF_INLANE 0
 #endif
 constexpr int kJpegLf = ZPX_JPEGB_LF;
+#ifndef ZPX_JPEGB_LF_PARTIAL // (A/B knob: 0 lets 4:1:1's empty chroma lanes vote)
+#define ZPX_JPEGB_LF_PARTIAL 1
+#endif
 
 // Samples stay in the signed domain (sample - 128, the IDCT's clamp range
 // before its level shift): the +128 costs nothing folded into the colour
@@ -767,7 +770,7 @@ void jpeg_block_kernel(const DevJpegFrame *__restrict__ frames, int tasks_x, int
                     // (a chroma pass's lanes past the task's chroma blocks --
                     // 4:1:1 / 4:1:0: lanes 32-63 -- read the descriptor array
                     // and never reach the output: left out of the test)
-                    constexpr bool kPartial = kind(p) == 1 && (p + 1) * 64 > NCB;
+                    constexpr bool kPartial = ZPX_JPEGB_LF_PARTIAL && kind(p) == 1 && (p + 1) * 64 > NCB;
                     const bool real = !kPartial || p * 64 + lane < NCB;
                     if (kJpegLf >= 2 && __builtin_amdgcn_ballot_w64(real && lf_high<CoefT, ZZ, 3>(raw) != 0u) == 0) {
                         idct_block_pairs<CoefT, ZZ, 3>(raw, qrow, s);

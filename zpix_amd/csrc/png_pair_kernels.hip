@@ -79,6 +79,12 @@ typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 template <typename T> __device__ __forceinline__ ZPX_GLOBAL T *gptr(gu8 *p) { return reinterpret_cast<ZPX_GLOBAL T *>(p); }
 
 constexpr int kG = 8; // steps per group (input burst)
+#ifndef ZPX_A7_NOLOAD
+#define ZPX_A7_NOLOAD 0
+#endif
+#ifndef ZPX_A7_NT
+#define ZPX_A7_NT 0
+#endif
 constexpr int kSleep = 2; // s_sleep between boundary polls (units of 64 cycles; 0 / 1 measured equal)
 
 template <int DEPTH> struct PairTraits;
@@ -268,8 +274,17 @@ __device__ __forceinline__ v4u a7_chunk(const A7Src &a, uint32_t k, uint32_t y)
     const uint8_t *pa = s5 ? a.s5 + row * a.s5stride + static_cast<uint64_t>(X0) * OBPX
                            : a.q2 + row * a.q2stride + static_cast<uint64_t>(X0 >> 1) * OBPX;
     const uint8_t *pb = s5 ? pa + 8 : a.s4 + row * a.s4stride + static_cast<uint64_t>(X0 >> 1) * OBPX;
+#if ZPX_A7_NOLOAD // (timing-only A/B: the merge without its staged loads; wrong pixels)
+    (void)pa;
+    (void)pb;
+    const v2u va{k, y}, vb{y, k};
+#elif ZPX_A7_NT
+    const v2u va = __builtin_nontemporal_load(reinterpret_cast<const ZPX_GLOBAL v2u *>((const ZPX_GLOBAL uint8_t *)pa));
+    const v2u vb = __builtin_nontemporal_load(reinterpret_cast<const ZPX_GLOBAL v2u *>((const ZPX_GLOBAL uint8_t *)pb));
+#else
     const v2u va = *reinterpret_cast<const ZPX_GLOBAL v2u *>((const ZPX_GLOBAL uint8_t *)pa);
     const v2u vb = *reinterpret_cast<const ZPX_GLOBAL v2u *>((const ZPX_GLOBAL uint8_t *)pb);
+#endif
     if constexpr (OBPX == 8) return v4u{va[0], va[1], vb[0], vb[1]};
     else return s5 ? v4u{va[0], va[1], vb[0], vb[1]} : v4u{va[0], vb[0], va[1], vb[1]}; // Q2 / S4 alternate
 }
