@@ -379,11 +379,22 @@ struct ZigOf {
 };
 constexpr ZigOf kZigOf{};
 
+// AC symbols whose code (<= 8 bits) and magnitude bits fit the next
+// kAcFastBits bits of the stream, decoded by one lookup (Huff::ac): entry =
+// bits used (0: not here) | kAcEob | run << 8 | value << 16 (the extended
+// coefficient, receiveExtend's).  A baseline q75 frame's AC codes are
+// mostly 2-8 bits with 1-3 magnitude bits.
+#ifndef ZPX_HUFF_FAST_BITS
+#define ZPX_HUFF_FAST_BITS 11
+#endif
+constexpr int kAcFastBits = ZPX_HUFF_FAST_BITS;
+constexpr uint32_t kAcEob = 16;
 struct Huff { // HuffTable.zig
     int32_t num_codes = 0;
     uint16_t lut[256] = {};
     uint8_t vals[256] = {};
     int32_t min_codes[16] = {}, max_codes[16] = {}, vals_indices[16] = {};
+    uint32_t ac[1u << kAcFastBits] = {}; // (dht; DC tables: the difference, run 0)
 };
 
 // internal status: the frame does not fit the pieces (jpeg_entropy_decode
@@ -669,6 +680,9 @@ class Decoder {
     static constexpr size_t kFastSlack = 2048; // > any block's entropy-coded bytes (64 x 27 bits, stuffed x2)
     struct MemberBits {
         Decoder &d;
+        static constexpr bool kAcFast = false;
+        uint32_t peek_ac(const Huff &) { return 0; }
+        void take_ac(uint32_t) {}
         int huffman(const Huff &h, uint8_t &out) { return d.huffman(h, out); }
         int receive_extend(uint8_t t, int32_t &out) { return d.receive_extend(t, out); }
         int bits(int32_t n, uint32_t &out) { return d.bits(n, out); }
@@ -685,6 +699,23 @@ class Decoder {
         size_t pos0 = 0;
         size_t unread0 = 0;
         explicit FastBits(Decoder &dd) : d(dd), src(dd.src_) { load(); }
+        static constexpr bool kAcFast = true;
+        // the combined AC entry (Huff::ac) of the next bits, 0 when they are
+        // not all buffered (a marker or the input's end ahead: the symbol
+        // path then reads them the reference's way)
+        __attribute__((always_inline)) uint32_t peek_ac(const Huff &h)
+        {
+            if (avail < kAcFastBits) refill();
+            return avail >= kAcFastBits ? h.ac[acc >> (64 - kAcFastBits)] : 0u;
+        }
+        // consume it: the reference's huffman ensures 8 bits, then
+        // receiveExtend its magnitude bits (need(8), need(size))
+        __attribute__((always_inline)) void take_ac(uint32_t e)
+        {
+            const int tot = static_cast<int>(e & 15);
+            H = std::max(H, C + std::max(8, tot));
+            consume(tot);
+        }
         __attribute__((always_inline)) void sync()
         {
             const int32_t k = H > bn0 ? (H - bn0 + 7) >> 3 : 0;
@@ -1019,6 +1050,55 @@ int Decoder::dht(int32_t n)
                 }
             }
         }
+        // the combined AC table (Huff::ac): codes of <= 8 bits, their
+        // symbol's magnitude bits with them when both fit kAcFastBits
+        memset(h.ac, 0, sizeof(h.ac));
+        if (tc == 0) { // DC: the difference's size t and its t bits (run 0, never kAcEob)
+            uint32_t c2 = 0;
+            int v2 = 0;
+            for (int len = 1; len <= 8; len++) {
+                c2 <<= 1;
+                for (int j = 0; j < count[len - 1]; j++, c2++, v2++) {
+                    const int size = h.vals[v2];
+                    const int tot = len + size;
+                    if (size > 16 || tot > kAcFastBits) continue; // (t > 16: ExcessiveDCComponent, the symbol path)
+                    for (uint32_t x = 0; x < (1u << size); x++) {
+                        int32_t v = static_cast<int32_t>(x);
+                        if (size > 0 && v < (int32_t(1) << (size - 1))) v += static_cast<int32_t>(0xffffffffu << size) + 1;
+                        const uint32_t e = static_cast<uint32_t>(tot) | static_cast<uint32_t>(v) << 16;
+                        const uint32_t base = ((c2 << size) | x) << (kAcFastBits - tot);
+                        for (uint32_t k = 0; k < (1u << (kAcFastBits - tot)); k++)
+                            if ((base | k) < (1u << kAcFastBits)) h.ac[base | k] = e;
+                    }
+                }
+            }
+        } else {
+            uint32_t c2 = 0;
+            int v2 = 0;
+            for (int len = 1; len <= 8; len++) {
+                c2 <<= 1;
+                for (int j = 0; j < count[len - 1]; j++, c2++, v2++) {
+                    const uint8_t sym = h.vals[v2];
+                    const int size = sym & 15, run = sym >> 4;
+                    if (size == 0 && run != 0) continue; // ZRL, EOBn: the symbol path
+                    const int tot = len + size;
+                    if (tot > kAcFastBits) continue;
+                    for (uint32_t x = 0; x < (1u << size); x++) {
+                        uint32_t e = static_cast<uint32_t>(tot) | static_cast<uint32_t>(run) << 8;
+                        if (size == 0) {
+                            e |= kAcEob;
+                        } else { // receiveExtend (decoder.zig:975-991) of the magnitude bits x
+                            int32_t v = static_cast<int32_t>(x);
+                            if (v < (int32_t(1) << (size - 1))) v += static_cast<int32_t>(0xffffffffu << size) + 1;
+                            e |= static_cast<uint32_t>(v) << 16;
+                        }
+                        const uint32_t base = ((c2 << size) | x) << (kAcFastBits - tot);
+                        for (uint32_t k = 0; k < (1u << (kAcFastBits - tot)); k++)
+                            if ((base | k) < (1u << kAcFastBits)) h.ac[base | k] = e;
+                    }
+                }
+            }
+        }
         int32_t cb = 0, idx = 0;
         for (int i = 0; i < 16; i++) {
             if (count[i] == 0) {
@@ -1324,11 +1404,18 @@ int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
     int32_t zig = sc.zs;
     if (zig == 0) {
         zig++;
-        uint8_t t;
-        ZTRY(r.huffman(hdc, t));
-        if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
         int32_t delta;
-        ZTRY(r.receive_extend(t, delta));
+        uint32_t e = 0;
+        if constexpr (R::kAcFast) e = r.peek_ac(hdc); // (the DC difference in one lookup)
+        if (e & 15) {
+            r.take_ac(e);
+            delta = static_cast<int32_t>(e) >> 16;
+        } else {
+            uint8_t t;
+            ZTRY(r.huffman(hdc, t));
+            if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+            ZTRY(r.receive_extend(t, delta));
+        }
         dcv += delta;
         b[0] = dcv << al;
         nzpos[nnz++] = 0;
@@ -1338,6 +1425,22 @@ int Decoder::first_block(R &r, const Scan &sc, const Huff &hdc, const Huff &hac,
         return 0;
     }
     for (; zig <= ze; zig++) {
+        if constexpr (R::kAcFast) { // one lookup: code and magnitude bits (Huff::ac)
+            const uint32_t e = r.peek_ac(hac);
+            if (e & kAcEob) {
+                r.take_ac(e);
+                eob_run_ = 0; // (1 << 0) - 1
+                break;
+            }
+            const int32_t run = static_cast<int32_t>((e >> 8) & 15);
+            if ((e & 15) != 0 && zig + run <= ze) {
+                r.take_ac(e);
+                zig += run;
+                b[kUnzig[zig]] = (static_cast<int32_t>(e) >> 16) << al;
+                nzpos[nnz++] = kUnzig[zig];
+                continue;
+            }
+        }
         uint8_t value;
         ZTRY(r.huffman(hac, value));
         const uint8_t v0r = value >> 4, v1 = value & 0x0f;
@@ -1376,11 +1479,18 @@ int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huf
     auto mag = [](int32_t v) { return v < 0 ? 0u - static_cast<uint32_t>(v) : static_cast<uint32_t>(v); };
     if (zig == 0) {
         zig++;
-        uint8_t t;
-        ZTRY(r.huffman(hdc, t));
-        if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
         int32_t delta;
-        ZTRY(r.receive_extend(t, delta));
+        uint32_t e = 0;
+        if constexpr (R::kAcFast) e = r.peek_ac(hdc); // (the DC difference in one lookup)
+        if (e & 15) {
+            r.take_ac(e);
+            delta = static_cast<int32_t>(e) >> 16;
+        } else {
+            uint8_t t;
+            ZTRY(r.huffman(hdc, t));
+            if (t > 16) return ZPX_E_EXCESSIVE_DC_COMPONENT;
+            ZTRY(r.receive_extend(t, delta));
+        }
         dcv += delta;
         const int32_t v = dcv << al;
         zz[0] = v;
@@ -1391,6 +1501,24 @@ int Decoder::first_block_pieces(R &r, const Scan &sc, const Huff &hdc, const Huf
         eob_run_--;
     } else {
         for (; zig <= ze; zig++) {
+            if constexpr (R::kAcFast) { // one lookup: code and magnitude bits (Huff::ac)
+                const uint32_t e = r.peek_ac(hac);
+                if (e & kAcEob) {
+                    r.take_ac(e);
+                    eob_run_ = 0; // (1 << 0) - 1
+                    break;
+                }
+                const int32_t run = static_cast<int32_t>((e >> 8) & 15);
+                if ((e & 15) != 0 && zig + run <= ze) {
+                    r.take_ac(e);
+                    zig += run;
+                    const int32_t v = (static_cast<int32_t>(e) >> 16) << al;
+                    zz[zig] = v;
+                    last = zig;
+                    m = std::max(m, mag(v));
+                    continue;
+                }
+            }
             uint8_t value;
             ZTRY(r.huffman(hac, value));
             const uint8_t v0r = value >> 4, v1 = value & 0x0f;
