@@ -1,0 +1,42 @@
+"""End-to-end batch (configs[3] on one GPU: the bench's 64 alternating 4K JPEG /
+tc8 PNG images) at several pipeline depths (slots = host tokens), rounds
+alternating, after one full-batch warm-up.
+Usage: python tools/e2e_depth_ab.py [rounds] [threads] [depth ...]  (0 = the default)"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT]
+
+import torch  # noqa: E402
+
+from tools import synthetic as S  # noqa: E402
+from zpix_amd import batch  # noqa: E402
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    threads = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    depths = [int(x) for x in sys.argv[3:]] or [0, 48]
+    W = H = 4096
+    uniq = {True: S.jpeg_420(0, W, H, 75), False: S.png_tc8_mixed(1, W, H)}
+    bufs = [uniq[i % 2 == 0] for i in range(64)]
+    arena = torch.empty(64 * W * H * 4, dtype=torch.uint8, device="cuda")
+    dst = [arena[i * W * H * 4:(i + 1) * W * H * 4].view(H, W, 4) for i in range(64)]
+    batch.decode_rgba(bufs, host_threads=threads, dst=dst)  # warm-up: the whole batch
+    torch.cuda.synchronize()
+    for r in range(rounds):
+        for dp in depths:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res, st = batch.decode_rgba(bufs, host_threads=threads, depth=dp, dst=dst, with_stats=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            assert all(x.status == "Ok" for x in res)
+            print(f"round {r} depth={dp}: wall {dt:.3f} s  {64 * W * H / dt / 1e6:7.1f} MPix/s  host {st.host_s:.2f} s "
+                  f"(jpeg {st.host_jpeg_s:.2f}, png {st.host_png_s:.2f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,7 @@
 tc8 PNG images, 16 host threads) from the pipeline's trace lines
 (ZPX_BATCH_TRACE=1, set here): run after a whole-batch warm-up; prints the
 per-worker busy spans and the dispatcher's events relative to the batch start.
-Usage: python tools/e2e_trace.py [threads] > timeline.txt 2> trace.log"""
+Usage: python tools/e2e_trace.py [threads] [depth] > timeline.txt 2> trace.log"""
 import os
 import sys
 import time
@@ -19,6 +19,7 @@ from zpix_amd import batch  # noqa: E402
 
 def main():
     threads = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    depth = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     W = H = 4096
     uniq = {True: S.jpeg_420(0, W, H, 75), False: S.png_tc8_mixed(1, W, H)}
     bufs = [uniq[i % 2 == 0] for i in range(64)]
@@ -29,7 +30,7 @@ def main():
     sys.stderr.flush()
     print(f"MARK {time.monotonic() * 1e3:.3f}", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    res, st = batch.decode_rgba(bufs, host_threads=threads, dst=dst, with_stats=True)
+    res, st = batch.decode_rgba(bufs, host_threads=threads, depth=depth, dst=dst, with_stats=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print(f"wall {dt:.3f} s  host {st.host_s:.2f} s (jpeg {st.host_jpeg_s:.2f}, png {st.host_png_s:.2f})", flush=True)
