@@ -151,6 +151,14 @@ int zpx_abi_version(void);
  * for the next batch to reuse with their pages -- and returns the bytes
  * released.  Safe at any time; buffers in use are not touched. */
 size_t zpx_host_pools_trim(void);
+/* Frees the batch pipeline's cached slots: zpx_batch_decode_rgba keeps a
+ * finished batch's slots (per device: their device buffers -- the largest
+ * image's input and coefficients, ~80 MB a slot for 4K -- events and pinned
+ * status words; at most 256 slots) for the next batch on the device, whose
+ * setup and teardown then allocate and free nothing.  Returns the device
+ * bytes released.  Safe at any time; slots of running batches are not
+ * touched. */
+size_t zpx_batch_cache_trim(void);
 /* Detail message of the last failure on this context (never NULL). */
 const char *zpx_last_error(const zpx_ctx *ctx);
 
@@ -660,7 +668,10 @@ int zpx_debug_shard_fake_comm(int on);
  *   "batch_makespan" 0: a batch worker pairs two PNGs whenever the batch
  *                 has items to spare (default 1: only while the pair's
  *                 estimated host time fits the batch's projected remaining
- *                 time per worker, so late PNGs run alone). */
+ *                 time per worker, so late PNGs run alone);
+ *   "batch_slot_cache" 0: every batch creates its slots and frees them at
+ *                 the end (default 1: reused from zpx_batch_cache_trim's
+ *                 cache). */
 int zpx_debug_option(const char *name, int value);
 /* Test hook: decodes a baseline 3-component interleaved JPEG into the
  * ZPX_COEFFS_PIECES form the batch pipeline uploads and

@@ -792,6 +792,12 @@ def test_host_entropy_progressive_parallel_matches_oracle():
                 assert np.array_equal(oc.grids[c], pc.grid(c).astype(np.int32)), (it, c)
 
 
+def test_batch_cache_trim_without_batches():
+    """zpx_batch_cache_trim with nothing cached (no batch has run in this
+    process without a GPU) returns 0 and touches no device."""
+    assert _lib.lib().zpx_batch_cache_trim() == 0
+
+
 def test_host_pools_trim():
     """zpx_host_pools_trim releases the host stages' recycled buffers: after
     a PNG parse the IDAT buffer is pooled (reused by the next parse with its

@@ -403,3 +403,29 @@ def test_batch_dense_coefficient_upload():
         check_results(bufs, batch.decode_rgba(bufs, host_threads=3))
     finally:
         _lib.lib().zpx_debug_option(b"jpeg_sparse", prev)
+
+
+def test_batch_slot_cache_reuse_and_trim():
+    """A finished batch's slots are cached per device and reused by the next
+    batch (zpx_batch_cache_trim frees them): the mixed batch decodes the same
+    with the cache off, through slots cached by a batch of other formats and
+    sizes (JPEG-only, then PNG-only, then the mix), and after a trim."""
+    L = _lib.lib()
+    bufs = mixed_buffers()
+    prev = L.zpx_debug_option(b"batch_slot_cache", 0)
+    try:
+        L.zpx_batch_cache_trim()
+        check_results(bufs, batch.decode_rgba(bufs, host_threads=3, depth=4))
+        assert L.zpx_batch_cache_trim() == 0  # (nothing cached with the switch off)
+        L.zpx_debug_option(b"batch_slot_cache", 1)
+        jpegs = [b for b in bufs if b[:2] == b"\xff\xd8"]
+        pngs = [b for b in bufs if b[:8] == b"\x89PNG\r\n\x1a\n"]
+        check_results(jpegs, batch.decode_rgba(jpegs, host_threads=2, depth=3))
+        check_results(pngs, batch.decode_rgba(pngs, host_threads=3, depth=5))  # 3 cached slots + 2 new
+        check_results(bufs, batch.decode_rgba(bufs, host_threads=3, depth=6))
+        check_results(bufs, batch.decode_rgba(bufs, host_threads=2, depth=2))
+        assert L.zpx_batch_cache_trim() > 0
+        assert L.zpx_batch_cache_trim() == 0
+        check_results(bufs, batch.decode_rgba(bufs, host_threads=3, depth=4))
+    finally:
+        L.zpx_debug_option(b"batch_slot_cache", prev)

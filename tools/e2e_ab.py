@@ -41,7 +41,7 @@ def main():
             dt = time.perf_counter() - t0
             L.zpx_debug_option(name, prev)
             assert all(x.status == "Ok" for x in res)
-            print(f"round {r} {name.decode()}={mode}: wall {dt:.3f} s  "
+            print(f"round {r} {name.decode()}={mode}: wall {dt:.3f} s (run loop {st.wall_s:.3f})  "
                   f"{64 * W * H / dt / 1e6:7.1f} MPix/s  host {st.host_s:.2f} s (jpeg {st.host_jpeg_s:.2f}, "
                   f"png {st.host_png_s:.2f})", flush=True)
 

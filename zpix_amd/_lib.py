@@ -166,6 +166,7 @@ EXPORTS = [
     "zpx_qoi_probe_buffer", "zpx_qoi_encode", "zpx_qoi_encode_bound", "zpx_qoi_encode_device",
     "zpx_debug_jpeg_sparse_grids", "zpx_debug_inflate_parallel", "zpx_debug_png_inflate_pair", "zpx_batch_wait_prefix",
     "zpx_debug_shard_fake_comm", "zpx_debug_option", "zpx_host_pools_trim",
+    "zpx_batch_cache_trim",
 ]
 
 _lib = None
@@ -183,6 +184,7 @@ def lib():
     sig = {
         "zpx_abi_version": (i32, []),
         "zpx_host_pools_trim": (sz, []),
+        "zpx_batch_cache_trim": (sz, []),
         "zpx_error_name": (C.c_char_p, [i32]),
         "zpx_last_error": (C.c_char_p, [vp]),
         "zpx_ctx_create": (i32, [i32, C.POINTER(vp)]),

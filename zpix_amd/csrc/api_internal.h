@@ -154,6 +154,10 @@ typedef void (*BatchDone)(void *user, int item);
 int batch_decode_rgba_hook(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
                            zpx_batch_stats *stats, BatchDone on_done, void *user);
 
+// batch.cpp: frees the batch pipeline's cached slots (zpx_batch_cache_trim);
+// returns their device bytes
+size_t batch_slot_cache_trim();
+
 // shard.cpp: destroy the cached gather communicators that include `device`
 // (zpx_ctx_destroy); a call still gathering on one finishes first
 void shard_release_comms(int device);

@@ -93,6 +93,40 @@ struct Slot {
 
 bool host_reserve(HostBuf &b, size_t n) { return b.bytes >= n || b.alloc(n, false); }
 
+void destroy_slot(Slot &s)
+{
+    if (s.ev_in) (void)hipEventDestroy(s.ev_in);
+    if (s.ev_kernel) (void)hipEventDestroy(s.ev_kernel);
+    if (s.ev_done) (void)hipEventDestroy(s.ev_done);
+    s.ev_in = s.ev_kernel = s.ev_done = nullptr;
+}
+
+size_t slot_bytes(const Slot &s)
+{
+    return s.din.bytes + s.dout.bytes + s.dimg.bytes + s.ddesc.bytes + s.dbound.bytes + s.dgrid.bytes + s.dstage.bytes +
+           s.dslab.bytes;
+}
+
+// The slots of finished batches, per device, for the next batch on it: a
+// batch's teardown freed ~3 x depth device buffers (hipFree unmaps them)
+// and its setup created 3 x depth events, ~9-11 ms outside the decode loop
+// of a 64 x 4K batch (~190 ms).  A slot is idle when it is cached (its
+// pipeline synchronised every stream) and keeps its device buffers, events,
+// pinned words and PNG epoch window; zpx_batch_cache_trim() frees them.
+// (Never destroyed at exit: the HIP runtime may be gone by then.)
+struct SlotCache {
+    static constexpr size_t kMaxSlots = 256;
+    static constexpr size_t kMaxBytes = size_t(32) << 30; // device bytes held at most
+    std::mutex mu;
+    size_t bytes = 0;
+    std::vector<std::pair<int, std::unique_ptr<Slot>>> slots; // (device, slot)
+};
+SlotCache &slot_cache()
+{
+    static SlotCache *c = new SlotCache;
+    return *c;
+}
+
 // test switch "jpeg_sparse" = 0: dense coefficient grids instead of pieces
 bool jpeg_sparse_upload() { return opt(Opt::JpegSparse) != 0; }
 
@@ -180,6 +214,7 @@ class Pipeline {
         return e;
     }
     std::vector<void *> retired_; // replaced slot buffers, freed by ~Pipeline
+    bool reusable_ = false;        // run() completed: its slots may go to the SlotCache
     void push_decoded(std::unique_ptr<Decoded> d, double dt);
     double host_s_ = 0, host_jpeg_s_ = 0, host_png_s_ = 0;
     int jpeg_items_ = 0, png_items_ = 0;
@@ -196,15 +231,24 @@ Pipeline::~Pipeline()
     cv_token_.notify_all();
     for (auto &t : workers_)
         if (t.joinable()) t.join();
-    (void)hipStreamSynchronize(ctx_->stream);
-    if (h2d_) (void)hipStreamSynchronize(h2d_);
-    if (d2h_) (void)hipStreamSynchronize(d2h_);
+    bool idle = hipStreamSynchronize(ctx_->stream) == hipSuccess;
+    if (h2d_) idle = hipStreamSynchronize(h2d_) == hipSuccess && idle;
+    if (d2h_) idle = hipStreamSynchronize(d2h_) == hipSuccess && idle;
     for (void *p : retired_) (void)hipFree(p);
-    for (auto &s : slots_) {
-        if (s->ev_in) (void)hipEventDestroy(s->ev_in);
-        if (s->ev_kernel) (void)hipEventDestroy(s->ev_kernel);
-        if (s->ev_done) (void)hipEventDestroy(s->ev_done);
+    if (reusable_ && idle && opt(Opt::BatchSlotCache)) {
+        SlotCache &c = slot_cache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        for (auto &sp : slots_) {
+            if (!sp || sp->busy || c.slots.size() >= SlotCache::kMaxSlots) continue;
+            const size_t b = slot_bytes(*sp);
+            if (c.bytes + b > SlotCache::kMaxBytes) continue;
+            sp->dec.reset();
+            c.bytes += b;
+            c.slots.emplace_back(ctx_->device, std::move(sp));
+        }
     }
+    for (auto &s : slots_)
+        if (s) destroy_slot(*s); // (not cached)
     if (h2d_) (void)hipStreamDestroy(h2d_);
     if (d2h_) (void)hipStreamDestroy(d2h_);
 }
@@ -435,7 +479,17 @@ int Pipeline::setup()
 {
     HIPCHK(ctx_, hipStreamCreateWithFlags(&h2d_, hipStreamNonBlocking));
     HIPCHK(ctx_, hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
-    for (int i = 0; i < depth_; i++) {
+    if (opt(Opt::BatchSlotCache)) { // the cached slots of this device first
+        SlotCache &c = slot_cache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        for (size_t k = c.slots.size(); k-- > 0 && int(slots_.size()) < depth_;)
+            if (c.slots[k].first == ctx_->device) {
+                c.bytes -= std::min(c.bytes, slot_bytes(*c.slots[k].second));
+                slots_.push_back(std::move(c.slots[k].second));
+                c.slots.erase(c.slots.begin() + static_cast<std::ptrdiff_t>(k));
+            }
+    }
+    for (int i = int(slots_.size()); i < depth_; i++) {
         std::unique_ptr<Slot> s(new Slot);
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming));
         HIPCHK(ctx_, hipEventCreateWithFlags(&s->ev_kernel, hipEventDisableTiming));
@@ -969,7 +1023,12 @@ int Pipeline::run(zpx_batch_stats *stats)
     cv_token_.notify_all();
     for (auto &t : workers_) t.join();
     workers_.clear();
-    for (int i = 0; i < n_; i++) failed_ += items_[i].status != ZPX_OK;
+    bool device_ok = true; // (a slot of an item that failed on the device is not reused)
+    for (int i = 0; i < n_; i++) {
+        failed_ += items_[i].status != ZPX_OK;
+        device_ok = device_ok && items_[i].status != ZPX_E_HIP;
+    }
+    reusable_ = rc == ZPX_OK && done == n_ && device_ok;
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->wall_s = now_s() - t0;
@@ -989,6 +1048,29 @@ int Pipeline::run(zpx_batch_stats *stats)
 }
 
 } // namespace
+
+size_t zpx::batch_slot_cache_trim()
+{
+    std::vector<std::pair<int, std::unique_ptr<Slot>>> out;
+    {
+        SlotCache &c = slot_cache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        out.swap(c.slots);
+        c.bytes = 0;
+    }
+    if (out.empty()) return 0;
+    size_t bytes = 0;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    for (auto &e : out) {
+        bytes += slot_bytes(*e.second);
+        (void)hipSetDevice(e.first);
+        destroy_slot(*e.second);
+        e.second.reset(); // (its buffers, pinned words and epoch window)
+    }
+    if (cur >= 0) (void)hipSetDevice(cur);
+    return bytes;
+}
 
 int zpx::batch_decode_rgba_hook(zpx_ctx *ctx, zpx_batch_item *items, int n_items, const zpx_batch_opts *opts,
                                 zpx_batch_stats *stats, BatchDone on_done, void *user)

@@ -6,7 +6,7 @@
 
 namespace zpx {
 
-enum class Opt { JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead, InflatePair, BatchMakespan, Count };
+enum class Opt { JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead, InflatePair, BatchMakespan, BatchSlotCache, Count };
 int opt(Opt o);
 
 } // namespace zpx

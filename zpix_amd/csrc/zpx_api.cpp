@@ -37,6 +37,7 @@ static const char *const kErrorNames[] = {
 
 extern "C" int zpx_abi_version(void) { return ZPX_ABI_VERSION; }
 extern "C" size_t zpx_host_pools_trim(void) { return zpx::png_pool_trim(); }
+extern "C" size_t zpx_batch_cache_trim(void) { return zpx::batch_slot_cache_trim(); }
 
 extern "C" const char *zpx_error_name(int code)
 {
@@ -1617,11 +1618,12 @@ static int zpx_debug_png_stall_impl(zpx_ctx *ctx, uint32_t spin_limit, double *s
 namespace zpx {
 namespace {
 // JpegStrip, JpegSparse, PngPair, QoiSegment, PngDeviceSlab, PngEpochCycle, ShardRcclSelf, BatchLookahead,
-// InflatePair, BatchMakespan
-std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}};
+// InflatePair, BatchMakespan, BatchSlotCache
+std::atomic<int> g_opt[static_cast<int>(Opt::Count)] = {{0}, {1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}, {1}};
 const char *const kOptNames[static_cast<int>(Opt::Count)] = {
     "jpeg_strip",      "jpeg_sparse",     "png_pair",        "qoi_segment",     "png_device_slab",
-    "png_epoch_cycle", "shard_rccl_self", "batch_lookahead", "inflate_pair",    "batch_makespan"};
+    "png_epoch_cycle", "shard_rccl_self", "batch_lookahead", "inflate_pair",    "batch_makespan",
+    "batch_slot_cache"};
 } // namespace
 int opt(Opt o) { return g_opt[static_cast<int>(o)].load(std::memory_order_relaxed); }
 } // namespace zpx
